@@ -1,0 +1,161 @@
+/*
+ * mdsx.h — C ABI of the MI355X-native MDS shard decoder (libmdsx.so).
+ *
+ * This is the drop-in boundary for ONE hot path of mosaicml/streaming: the per-sample MDS decode
+ * path under streaming/base (offsets-table scan, per-sample byte-range gather, per-column decode).
+ * Every entry point below names the reference interface it replaces (paths relative to the
+ * mosaicml/streaming repository root).
+ *
+ * Conventions
+ *   - Plain C: pointers, sizes, ints. No torch / HIP C++ types in signatures; `stream` is a
+ *     hipStream_t passed as void* (NULL = the default stream).
+ *   - The library NEVER allocates or frees device memory and keeps no pointer after a call returns.
+ *     The caller (the Python host layer, through the PyTorch caching allocator) owns the shard
+ *     batch buffer, the descriptor tables, every output buffer and the workspace.
+ *   - All device work is enqueued on `stream`; calls return once it is enqueued. Errors found by
+ *     the kernels (malformed shards) are written to the mdsx_status record at the start of the
+ *     workspace and read by the caller after the stream completes.
+ *   - Functions are reentrant. The only global state is a thread-local last-error string.
+ *
+ * Return codes: MDSX_OK (0) or a negative MDSX_E_* value; mdsx_last_error() gives the message.
+ */
+#ifndef MDSX_H_
+#define MDSX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- return / status codes ------------------------------------------------------------------ */
+#define MDSX_OK 0
+#define MDSX_E_ARG (-1)      /* bad argument (null pointer, size mismatch, too many columns)        */
+#define MDSX_E_ENCODING (-2) /* unsupported encoding string (encodings.py:697-714,770-772)      */
+#define MDSX_E_HEADER (-3)   /* shard header inconsistent: num_samples != index `samples`, offsets
+                                table past the file, offsets[N] != file size (mds/writer.py:133-144) */
+#define MDSX_E_BOUNDS (-4)   /* a sample or column byte range leaves its sample / shard
+                                (mds/reader.py:103-149 would slice short or raise)                 */
+#define MDSX_E_HIP (-5)      /* a HIP runtime call failed                                         */
+#define MDSX_E_CAPACITY (-6) /* a ragged output buffer is smaller than the bytes to be written     */
+#define MDSX_E_EMPTY (-7)    /* a sample has zero bytes: reference raises IndexError
+                                (mds/reader.py:145-148)                                            */
+
+/* ---- column kinds (what the device does with a column) -------------------------------------- */
+#define MDSX_KIND_FIXED 0 /* fixed-size column: int, uint8..float64, ndarray:<dtype>:<shape>.
+                             Output: row-major [rows, row_bytes] bytes (a dtype[rows, *shape]
+                             tensor). encodings.py:84-94,148-161,270-305,308-397                   */
+#define MDSX_KIND_BYTES 1 /* variable-size raw bytes (encodings.py:62-70). Also used for every
+                             encoding whose decoded value is a host Python object (pil, jpeg, png,
+                             list[*], jpeg_array, pkl, json, str_int/_float/_decimal,
+                             encodings.py:410-650): the device gathers the bytes, the host applies
+                             the reference semantics.                                               */
+#define MDSX_KIND_STR 2   /* variable-size UTF-8 text (encodings.py:73-81). Ragged bytes plus a
+                             per-row flag set where bytes.decode('utf-8') would raise.               */
+#define MDSX_KIND_NDARRAY 3 /* dynamic ndarray ('ndarray', 'ndarray:<dtype>'; encodings.py:97-305):
+                             ragged bytes of the whole encoded value (header + values); the host
+                             splits the small header.                                               */
+
+#define MDSX_MAX_COLUMNS 64
+
+typedef struct mdsx_plan mdsx_plan; /* opaque, host-side, immutable after creation               */
+
+/* One shard of a device batch. A batch is a single device buffer holding several shard files,
+ * each starting at a 256-byte-aligned `offset`, with at least MDSX_BATCH_PAD bytes of readable
+ * slack before the first and after the last shard. */
+typedef struct mdsx_shard_desc {
+  uint64_t offset;  /* byte offset of the shard file inside the batch buffer (multiple of 256)   */
+  uint64_t bytes;   /* shard file size: index.json raw_data.bytes                               */
+  uint64_t row0;    /* first output row of this shard in the batch                              */
+  uint32_t samples; /* index.json `samples` (checked against the file header)                   */
+  uint32_t tile0;   /* first tile of this shard in the batch's tile numbering                   */
+} mdsx_shard_desc;
+
+#define MDSX_BATCH_PAD 256
+
+/* Output of one column. Device pointers. */
+typedef struct mdsx_column_out {
+  void* data;         /* FIXED: rows*row_bytes bytes. var kinds: packed values (uint8)          */
+  int64_t* offsets;   /* var kinds: int64[rows + 1] byte offsets into data. NULL for FIXED      */
+  uint8_t* flags;     /* STR: uint8[rows], 1 = invalid UTF-8 (decode would raise). Else NULL     */
+  uint64_t capacity;  /* var kinds: bytes available at data (checked against the scanned total) */
+} mdsx_column_out;
+
+/* Error record at byte 0 of the workspace (zeroed by every scan/decode call). */
+typedef struct mdsx_status {
+  int32_t code;   /* 0 or the first MDSX_E_* found by a kernel                                  */
+  int32_t shard;  /* batch shard index of that error                                            */
+  int32_t row;    /* sample index inside the shard (-1: shard header)                           */
+  int32_t column; /* column index (-1: whole sample)                                            */
+} mdsx_status;
+
+/* ---- version / diagnostics ------------------------------------------------------------------ */
+const char* mdsx_version(void);
+const char* mdsx_last_error(void); /* thread-local message of the last failing call            */
+
+/* ---- plan: per-shard schema ------------------------------------------------------------------
+ * Replaces the per-sample encoding dispatch: mds_decode -> _get_coder (encodings.py:697-714,
+ * 760-773) and NDArray.from_str / _get_static_size (encodings.py:148-193), which the reference
+ * re-parses for every column of every sample. Built once per schema from the shard's index.json
+ * entry as read by MDSReader.from_json (mds/reader.py:59-86): column_encodings and column_sizes
+ * (sizes: a positive byte count for fixed columns; 0 or negative for variable columns, mirroring
+ * the `if size:` test of mds/reader.py:114). */
+int mdsx_plan_create(const char* const* encodings, const int64_t* column_sizes, int ncols,
+                     mdsx_plan** out);
+void mdsx_plan_destroy(mdsx_plan* plan);
+int mdsx_plan_num_columns(const mdsx_plan* plan);
+int mdsx_plan_num_var(const mdsx_plan* plan);
+/* Rows per tile for this schema (256, or 64 for very wide schemas). Tile t of shard s covers rows
+ * [(t - tile0) * tile_rows, ...) of that shard; a shard has ceil(samples / tile_rows) tiles. */
+int mdsx_plan_tile_rows(const mdsx_plan* plan);
+/* kind (MDSX_KIND_*), bytes per row for FIXED (0 for var), element size in bytes (dtype size;
+ * 1 for byte-like kinds). */
+int mdsx_plan_column(const mdsx_plan* plan, int col, int* kind, int64_t* row_bytes,
+                     int* elem_bytes);
+/* MDSReader.validate (mds/reader.py:88-101) + is_mds_encoding_safe (encodings.py:730-739):
+ * returns 1 if every column is safe ('pkl' is not), 0 otherwise. */
+int mdsx_plan_is_safe(const mdsx_plan* plan);
+
+/* ---- workspace ----------------------------------------------------------------------------- */
+/* Bytes of device workspace a scan/decode of `ntiles` tiles needs (status record + per-tile
+ * ragged-column sums). 256-byte aligned pointer expected. */
+uint64_t mdsx_workspace_bytes(const mdsx_plan* plan, uint32_t ntiles);
+
+/* ---- the hot path ---------------------------------------------------------------------------
+ * Pass 1. Resets the status record in the workspace (for an all-fixed plan that is all it
+ * does), then, for variable-size columns, replaces the per-sample head
+ * parse of MDSReader.decode_sample (mds/reader.py:111-118) and the offsets-table read of
+ * MDSReader.get_sample_data (mds/reader.py:128-149), over whole shards: reads offsets[] and every
+ * sample's u32 size head, checks the ranges, and writes, for every ragged column, the per-row
+ * byte offsets (outs[c].offsets, int64[rows+1]) and the column total (d_totals[v] for the v-th
+ * variable column, int64, device) so the caller can size the value buffers.
+ *   d_batch     : device batch buffer (shard files at desc.offset)
+ *   d_shards    : device array of nshards descriptors
+ *   d_tile_shard: device uint32[ntiles], the shard of each tile (tiles never cross shards;
+ *                 shard s owns tiles [tile0, tile0 + ceil(samples / tile_rows)))
+ *   total_rows  : rows of the batch (sum of samples); offsets[total_rows] receives the total
+ *   outs        : HOST array of plan->ncols column outputs (device pointers inside); only
+ *                 .offsets of variable columns is used by this pass
+ *   d_workspace : device scratch of mdsx_workspace_bytes(plan, ntiles) bytes
+ *   d_totals    : device int64[num_var] (may be NULL if the caller does not need the totals)  */
+int mdsx_scan_shards(const mdsx_plan* plan, const uint8_t* d_batch,
+                     const mdsx_shard_desc* d_shards, int nshards, const uint32_t* d_tile_shard,
+                     uint32_t ntiles, uint64_t total_rows, const mdsx_column_out* outs,
+                     void* d_workspace, int64_t* d_totals, void* stream);
+
+/* Pass 2. Replaces MDSReader.get_sample_data + decode_sample + mds_decode for every sample of
+ * every shard in the batch (mds/reader.py:103-149, encodings.py:62-397,760-773): gathers each
+ * column's bytes of every sample into its output (fixed columns as dtype rows, ragged columns as
+ * packed values at the offsets from pass 1) and flags invalid UTF-8 rows of str columns.
+ * mdsx_scan_shards must have run on the same stream with the same arguments and workspace
+ * (every plan: it resets the status record this pass reports into). */
+int mdsx_decode_shards(const mdsx_plan* plan, const uint8_t* d_batch,
+                       const mdsx_shard_desc* d_shards, int nshards, const uint32_t* d_tile_shard,
+                       uint32_t ntiles, uint64_t total_rows, const mdsx_column_out* outs,
+                       void* d_workspace, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MDSX_H_ */

@@ -1,0 +1,175 @@
+"""ctypes binding of libmdsx.so, the C ABI declared in ``include/mdsx.h``.
+
+The library is the product path: there is no CPU fallback. If it is missing or fails to load,
+every decode entry point raises :class:`NativeLibraryError`.
+
+This module imports torch before loading the library so that the HIP runtime torch ships
+(``libamdhip64.so.7``) is the one the library binds to: one runtime, one device context.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+import torch  # noqa: F401  (must be loaded before libmdsx.so, see module docstring)
+
+__all__ = [
+    'NativeLibraryError', 'MDSX_OK', 'MDSX_E_ARG', 'MDSX_E_ENCODING', 'MDSX_E_HEADER',
+    'MDSX_E_BOUNDS', 'MDSX_E_HIP', 'MDSX_E_CAPACITY', 'MDSX_E_EMPTY', 'KIND_FIXED', 'KIND_BYTES',
+    'KIND_STR', 'KIND_NDARRAY', 'ShardDesc', 'ColumnOut', 'Status', 'lib', 'lib_path',
+    'EXPORTED_SYMBOLS', 'raise_for_code'
+]
+
+MDSX_OK = 0
+MDSX_E_ARG = -1
+MDSX_E_ENCODING = -2
+MDSX_E_HEADER = -3
+MDSX_E_BOUNDS = -4
+MDSX_E_HIP = -5
+MDSX_E_CAPACITY = -6
+MDSX_E_EMPTY = -7
+
+KIND_FIXED = 0
+KIND_BYTES = 1
+KIND_STR = 2
+KIND_NDARRAY = 3
+
+MAX_COLUMNS = 64
+BATCH_PAD = 256
+
+# Every function include/mdsx.h declares (checked by tests/test_native_abi.py).
+EXPORTED_SYMBOLS = (
+    'mdsx_version',
+    'mdsx_last_error',
+    'mdsx_plan_create',
+    'mdsx_plan_destroy',
+    'mdsx_plan_num_columns',
+    'mdsx_plan_num_var',
+    'mdsx_plan_tile_rows',
+    'mdsx_plan_column',
+    'mdsx_plan_is_safe',
+    'mdsx_workspace_bytes',
+    'mdsx_scan_shards',
+    'mdsx_decode_shards',
+)
+
+
+class NativeLibraryError(RuntimeError):
+    """libmdsx.so is missing or could not be loaded (the decoder has no CPU fallback)."""
+
+
+class ShardDesc(ctypes.Structure):
+    """``mdsx_shard_desc``."""
+    _fields_ = [('offset', ctypes.c_uint64), ('bytes', ctypes.c_uint64), ('row0', ctypes.c_uint64),
+                ('samples', ctypes.c_uint32), ('tile0', ctypes.c_uint32)]
+
+
+class ColumnOut(ctypes.Structure):
+    """``mdsx_column_out``."""
+    _fields_ = [('data', ctypes.c_void_p), ('offsets', ctypes.c_void_p), ('flags', ctypes.c_void_p),
+                ('capacity', ctypes.c_uint64)]
+
+
+class Status(ctypes.Structure):
+    """``mdsx_status``."""
+    _fields_ = [('code', ctypes.c_int32), ('shard', ctypes.c_int32), ('row', ctypes.c_int32),
+                ('column', ctypes.c_int32)]
+
+
+assert ctypes.sizeof(ShardDesc) == 32
+assert ctypes.sizeof(ColumnOut) == 32
+
+_here = os.path.dirname(os.path.abspath(__file__))
+lib_path = os.path.join(_here, 'lib', 'libmdsx.so')
+
+_lock = threading.Lock()
+_lib: Optional[ctypes.CDLL] = None
+
+
+def _declare(handle: ctypes.CDLL) -> None:
+    c_int, c_u32, c_u64, vp = ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p
+    handle.mdsx_version.restype = ctypes.c_char_p
+    handle.mdsx_version.argtypes = []
+    handle.mdsx_last_error.restype = ctypes.c_char_p
+    handle.mdsx_last_error.argtypes = []
+    handle.mdsx_plan_create.restype = c_int
+    handle.mdsx_plan_create.argtypes = [
+        ctypes.POINTER(ctypes.c_char_p),
+        ctypes.POINTER(ctypes.c_int64), c_int,
+        ctypes.POINTER(vp)
+    ]
+    handle.mdsx_plan_destroy.restype = None
+    handle.mdsx_plan_destroy.argtypes = [vp]
+    for name in ('mdsx_plan_num_columns', 'mdsx_plan_num_var', 'mdsx_plan_tile_rows',
+                 'mdsx_plan_is_safe'):
+        fn = getattr(handle, name)
+        fn.restype = c_int
+        fn.argtypes = [vp]
+    handle.mdsx_plan_column.restype = c_int
+    handle.mdsx_plan_column.argtypes = [
+        vp, c_int,
+        ctypes.POINTER(c_int),
+        ctypes.POINTER(ctypes.c_int64),
+        ctypes.POINTER(c_int)
+    ]
+    handle.mdsx_workspace_bytes.restype = c_u64
+    handle.mdsx_workspace_bytes.argtypes = [vp, c_u32]
+    handle.mdsx_scan_shards.restype = c_int
+    handle.mdsx_scan_shards.argtypes = [
+        vp, vp, vp, c_int, vp, c_u32, c_u64,
+        ctypes.POINTER(ColumnOut), vp, vp, vp
+    ]
+    handle.mdsx_decode_shards.restype = c_int
+    handle.mdsx_decode_shards.argtypes = [
+        vp, vp, vp, c_int, vp, c_u32, c_u64,
+        ctypes.POINTER(ColumnOut), vp, vp
+    ]
+
+
+def lib() -> ctypes.CDLL:
+    """Load (once) and return libmdsx.so.
+
+    Raises:
+        NativeLibraryError: if the shared library is absent or cannot be loaded.
+    """
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(lib_path):
+                raise NativeLibraryError(
+                    f'libmdsx.so not found at {lib_path}: build it with '
+                    f'`python -c "import __graft_entry__ as g; g.build()"` '
+                    f'(or python -m streaming_amd.build). There is no CPU fallback.')
+            try:
+                handle = ctypes.CDLL(lib_path)
+            except OSError as e:
+                raise NativeLibraryError(f'failed to load {lib_path}: {e}') from e
+            _declare(handle)
+            _lib = handle
+    return _lib
+
+
+def last_error() -> str:
+    msg = lib().mdsx_last_error()
+    return msg.decode('utf-8', 'replace') if msg else ''
+
+
+def raise_for_code(code: int, where: str) -> None:
+    """Map an MDSX_E_* code to the exception type the reference raises for that condition."""
+    if code == MDSX_OK:
+        return
+    msg = f'{where}: {last_error()}'
+    if code == MDSX_E_ENCODING:
+        raise ValueError(msg)
+    if code == MDSX_E_ARG:
+        raise ValueError(msg)
+    if code == MDSX_E_EMPTY:
+        raise IndexError(msg)
+    if code in (MDSX_E_HEADER, MDSX_E_BOUNDS):
+        raise ValueError(msg)
+    raise RuntimeError(f'{msg} (mdsx code {code})')

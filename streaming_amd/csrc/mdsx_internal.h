@@ -1,0 +1,42 @@
+// Internal declarations shared by the host plan builder and the HIP kernels of libmdsx.so.
+#pragma once
+
+#include <cstdint>
+#include <string>
+
+#include "../../include/mdsx.h"
+
+namespace mdsx {
+
+// What the encoding string means (independent of the index's fixed/variable layout).
+enum Semantic : int {
+  SEM_BYTES = 0,          // 'bytes'
+  SEM_STR = 1,            // 'str'
+  SEM_SCALAR = 2,         // 'int', uint8..float64
+  SEM_NDARRAY_STATIC = 3, // 'ndarray:<dtype>:<shape>'
+  SEM_NDARRAY_DYN = 4,    // 'ndarray', 'ndarray:', 'ndarray:<dtype>'
+  SEM_HOST_OBJECT = 5,    // pil, jpeg, png, list[*], jpeg_array, pkl, json, str_* (host decode)
+};
+
+struct ColumnSpec {
+  std::string encoding;
+  int semantic = SEM_BYTES;
+  int kind = MDSX_KIND_BYTES;  // device layout class (from the index's column_sizes)
+  int64_t row_bytes = 0;       // fixed size from the index, 0 for variable columns
+  int64_t natural_size = -1;   // fixed size implied by the encoding, -1 if variable
+  int elem_bytes = 1;          // dtype itemsize (1 for byte-like)
+  int var_index = -1;          // position among the variable columns (head order), -1 if fixed
+};
+
+int fail(int code, const std::string& msg);
+
+}  // namespace mdsx
+
+struct mdsx_plan {
+  int ncols = 0;
+  int nvar = 0;
+  int tile_rows = 256;
+  int64_t fixed_sum = 0;
+  bool safe = true;
+  mdsx::ColumnSpec cols[MDSX_MAX_COLUMNS];
+};

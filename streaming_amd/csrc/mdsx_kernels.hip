@@ -1,0 +1,566 @@
+// MI355X (gfx950, CDNA4) kernels of the MDS shard decoder, and the C ABI entry points that
+// launch them (declared in include/mdsx.h).
+//
+// The reference decodes one sample per Python call: MDSReader.get_sample_data opens the shard,
+// seeks into the u32 offsets table, reads [begin, end) (streaming/base/format/mds/reader.py:128-149),
+// then decode_sample splits the columns with the u32 size head of the variable columns and calls
+// mds_decode per column (mds/reader.py:103-126, encodings.py:760-773). Here whole shards are
+// HBM-resident and decoded at once:
+//
+//   scan_tiles_kernel    one workgroup per tile of rows: offsets-table scan + u32 size heads ->
+//                        per-row lengths of every ragged column, block exclusive scan (wave64
+//                        shuffles + LDS), per-tile totals.                      (ragged plans only)
+//   scan_totals_kernel   one workgroup per ragged column: exclusive scan of the tile totals.
+//   decode_kernel        one workgroup per tile: per-row column boundaries into LDS, small fixed
+//                        columns gathered one row per lane, every other column copied one row per
+//                        wave with 16-byte aligned loads and stores: the source is realigned in
+//                        registers (v_alignbyte funnel over the neighbour lane's chunk), so HBM is
+//                        read and written in whole 1 KiB wave transactions whatever the byte
+//                        alignment of the sample. str columns are UTF-8 validated in the same pass.
+//
+// Every load stays inside [shard - 32, shard + bytes + 32): the batch buffer carries
+// MDSX_BATCH_PAD bytes of slack around its shards, and every sample range is checked against
+// the shard before it is touched.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+
+#include "mdsx_internal.h"
+
+namespace mdsx_kernels {
+
+constexpr int kBlock = 256;   // 4 waves
+constexpr int kUnroll = 4;    // 16-byte chunks in flight per lane in wave_copy (4 KiB per wave)
+constexpr int kSmallMax = 16; // fixed columns up to this many bytes: one row per lane
+
+struct DevCol {
+  void* data;
+  int64_t* offsets;
+  uint8_t* flags;
+  uint64_t capacity;
+  uint32_t row_bytes;
+  int16_t kind;
+  int16_t var_index;
+};
+
+struct DevArgs {
+  const uint8_t* batch;
+  const mdsx_shard_desc* shards;
+  const uint32_t* tile_shard;
+  mdsx_status* status;
+  int64_t* tile_total;   // [nvar][ntiles]
+  int64_t* tile_prefix;  // [nvar][ntiles]
+  int64_t* totals;       // [nvar] or null
+  uint64_t total_rows;
+  uint32_t ntiles;
+  int32_t nshards;
+  int32_t ncols;
+  int32_t nvar;
+  int32_t tile_rows;
+  int32_t pad_;
+  DevCol cols[MDSX_MAX_COLUMNS];
+};
+
+__device__ __forceinline__ uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t r) {
+  return __builtin_amdgcn_alignbyte(hi, lo, r);
+}
+
+__device__ __forceinline__ void report(mdsx_status* st, int code, int shard, int row, int col) {
+  if (atomicCAS(&st->code, 0, code) == 0) {
+    st->shard = shard;
+    st->row = row;
+    st->column = col;
+  }
+}
+
+// u32 at any byte address (reads the two aligned dwords that cover it).
+__device__ __forceinline__ uint32_t load_u32_any(const uint8_t* p) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uint64_t(3));
+  return alignbyte(q[1], q[0], uint32_t(a & 3));
+}
+
+// Per-shard facts shared by the scan and decode kernels.
+struct TileView {
+  const uint8_t* shard;
+  const uint32_t* offs;  // offsets table (absolute file offsets), 4-byte aligned
+  mdsx_shard_desc d;
+  uint32_t shard_idx;
+  uint32_t r0;     // first row (inside the shard) of this tile
+  uint32_t nrows;  // rows of this tile
+  uint64_t hdr_end;
+  bool table_ok;   // the offsets table of `samples` rows fits in the file
+};
+
+__device__ __forceinline__ TileView tile_view(const DevArgs& a) {
+  TileView v;
+  const uint32_t tile = blockIdx.x;
+  v.shard_idx = a.tile_shard[tile];
+  v.d = a.shards[v.shard_idx];
+  v.shard = a.batch + v.d.offset;
+  v.offs = reinterpret_cast<const uint32_t*>(v.shard + 4);
+  v.r0 = (tile - v.d.tile0) * uint32_t(a.tile_rows);
+  v.nrows = v.d.samples > v.r0 ? min(uint32_t(a.tile_rows), v.d.samples - v.r0) : 0u;
+  v.hdr_end = 4ull + 4ull * (uint64_t(v.d.samples) + 1ull);
+  v.table_ok = v.hdr_end <= v.d.bytes;
+  return v;
+}
+
+// Range of sample i of the shard (mds/reader.py:137-142) and its validity. A sample with zero
+// bytes is the reference's IndexError (mds/reader.py:145-148).
+__device__ __forceinline__ int sample_range(const TileView& v, uint32_t i, uint32_t* b,
+                                            uint32_t* e) {
+  *b = v.offs[i];
+  *e = v.offs[i + 1];
+  if (!(v.hdr_end <= *b && *b <= *e && *e <= v.d.bytes)) return MDSX_E_BOUNDS;
+  if (*b == *e) return MDSX_E_EMPTY;
+  return MDSX_OK;
+}
+
+// Exclusive scan over the 256 threads of the block; *total gets the block sum.
+__device__ __forceinline__ int64_t block_exclusive_scan(int64_t x, int64_t* s_wsum,
+                                                        int64_t* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t incl = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) s_wsum[w] = incl;
+  __syncthreads();
+  int64_t base = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < kBlock / 64; ++k) {
+    const int64_t s = s_wsum[k];
+    base += (k < w) ? s : 0;
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + incl - x;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Pass 1a: per-row ragged lengths -> local exclusive offsets + per-tile totals.
+__global__ __launch_bounds__(kBlock) void scan_tiles_kernel(const DevArgs a) {
+  __shared__ int64_t s_wsum[kBlock / 64];
+  const TileView v = tile_view(a);
+  const int t = threadIdx.x;
+  const uint32_t i = v.r0 + t;
+  const bool in_tile = v.table_ok && t < a.tile_rows && t < int(v.nrows);
+  uint32_t b = 0, e = 0;
+  bool ok = false;
+  if (in_tile) {
+    const int rc = sample_range(v, i, &b, &e);
+    ok = rc == MDSX_OK && uint64_t(b) + 4ull * a.nvar <= e;
+    if (ok) {  // the whole sample must hold its heads and columns; else emit zero lengths
+      uint64_t need = 4ull * a.nvar;
+      for (int c = 0; c < a.ncols; ++c) {
+        const DevCol& col = a.cols[c];
+        need += col.var_index >= 0 ? load_u32_any(v.shard + b + 4u * uint32_t(col.var_index))
+                                   : col.row_bytes;
+      }
+      ok = uint64_t(b) + need <= e;
+    }
+  }
+  for (int c = 0; c < a.ncols; ++c) {
+    const DevCol& col = a.cols[c];
+    if (col.var_index < 0) continue;
+    const int vi = col.var_index;
+    const int64_t len = ok ? int64_t(load_u32_any(v.shard + b + 4u * uint32_t(vi))) : 0;
+    int64_t total;
+    const int64_t excl = block_exclusive_scan(len, s_wsum, &total);
+    if (in_tile) col.offsets[v.d.row0 + i] = excl;
+    if (t == 0) a.tile_total[uint64_t(vi) * a.ntiles + blockIdx.x] = total;
+  }
+}
+
+// Pass 1b: exclusive scan of the tile totals of one ragged column (one workgroup per column).
+__global__ __launch_bounds__(kBlock) void scan_totals_kernel(const DevArgs a) {
+  __shared__ int64_t s_wsum[kBlock / 64];
+  const int vi = blockIdx.x;
+  const int64_t* in = a.tile_total + uint64_t(vi) * a.ntiles;
+  int64_t* out = a.tile_prefix + uint64_t(vi) * a.ntiles;
+  int64_t carry = 0;
+  for (uint32_t base = 0; base < a.ntiles; base += kBlock) {
+    const uint32_t k = base + threadIdx.x;
+    const int64_t x = k < a.ntiles ? in[k] : 0;
+    int64_t total;
+    const int64_t excl = block_exclusive_scan(x, s_wsum, &total);
+    if (k < a.ntiles) out[k] = carry + excl;
+    carry += total;
+  }
+  if (threadIdx.x == 0) {
+    if (a.totals) a.totals[vi] = carry;
+    for (int c = 0; c < a.ncols; ++c)
+      if (a.cols[c].var_index == vi) a.cols[c].offsets[a.total_rows] = carry;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Realignment: bytes [sh, sh + 16) of the 32-byte pair (lo, hi). sh is wave-uniform.
+__device__ __forceinline__ uint4 funnel16(const uint4 lo, const uint4 hi, uint32_t sh) {
+  const uint32_t r = sh & 3;
+  switch (sh >> 2) {
+    case 0:
+      return make_uint4(alignbyte(lo.y, lo.x, r), alignbyte(lo.z, lo.y, r),
+                        alignbyte(lo.w, lo.z, r), alignbyte(hi.x, lo.w, r));
+    case 1:
+      return make_uint4(alignbyte(lo.z, lo.y, r), alignbyte(lo.w, lo.z, r),
+                        alignbyte(hi.x, lo.w, r), alignbyte(hi.y, hi.x, r));
+    case 2:
+      return make_uint4(alignbyte(lo.w, lo.z, r), alignbyte(hi.x, lo.w, r),
+                        alignbyte(hi.y, hi.x, r), alignbyte(hi.z, hi.y, r));
+    default:
+      return make_uint4(alignbyte(hi.x, lo.w, r), alignbyte(hi.y, hi.x, r),
+                        alignbyte(hi.z, hi.y, r), alignbyte(hi.w, hi.z, r));
+  }
+}
+
+__device__ __forceinline__ uint32_t byte_of(const uint4& v, int j) {
+  const uint32_t w = (j < 4) ? v.x : (j < 8) ? v.y : (j < 12) ? v.z : v.w;
+  return (w >> (8 * (j & 3))) & 0xffu;
+}
+
+__device__ __forceinline__ uint4 shfl_down1(const uint4 v) {
+  return make_uint4(__shfl_down(v.x, 1), __shfl_down(v.y, 1), __shfl_down(v.z, 1),
+                    __shfl_down(v.w, 1));
+}
+
+__device__ __forceinline__ uint4 readlane0(const uint4 v) {
+  return make_uint4(__builtin_amdgcn_readlane(v.x, 0), __builtin_amdgcn_readlane(v.y, 0),
+                    __builtin_amdgcn_readlane(v.z, 0), __builtin_amdgcn_readlane(v.w, 0));
+}
+
+// Strict UTF-8 well-formedness (what bytes.decode('utf-8') accepts, encodings.py:80-81) of the
+// 16 bytes of `v` at segment positions pos0 .. pos0+15, given the 3 bytes before them in pw
+// (bytes 1..3 of the previous chunk's last dword). Bytes at negative positions are zero.
+__device__ __forceinline__ bool utf8_chunk_bad(const uint4 v, uint32_t pw, int64_t pos0,
+                                               int64_t len) {
+  uint32_t p1 = (pw >> 24) & 0xffu, p2 = (pw >> 16) & 0xffu, p3 = (pw >> 8) & 0xffu;
+  const bool ascii = ((v.x | v.y | v.z | v.w) & 0x80808080u) == 0;
+  if (ascii && p1 < 0xC0u && p2 < 0xE0u && p3 < 0xF0u) return false;
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t b = byte_of(v, j);
+    const int64_t pos = pos0 + j;
+    if (pos >= 0 && pos < len) {
+      const bool cont = (b & 0xC0u) == 0x80u;
+      const bool need = p1 >= 0xC0u || p2 >= 0xE0u || p3 >= 0xF0u;
+      bad |= cont != need;
+      bad |= b == 0xC0u || b == 0xC1u || b >= 0xF5u;
+      bad |= (p1 == 0xE0u && b < 0xA0u) || (p1 == 0xEDu && b > 0x9Fu) ||
+             (p1 == 0xF0u && b < 0x90u) || (p1 == 0xF4u && b > 0x8Fu);
+      bad |= (b >= 0xC0u && pos + 1 >= len) || (b >= 0xE0u && pos + 2 >= len) ||
+             (b >= 0xF0u && pos + 3 >= len);
+    }
+    p3 = p2;
+    p2 = p1;
+    p1 = b;
+  }
+  return bad;
+}
+
+// One wave copies `len` bytes from src to dst (any alignment of either). Destination chunks are
+// 16-byte aligned; lane k of a step owns chunk k. Its source bytes straddle two aligned 16-byte
+// source chunks: it loads the first and takes the second from lane k+1 (lane 63 from lane 0 of
+// the next step, or one extra load at the end of a batch). Partial chunks at the two ends are
+// written byte by byte. With kUtf8, returns whether the segment is not well-formed UTF-8
+// (wave-uniform).
+template <bool kUtf8>
+__device__ __forceinline__ bool wave_copy(const uint8_t* src, uint8_t* dst, uint64_t len,
+                                          int lane) {
+  if (len == 0) return false;
+  const uint64_t d0 = reinterpret_cast<uint64_t>(dst);
+  const uint64_t dend = d0 + len;
+  const uint64_t dbeg = d0 & ~uint64_t(15);
+  const uint64_t nchunks = (((dend + 15) & ~uint64_t(15)) - dbeg) >> 4;
+  const uint64_t sfirst = reinterpret_cast<uint64_t>(src) - (d0 - dbeg);
+  const uint32_t sh = uint32_t(sfirst & 15);
+  const uint4* sal = reinterpret_cast<const uint4*>(sfirst & ~uint64_t(15));
+  const uint64_t nload = nchunks + (sh ? 1 : 0);
+  bool bad = false;
+  uint32_t carry = 0;  // last dword of the previous chunk (UTF-8 look-back)
+  for (uint64_t base = 0; base < nchunks; base += 64 * kUnroll) {
+    uint4 lo[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const uint64_t k = base + uint64_t(u) * 64 + lane;
+      lo[u] = (k < nload) ? sal[k] : make_uint4(0, 0, 0, 0);
+    }
+    uint4 tail = make_uint4(0, 0, 0, 0);
+    if (sh != 0 && lane == 63) {
+      const uint64_t k = base + 64 * kUnroll;
+      if (k < nload) tail = sal[k];
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      if (base + uint64_t(u) * 64 >= nchunks) break;  // wave-uniform
+      const uint64_t k = base + uint64_t(u) * 64 + lane;
+      uint4 out = lo[u];
+      if (sh != 0) {
+        uint4 hi = shfl_down1(lo[u]);
+        const uint4 nxt = (u + 1 < kUnroll) ? readlane0(lo[u + 1 < kUnroll ? u + 1 : u]) : tail;
+        if (lane == 63) hi = nxt;
+        out = funnel16(lo[u], hi, sh);
+      }
+      const uint64_t D = dbeg + 16 * k;
+      if (kUtf8) {
+        uint4 vout = out;
+        if (k == 0 && D < d0) {  // zero the bytes before the segment start
+          const uint32_t head = uint32_t(d0 - D);
+          const uint32_t m0 = head >= 4 ? 0u : (0xffffffffu << (8 * head));
+          const uint32_t m1 = head >= 8 ? 0u : head <= 4 ? 0xffffffffu : (0xffffffffu << (8 * (head - 4)));
+          const uint32_t m2 = head >= 12 ? 0u : head <= 8 ? 0xffffffffu : (0xffffffffu << (8 * (head - 8)));
+          const uint32_t m3 = head <= 12 ? 0xffffffffu : (0xffffffffu << (8 * (head - 12)));
+          vout = make_uint4(vout.x & m0, vout.y & m1, vout.z & m2, vout.w & m3);
+        }
+        uint32_t pw = __shfl_up(vout.w, 1);
+        if (lane == 0) pw = carry;
+        carry = __shfl(vout.w, 63);
+        if (k < nchunks) bad |= utf8_chunk_bad(vout, pw, int64_t(D) - int64_t(d0), int64_t(len));
+      }
+      if (k < nchunks) {
+        if (D >= d0 && D + 16 <= dend) {
+          *reinterpret_cast<uint4*>(D) = out;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const uint64_t A = D + j;
+            if (A >= d0 && A < dend) *reinterpret_cast<uint8_t*>(A) = uint8_t(byte_of(out, j));
+          }
+        }
+      }
+    }
+  }
+  if (kUtf8) return __any(bad);
+  return false;
+}
+
+// Fixed column of 1..16 bytes: one row per lane. dst is aligned to the largest power of two
+// dividing the row size (outputs are 256-byte aligned tensors).
+__device__ __forceinline__ void gather_small(const uint8_t* p, uint8_t* dst, uint32_t size) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uint64_t(3));
+  const uint32_t r = uint32_t(a & 3);
+  const uint32_t nd = (size + 6) >> 2;  // dwords covering r + size bytes for any r <= 3
+  const uint32_t w0 = q[0];
+  const uint32_t w1 = nd > 1 ? q[1] : 0u;
+  const uint32_t w2 = nd > 2 ? q[2] : 0u;
+  const uint32_t w3 = nd > 3 ? q[3] : 0u;
+  const uint32_t w4 = nd > 4 ? q[4] : 0u;
+  const uint4 o = make_uint4(alignbyte(w1, w0, r), alignbyte(w2, w1, r), alignbyte(w3, w2, r),
+                             alignbyte(w4, w3, r));
+  switch (size) {
+    case 1: *dst = uint8_t(o.x); break;
+    case 2: *reinterpret_cast<uint16_t*>(dst) = uint16_t(o.x); break;
+    case 4: *reinterpret_cast<uint32_t*>(dst) = o.x; break;
+    case 8: *reinterpret_cast<uint2*>(dst) = make_uint2(o.x, o.y); break;
+    case 12:
+      reinterpret_cast<uint32_t*>(dst)[0] = o.x;
+      reinterpret_cast<uint32_t*>(dst)[1] = o.y;
+      reinterpret_cast<uint32_t*>(dst)[2] = o.z;
+      break;
+    case 16: *reinterpret_cast<uint4*>(dst) = o; break;
+    default:
+      for (uint32_t j = 0; j < size; ++j) dst[j] = uint8_t(byte_of(o, int(j)));
+  }
+}
+
+// Pass 2: decode every column of every row of a tile.
+__global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int TR = a.tile_rows;
+  uint64_t* s_vdst = reinterpret_cast<uint64_t*>(smem);       // [nvar][TR] destination offsets
+  uint32_t* s_src = reinterpret_cast<uint32_t*>(s_vdst + a.nvar * TR);  // [ncols][TR] src offsets
+  uint32_t* s_vlen = s_src + a.ncols * TR;                      // [nvar][TR] ragged lengths
+  uint8_t* s_ok = reinterpret_cast<uint8_t*>(s_vlen + a.nvar * TR);     // [TR]
+
+  const TileView v = tile_view(a);
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6;
+
+  if (!v.table_ok) {
+    if (t == 0 && blockIdx.x == v.d.tile0) report(a.status, MDSX_E_HEADER, v.shard_idx, -1, -1);
+    return;  // block-uniform
+  }
+  if (t == 0 && blockIdx.x == v.d.tile0) {
+    // Header written by encode_joint_shard (mds/writer.py:133-144): u32 N, then N+1 offsets.
+    const uint32_t n = *reinterpret_cast<const uint32_t*>(v.shard);
+    const uint32_t first = v.offs[0];
+    if (n != v.d.samples || first < v.hdr_end || v.offs[v.d.samples] > v.d.bytes)
+      report(a.status, MDSX_E_HEADER, v.shard_idx, -1, -1);
+  }
+
+  // ---- column boundaries of this lane's row (MDSReader.decode_sample, mds/reader.py:111-125)
+  if (t < int(v.nrows)) {
+    const uint32_t i = v.r0 + t;
+    const uint64_t row = v.d.row0 + i;
+    uint32_t b = 0, e = 0;
+    int rc = sample_range(v, i, &b, &e);
+    bool ok = rc == MDSX_OK;
+    if (ok && uint64_t(b) + 4ull * a.nvar > e) {
+      ok = false;
+      rc = MDSX_E_BOUNDS;
+    }
+    uint64_t pos = uint64_t(b) + 4ull * a.nvar;
+    for (int c = 0; c < a.ncols; ++c) {
+      const DevCol& col = a.cols[c];
+      uint64_t len = col.row_bytes;
+      if (col.var_index >= 0) {
+        len = ok ? load_u32_any(v.shard + b + 4u * uint32_t(col.var_index)) : 0u;
+        const int64_t off = a.tile_prefix[uint64_t(col.var_index) * a.ntiles + blockIdx.x] +
+                            col.offsets[row];
+        col.offsets[row] = off;
+        s_vdst[col.var_index * TR + t] = uint64_t(off);
+        if (ok && uint64_t(off) + len > col.capacity) {
+          report(a.status, MDSX_E_CAPACITY, v.shard_idx, int(i), c);
+          ok = false;
+        }
+        s_vlen[col.var_index * TR + t] = uint32_t(len);
+      }
+      s_src[c * TR + t] = uint32_t(pos);
+      pos += len;
+    }
+    if (ok && pos > e) {
+      ok = false;
+      rc = MDSX_E_BOUNDS;
+    }
+    if (!ok && rc != MDSX_OK) report(a.status, rc, v.shard_idx, int(i), -1);
+    s_ok[t] = ok ? 1 : 0;
+  }
+  __syncthreads();
+
+  // ---- small fixed columns: one row per lane
+  if (t < int(v.nrows) && s_ok[t]) {
+    const uint64_t row = v.d.row0 + v.r0 + t;
+    for (int c = 0; c < a.ncols; ++c) {
+      const DevCol& col = a.cols[c];
+      if (col.var_index >= 0 || col.row_bytes > uint32_t(kSmallMax)) continue;
+      gather_small(v.shard + s_src[c * TR + t],
+                   static_cast<uint8_t*>(col.data) + row * col.row_bytes, col.row_bytes);
+    }
+  }
+
+  // ---- large fixed and ragged columns: one row per wave
+  for (int r = wave; r < int(v.nrows); r += kBlock / 64) {
+    if (!s_ok[r]) continue;  // wave-uniform
+    const uint64_t row = v.d.row0 + v.r0 + r;
+    for (int c = 0; c < a.ncols; ++c) {
+      const DevCol& col = a.cols[c];
+      const uint8_t* src = v.shard + s_src[c * TR + r];
+      if (col.var_index < 0) {
+        if (col.row_bytes <= uint32_t(kSmallMax)) continue;
+        wave_copy<false>(src, static_cast<uint8_t*>(col.data) + row * col.row_bytes,
+                         col.row_bytes, lane);
+      } else {
+        const int vi = col.var_index;
+        uint8_t* dst = static_cast<uint8_t*>(col.data) + s_vdst[vi * TR + r];
+        const uint64_t len = s_vlen[vi * TR + r];
+        if (col.kind == MDSX_KIND_STR) {
+          const bool bad = wave_copy<true>(src, dst, len, lane);
+          if (lane == 0 && col.flags) col.flags[row] = bad ? 1 : 0;
+        } else {
+          wave_copy<false>(src, dst, len, lane);
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+int build_args(const mdsx_plan* plan, const uint8_t* d_batch, const mdsx_shard_desc* d_shards,
+               int nshards, const uint32_t* d_tile_shard, uint32_t ntiles,
+               const mdsx_column_out* outs, void* d_workspace, int64_t* d_totals,
+               DevArgs* a) {
+  if (!plan || !d_batch || !d_shards || !d_tile_shard || !d_workspace || nshards <= 0)
+    return mdsx::fail(MDSX_E_ARG, "mdsx: null argument or empty batch");
+  if (plan->ncols > 0 && !outs) return mdsx::fail(MDSX_E_ARG, "mdsx: outs is NULL");
+  std::memset(a, 0, sizeof(*a));
+  a->batch = d_batch;
+  a->shards = d_shards;
+  a->tile_shard = d_tile_shard;
+  uint8_t* ws = static_cast<uint8_t*>(d_workspace);
+  a->status = reinterpret_cast<mdsx_status*>(ws);
+  a->tile_total = reinterpret_cast<int64_t*>(ws + 256);
+  a->tile_prefix = a->tile_total + uint64_t(plan->nvar) * ntiles;
+  a->totals = d_totals;
+  a->ntiles = ntiles;
+  a->nshards = nshards;
+  a->ncols = plan->ncols;
+  a->nvar = plan->nvar;
+  a->tile_rows = plan->tile_rows;
+  for (int c = 0; c < plan->ncols; ++c) {
+    const mdsx::ColumnSpec& s = plan->cols[c];
+    DevCol& d = a->cols[c];
+    d.data = outs[c].data;
+    d.offsets = outs[c].offsets;
+    d.flags = outs[c].flags;
+    d.capacity = outs[c].capacity;
+    d.row_bytes = uint32_t(s.row_bytes);
+    d.kind = int16_t(s.kind);
+    d.var_index = int16_t(s.var_index);
+    if (s.kind == MDSX_KIND_FIXED) {
+      if (!d.data) return mdsx::fail(MDSX_E_ARG, "mdsx: null data pointer for a fixed column");
+    } else {
+      if (!d.offsets || (!d.data && d.capacity > 0))
+        return mdsx::fail(MDSX_E_ARG, "mdsx: null offsets/data for a ragged column");
+    }
+  }
+  return MDSX_OK;
+}
+
+int hip_check(hipError_t e, const char* what) {
+  if (e == hipSuccess) return MDSX_OK;
+  return mdsx::fail(MDSX_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+}  // namespace mdsx_kernels
+
+using namespace mdsx_kernels;
+
+extern "C" {
+
+int mdsx_scan_shards(const mdsx_plan* plan, const uint8_t* d_batch,
+                     const mdsx_shard_desc* d_shards, int nshards, const uint32_t* d_tile_shard,
+                     uint32_t ntiles, uint64_t total_rows, const mdsx_column_out* outs,
+                     void* d_workspace, int64_t* d_totals, void* stream) {
+  DevArgs a;
+  int rc = build_args(plan, d_batch, d_shards, nshards, d_tile_shard, ntiles, outs, d_workspace,
+                      d_totals, &a);
+  if (rc != MDSX_OK) return rc;
+  a.total_rows = total_rows;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  rc = hip_check(hipMemsetAsync(d_workspace, 0, sizeof(mdsx_status), s), "hipMemsetAsync");
+  if (rc != MDSX_OK || plan->nvar == 0) return rc;
+  if (ntiles > 0) {
+    hipLaunchKernelGGL(scan_tiles_kernel, dim3(ntiles), dim3(kBlock), 0, s, a);
+    rc = hip_check(hipGetLastError(), "scan_tiles_kernel launch");
+    if (rc != MDSX_OK) return rc;
+  }
+  hipLaunchKernelGGL(scan_totals_kernel, dim3(plan->nvar), dim3(kBlock), 0, s, a);
+  return hip_check(hipGetLastError(), "scan_totals_kernel launch");
+}
+
+int mdsx_decode_shards(const mdsx_plan* plan, const uint8_t* d_batch,
+                       const mdsx_shard_desc* d_shards, int nshards, const uint32_t* d_tile_shard,
+                       uint32_t ntiles, uint64_t total_rows, const mdsx_column_out* outs,
+                       void* d_workspace, void* stream) {
+  DevArgs a;
+  int rc = build_args(plan, d_batch, d_shards, nshards, d_tile_shard, ntiles, outs, d_workspace,
+                      nullptr, &a);
+  if (rc != MDSX_OK) return rc;
+  a.total_rows = total_rows;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (ntiles == 0) return MDSX_OK;
+  const size_t lds = size_t(plan->tile_rows) *
+                         (8 * size_t(plan->nvar) + 4 * size_t(plan->ncols) + 4 * size_t(plan->nvar) + 1) +
+                     16;
+  hipLaunchKernelGGL(decode_kernel, dim3(ntiles), dim3(kBlock), lds, s, a);
+  return hip_check(hipGetLastError(), "decode_kernel launch");
+}
+
+}  // extern "C"

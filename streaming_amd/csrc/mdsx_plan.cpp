@@ -1,0 +1,268 @@
+// Host-side schema plan for the MDS decoder (part of libmdsx.so).
+//
+// Replaces the per-sample encoding dispatch of the reference: mds_decode -> _get_coder
+// (streaming/base/format/mds/encodings.py:697-714,760-773), NDArray.from_str and
+// _get_static_size (encodings.py:148-193) and the fixed/variable column split that
+// MDSReader.decode_sample does per sample (mds/reader.py:111-118). The reference re-parses the
+// encoding string for every column of every sample; here it is parsed once per schema.
+#include <cctype>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "mdsx_internal.h"
+
+namespace mdsx {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+namespace {
+
+// NDArray._int2value_dtype values (encodings.py:131-143) -> itemsize.
+int value_dtype_size(const std::string& name) {
+  if (name == "uint8" || name == "int8") return 1;
+  if (name == "uint16" || name == "int16" || name == "float16") return 2;
+  if (name == "uint32" || name == "int32" || name == "float32") return 4;
+  if (name == "uint64" || name == "int64" || name == "float64") return 8;
+  return 0;
+}
+
+std::string strip(const std::string& s) {
+  size_t b = 0, e = s.size();
+  while (b < e && std::isspace(static_cast<unsigned char>(s[b]))) ++b;
+  while (e > b && std::isspace(static_cast<unsigned char>(s[e - 1]))) --e;
+  return s.substr(b, e - b);
+}
+
+// Python int(str) for a decimal literal: optional sign, digits, single '_' between digits.
+bool parse_py_int(const std::string& text, int64_t* out) {
+  std::string s = strip(text);
+  if (s.empty()) return false;
+  size_t i = 0;
+  bool neg = false;
+  if (s[0] == '+' || s[0] == '-') {
+    neg = s[0] == '-';
+    i = 1;
+  }
+  if (i >= s.size()) return false;
+  int64_t v = 0;
+  bool prev_digit = false;
+  for (; i < s.size(); ++i) {
+    char c = s[i];
+    if (c == '_') {
+      if (!prev_digit || i + 1 >= s.size() || !std::isdigit(static_cast<unsigned char>(s[i + 1])))
+        return false;
+      prev_digit = false;
+      continue;
+    }
+    if (!std::isdigit(static_cast<unsigned char>(c))) return false;
+    if (v > (INT64_MAX - 9) / 10) return false;
+    v = v * 10 + (c - '0');
+    prev_digit = true;
+  }
+  *out = neg ? -v : v;
+  return true;
+}
+
+std::vector<std::string> split(const std::string& s, char sep) {
+  std::vector<std::string> parts;
+  size_t start = 0;
+  for (;;) {
+    size_t p = s.find(sep, start);
+    if (p == std::string::npos) {
+      parts.push_back(s.substr(start));
+      return parts;
+    }
+    parts.push_back(s.substr(start, p - start));
+    start = p + 1;
+  }
+}
+
+// Encodings whose decoded value is a host Python object (encodings.py:410-650). The device
+// gathers their bytes; the host applies the reference semantics.
+bool is_host_object_encoding(const std::string& name) {
+  static const char* kNames[] = {"str_int", "str_float", "str_decimal", "pil",       "jpeg",
+                                 "jpeg_array", "jpegarray", "png",       "list[pil]", "list[jpeg]",
+                                 "list[png]", "pkl",       "json"};
+  for (const char* n : kNames)
+    if (name == n) return true;
+  return false;
+}
+
+// Mirrors _get_coder (encodings.py:697-714): returns MDSX_OK and fills the column's natural
+// encoding facts, or MDSX_E_ENCODING where the reference returns None or raises.
+int parse_encoding(const std::string& enc, ColumnSpec* c) {
+  size_t colon = enc.find(':');
+  c->natural_size = -1;
+  c->elem_bytes = 1;
+  if (colon == std::string::npos) {
+    if (enc == "bytes") {
+      c->semantic = SEM_BYTES;
+      return MDSX_OK;
+    }
+    if (enc == "str") {
+      c->semantic = SEM_STR;
+      return MDSX_OK;
+    }
+    if (enc == "int") {  // Int: int64 (encodings.py:84-94)
+      c->semantic = SEM_SCALAR;
+      c->natural_size = 8;
+      c->elem_bytes = 8;
+      return MDSX_OK;
+    }
+    if (enc == "ndarray") {  // dynamic dtype + shape
+      c->semantic = SEM_NDARRAY_DYN;
+      return MDSX_OK;
+    }
+    int sz = value_dtype_size(enc);
+    if (sz) {  // Scalar family (encodings.py:308-397)
+      c->semantic = SEM_SCALAR;
+      c->natural_size = sz;
+      c->elem_bytes = sz;
+      return MDSX_OK;
+    }
+    if (is_host_object_encoding(enc)) {
+      c->semantic = SEM_HOST_OBJECT;
+      return MDSX_OK;
+    }
+    return fail(MDSX_E_ENCODING, "Unsupported encoding: " + enc + ".");
+  }
+  std::string name = enc.substr(0, colon);
+  std::string config = enc.substr(colon + 1);
+  if (name != "ndarray")  // only NDArray has from_str (encodings.py:173-193)
+    return fail(MDSX_E_ENCODING, "Unsupported encoding: " + enc + ".");
+  std::vector<std::string> args;
+  if (!config.empty()) args = split(config, ':');
+  if (args.size() > 2) return fail(MDSX_E_ENCODING, "Unsupported encoding: " + enc + ".");
+  if (args.empty()) {
+    c->semantic = SEM_NDARRAY_DYN;
+    return MDSX_OK;
+  }
+  int sz = value_dtype_size(args[0]);
+  if (!sz) return fail(MDSX_E_ENCODING, "Unsupported ndarray dtype in encoding: " + enc + ".");
+  c->elem_bytes = sz;
+  if (args.size() == 1) {  // static dtype, dynamic shape
+    c->semantic = SEM_NDARRAY_DYN;
+    return MDSX_OK;
+  }
+  int64_t count = 1;
+  for (const std::string& d : split(args[1], ',')) {
+    int64_t v = 0;
+    if (!parse_py_int(d, &v) || v < 1)
+      return fail(MDSX_E_ENCODING, "Bad ndarray shape in encoding: " + enc + ".");
+    if (count > (int64_t(1) << 40) / v)
+      return fail(MDSX_E_ENCODING, "ndarray shape too large in encoding: " + enc + ".");
+    count *= v;
+  }
+  c->semantic = SEM_NDARRAY_STATIC;
+  c->natural_size = count * sz;
+  return MDSX_OK;
+}
+
+}  // namespace
+}  // namespace mdsx
+
+using namespace mdsx;
+
+extern "C" {
+
+const char* mdsx_last_error(void) { return g_last_error.c_str(); }
+
+const char* mdsx_version(void) { return "mdsx 0.1.0 (gfx950)"; }
+
+int mdsx_plan_create(const char* const* encodings, const int64_t* column_sizes, int ncols,
+                     mdsx_plan** out) {
+  if (!out) return fail(MDSX_E_ARG, "mdsx_plan_create: out is NULL");
+  *out = nullptr;
+  if (ncols < 0 || ncols > MDSX_MAX_COLUMNS)
+    return fail(MDSX_E_ARG, "mdsx_plan_create: ncols must be in [0, 64]");
+  if (ncols > 0 && (!encodings || !column_sizes))
+    return fail(MDSX_E_ARG, "mdsx_plan_create: null encodings or column_sizes");
+  mdsx_plan* p = new (std::nothrow) mdsx_plan();
+  if (!p) return fail(MDSX_E_ARG, "mdsx_plan_create: out of host memory");
+  p->ncols = ncols;
+  p->nvar = 0;
+  p->fixed_sum = 0;
+  p->safe = true;
+  for (int i = 0; i < ncols; ++i) {
+    ColumnSpec& c = p->cols[i];
+    if (!encodings[i]) {
+      delete p;
+      return fail(MDSX_E_ARG, "mdsx_plan_create: null encoding string");
+    }
+    c.encoding = encodings[i];
+    int rc = parse_encoding(c.encoding, &c);
+    if (rc != MDSX_OK) {
+      delete p;
+      return rc;
+    }
+    if (c.encoding == "pkl") p->safe = false;  // _unsafe_encodings (encodings.py:685)
+    // Layout follows the index's column_sizes exactly as MDSReader.decode_sample does
+    // (`if size:` at mds/reader.py:114): a truthy size is a fixed column, anything else reads a
+    // u32 size from the sample head.
+    int64_t size = column_sizes[i];
+    if (size > 0) {
+      if (size >= (int64_t(1) << 32)) {
+        delete p;
+        return fail(MDSX_E_ENCODING, "column size past the u32 shard offset range");
+      }
+      c.kind = MDSX_KIND_FIXED;
+      c.row_bytes = size;
+      c.var_index = -1;
+      p->fixed_sum += size;
+    } else {
+      c.row_bytes = 0;
+      c.var_index = p->nvar++;
+      if (c.semantic == SEM_STR)
+        c.kind = MDSX_KIND_STR;
+      else if (c.semantic == SEM_NDARRAY_DYN)
+        c.kind = MDSX_KIND_NDARRAY;
+      else
+        c.kind = MDSX_KIND_BYTES;
+    }
+  }
+  // LDS per tile: a u32 source offset per (row, column), and for each ragged column a u32 length
+  // and a u64 destination offset per row. Wide schemas get a smaller tile.
+  int64_t per_row = 4 * int64_t(ncols) + 12 * int64_t(p->nvar);
+  p->tile_rows = (per_row * 256 <= 48 * 1024) ? 256 : 64;
+  *out = p;
+  return MDSX_OK;
+}
+
+void mdsx_plan_destroy(mdsx_plan* plan) { delete plan; }
+
+int mdsx_plan_num_columns(const mdsx_plan* plan) { return plan ? plan->ncols : MDSX_E_ARG; }
+
+int mdsx_plan_num_var(const mdsx_plan* plan) { return plan ? plan->nvar : MDSX_E_ARG; }
+
+int mdsx_plan_tile_rows(const mdsx_plan* plan) { return plan ? plan->tile_rows : MDSX_E_ARG; }
+
+int mdsx_plan_column(const mdsx_plan* plan, int col, int* kind, int64_t* row_bytes,
+                     int* elem_bytes) {
+  if (!plan || col < 0 || col >= plan->ncols)
+    return fail(MDSX_E_ARG, "mdsx_plan_column: bad plan or column");
+  const ColumnSpec& c = plan->cols[col];
+  if (kind) *kind = c.kind;
+  if (row_bytes) *row_bytes = c.row_bytes;
+  if (elem_bytes) *elem_bytes = c.elem_bytes;
+  return MDSX_OK;
+}
+
+int mdsx_plan_is_safe(const mdsx_plan* plan) { return plan && plan->safe ? 1 : 0; }
+
+uint64_t mdsx_workspace_bytes(const mdsx_plan* plan, uint32_t ntiles) {
+  if (!plan) return 0;
+  // [status: 256 B][tile totals: nvar * ntiles * 8][tile prefixes: nvar * ntiles * 8]
+  uint64_t per = uint64_t(plan->nvar) * ntiles * 8;
+  return 256 + ((2 * per + 255) & ~uint64_t(255));
+}
+
+}  // extern "C"

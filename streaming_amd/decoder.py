@@ -1,0 +1,465 @@
+"""Whole-shard device decode: plans, device shard batches and decoded columns.
+
+This is the host side of the hot path. It replaces, for whole shards at once, the per-sample
+chain ``Reader.get_item -> MDSReader.get_sample_data -> MDSReader.decode_sample -> mds_decode``
+(``streaming/base/format/base/reader.py:310-320``, ``format/mds/reader.py:103-149``,
+``format/mds/encodings.py:760-773``):
+
+* :class:`Plan` -- the schema of a shard (``MDSReader.from_json``, ``mds/reader.py:59-86``),
+  compiled once by ``mdsx_plan_create``;
+* :class:`DeviceBatch` -- one or more shard files staged in a single HBM buffer
+  (``mdsx_shard_desc`` table + tile table);
+* :func:`decode_batch` / :class:`BatchDecoder` -- ``mdsx_scan_shards`` + ``mdsx_decode_shards``
+  on the current torch stream, giving torch tensors: fixed columns as ``dtype[rows, *shape]``,
+  ragged columns (bytes / str / dynamic ndarray / host-object encodings) as
+  :class:`RaggedColumn` (packed ``uint8`` values + ``int64`` offsets [+ str validity flags]).
+
+Every decode goes through libmdsx.so; there is no CPU path.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass, field
+from typing import Optional, Sequence, Union
+
+import numpy as np
+import torch
+
+from streaming_amd import _native
+from streaming_amd._native import (BATCH_PAD, KIND_BYTES, KIND_FIXED, KIND_NDARRAY, KIND_STR,
+                                   ColumnOut, ShardDesc)
+from streaming_amd.encodings import EncodingInfo, parse_encoding
+
+__all__ = [
+    'Plan', 'DeviceBatch', 'RaggedColumn', 'DecodedBatch', 'BatchDecoder', 'decode_batch',
+    'make_batch', 'stage_shards', 'torch_dtype', 'output_bytes'
+]
+
+_TORCH_DTYPES = {
+    'uint8': torch.uint8,
+    'int8': torch.int8,
+    'uint16': torch.uint16,
+    'int16': torch.int16,
+    'float16': torch.float16,
+    'uint32': torch.uint32,
+    'int32': torch.int32,
+    'float32': torch.float32,
+    'uint64': torch.uint64,
+    'int64': torch.int64,
+    'float64': torch.float64,
+}
+
+
+def torch_dtype(name: str) -> torch.dtype:
+    return _TORCH_DTYPES[name]
+
+
+def _check(code: int, where: str) -> None:
+    _native.raise_for_code(code, where)
+
+
+@dataclass
+class ColumnPlan:
+    """One column of a :class:`Plan`."""
+    index: int
+    name: str
+    encoding: str
+    info: Optional[EncodingInfo]
+    kind: int  # _native.KIND_*
+    row_bytes: int  # fixed columns
+    elem_bytes: int
+
+    @property
+    def is_fixed(self) -> bool:
+        return self.kind == KIND_FIXED
+
+    def tensor_view(self) -> tuple[torch.dtype, tuple[int, ...]]:
+        """dtype and per-row shape of a fixed column's output tensor."""
+        info = self.info
+        if info is not None and info.dtype is not None and info.shape is not None and \
+                info.size == self.row_bytes:
+            return torch_dtype(info.dtype), tuple(info.shape)
+        return torch.uint8, (self.row_bytes,)
+
+
+class Plan:
+    """A compiled MDS schema: ``mdsx_plan_create`` over (encodings, column_sizes).
+
+    Args:
+        column_names: shard column names (sorted, as written by ``MDSWriter``).
+        column_encodings: encoding strings (``index.json`` ``column_encodings``).
+        column_sizes: fixed sizes or None (``index.json`` ``column_sizes``).
+    """
+
+    def __init__(self, column_names: Sequence[str], column_encodings: Sequence[str],
+                 column_sizes: Sequence[Optional[int]]) -> None:
+        if not (len(column_names) == len(column_encodings) == len(column_sizes)):
+            raise ValueError('column_names, column_encodings and column_sizes differ in length')
+        self._lib = _native.lib()
+        n = len(column_encodings)
+        enc_bytes = [e.encode('utf-8') for e in column_encodings]
+        encs = (ctypes.c_char_p * max(n, 1))(*enc_bytes)
+        sizes = (ctypes.c_int64 * max(n, 1))(*[int(s) if s else 0 for s in column_sizes])
+        handle = ctypes.c_void_p()
+        _check(self._lib.mdsx_plan_create(encs, sizes, n, ctypes.byref(handle)),
+               'mdsx_plan_create')
+        self._handle = handle
+        self.key = (tuple(column_names), tuple(column_encodings),
+                    tuple(int(s) if s else 0 for s in column_sizes))
+        self.columns: list[ColumnPlan] = []
+        for i, (name, enc) in enumerate(zip(column_names, column_encodings)):
+            kind, row_bytes, elem = ctypes.c_int(), ctypes.c_int64(), ctypes.c_int()
+            _check(
+                self._lib.mdsx_plan_column(handle, i, ctypes.byref(kind), ctypes.byref(row_bytes),
+                                           ctypes.byref(elem)), 'mdsx_plan_column')
+            try:
+                info = parse_encoding(enc)
+            except Exception:  # the C++ parser already accepted it; keep raw bytes semantics
+                info = None
+            self.columns.append(
+                ColumnPlan(i, name, enc, info, kind.value, row_bytes.value, elem.value))
+        self.num_var = self._lib.mdsx_plan_num_var(handle)
+        self.tile_rows = self._lib.mdsx_plan_tile_rows(handle)
+        self.is_safe = bool(self._lib.mdsx_plan_is_safe(handle))
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._handle
+
+    @property
+    def names(self) -> list[str]:
+        return [c.name for c in self.columns]
+
+    def workspace_bytes(self, ntiles: int) -> int:
+        return int(self._lib.mdsx_workspace_bytes(self._handle, ntiles))
+
+    def fixed_row_bytes(self) -> int:
+        return sum(c.row_bytes for c in self.columns if c.is_fixed)
+
+    def __del__(self) -> None:
+        handle = getattr(self, '_handle', None)
+        if handle is not None and handle.value:
+            try:
+                self._lib.mdsx_plan_destroy(handle)
+            except Exception:
+                pass
+            self._handle = ctypes.c_void_p()
+
+
+@dataclass
+class DeviceBatch:
+    """Shard files resident in one device buffer, plus the descriptor and tile tables.
+
+    Attributes:
+        buffer: uint8 device tensor; shard s occupies ``buffer[offsets[s]:offsets[s]+sizes[s]]``.
+        descs: device tensor holding ``nshards`` ``mdsx_shard_desc`` records.
+        tile_shard: device int32 tensor (read as uint32), the shard of each tile.
+    """
+    buffer: torch.Tensor
+    descs: torch.Tensor
+    tile_shard: torch.Tensor
+    offsets: list[int]
+    sizes: list[int]
+    samples: list[int]
+    row0: list[int]
+    ntiles: int
+    total_rows: int
+    tile_rows: int
+
+    @property
+    def nshards(self) -> int:
+        return len(self.sizes)
+
+    @property
+    def shard_bytes(self) -> int:
+        return int(sum(self.sizes))
+
+    @property
+    def device(self) -> torch.device:
+        return self.buffer.device
+
+
+def _layout(sizes: Sequence[int]) -> tuple[list[int], int]:
+    offsets, pos = [], BATCH_PAD
+    for size in sizes:
+        offsets.append(pos)
+        pos = (pos + int(size) + 255) & ~255
+    return offsets, pos + BATCH_PAD
+
+
+def _tables(sizes: Sequence[int], samples: Sequence[int], offsets: Sequence[int],
+            tile_rows: int) -> tuple[np.ndarray, np.ndarray, list[int], int, int]:
+    descs = (ShardDesc * max(len(sizes), 1))()
+    tile_shard, row0, rows, tiles = [], [], 0, 0
+    for s, (size, n, off) in enumerate(zip(sizes, samples, offsets)):
+        nt = math.ceil(int(n) / tile_rows)
+        d = descs[s]
+        d.offset, d.bytes, d.row0, d.samples, d.tile0 = off, int(size), rows, int(n), tiles
+        row0.append(rows)
+        tile_shard.extend([s] * nt)
+        rows += int(n)
+        tiles += nt
+    raw = np.frombuffer(bytes(descs), np.uint8)[:32 * len(sizes)].copy()
+    return raw, np.array(tile_shard, np.int32), row0, rows, tiles
+
+
+def make_batch(plan: Plan,
+               sizes: Sequence[int],
+               samples: Sequence[int],
+               device: Union[str, torch.device, None] = None) -> DeviceBatch:
+    """Allocate a zeroed batch buffer laid out for shards of ``sizes`` bytes (filled by the
+    caller at ``batch.offsets[s]``) with its descriptor and tile tables."""
+    if len(sizes) != len(samples):
+        raise ValueError('sizes and samples differ in length')
+    if not len(sizes):
+        raise ValueError('a batch needs at least one shard')
+    device = torch.device(device or 'cuda')
+    if device.type == 'cuda' and device.index is None:
+        device = torch.device('cuda', torch.cuda.current_device())
+    sizes = [int(x) for x in sizes]
+    offsets, total = _layout(sizes)
+    buffer = torch.zeros(total, dtype=torch.uint8, device=device)
+    raw, tile_shard, row0, rows, tiles = _tables(sizes, samples, offsets, plan.tile_rows)
+    descs = torch.from_numpy(raw).to(device)
+    tiles_t = torch.from_numpy(tile_shard).to(device) if tiles else torch.zeros(
+        1, dtype=torch.int32, device=device)
+    return DeviceBatch(buffer, descs, tiles_t, offsets, sizes, [int(n) for n in samples], row0,
+                       tiles, rows, plan.tile_rows)
+
+
+def stage_shards(shards: Sequence[Union[bytes, bytearray, memoryview, np.ndarray, torch.Tensor]],
+                 samples: Sequence[int],
+                 plan: Plan,
+                 device: Union[str, torch.device, None] = None,
+                 pin: bool = True) -> DeviceBatch:
+    """Copy shard files into one device buffer (host -> pinned staging -> HBM).
+
+    ``shards`` may also be uint8 device tensors already in HBM (copied device-to-device).
+    """
+    if len(shards) != len(samples):
+        raise ValueError('shards and samples differ in length')
+    sizes = [int(x.numel()) if isinstance(x, torch.Tensor) else len(memoryview(x).cast('B'))
+             for x in shards]
+    batch = make_batch(plan, sizes, samples, device)
+    host = [(i, x) for i, x in enumerate(shards) if not isinstance(x, torch.Tensor)]
+    if host:
+        lo = batch.offsets[host[0][0]]
+        hi = batch.offsets[host[-1][0]] + sizes[host[-1][0]]
+        staging = torch.empty(hi - lo, dtype=torch.uint8,
+                              pin_memory=pin and batch.device.type == 'cuda')
+        view = staging.numpy()
+        for i, x in host:
+            o = batch.offsets[i] - lo
+            view[o:o + sizes[i]] = np.frombuffer(memoryview(x).cast('B'), np.uint8)
+        # one H2D over the staged span; gaps between shards are never read as sample bytes
+        batch.buffer[lo:hi].copy_(staging, non_blocking=True)
+    for i, x in enumerate(shards):
+        if isinstance(x, torch.Tensor):
+            batch.buffer[batch.offsets[i]:batch.offsets[i] + sizes[i]].copy_(
+                x.reshape(-1).view(torch.uint8), non_blocking=True)
+    if host:
+        torch.cuda.current_stream(batch.device).synchronize()  # staging must outlive the copy
+    return batch
+
+
+@dataclass
+class RaggedColumn:
+    """A variable-size column: row i is ``values[offsets[i]:offsets[i+1]]``.
+
+    ``flags`` (str columns) is 1 where the row is not well-formed UTF-8, i.e. where the reference's
+    ``bytes.decode('utf-8')`` raises (encodings.py:80-81).
+    """
+    values: torch.Tensor
+    offsets: torch.Tensor
+    flags: Optional[torch.Tensor] = None
+
+    def __len__(self) -> int:
+        return int(self.offsets.numel()) - 1
+
+
+@dataclass
+class DecodedBatch:
+    """Decoded columns of a :class:`DeviceBatch` (device tensors)."""
+    columns: dict[str, Union[torch.Tensor, RaggedColumn]]
+    rows: int
+    row0: list[int] = field(default_factory=list)
+
+    def __getitem__(self, name: str) -> Union[torch.Tensor, RaggedColumn]:
+        return self.columns[name]
+
+
+def _status_error(status: _native.Status, plan: Plan) -> Exception:
+    code = status.code
+    col = ''
+    if 0 <= status.column < len(plan.columns):
+        col = f', column {plan.columns[status.column].name!r}'
+    where = f'shard {status.shard}, sample {status.row}{col}'
+    if code == _native.MDSX_E_EMPTY:
+        return IndexError(f'Relative sample index {status.row} is not present in shard '
+                          f'{status.shard} (empty sample).')
+    if code == _native.MDSX_E_HEADER:
+        return ValueError(f'Malformed MDS shard header ({where}).')
+    if code == _native.MDSX_E_BOUNDS:
+        return ValueError(f'MDS sample or column out of bounds ({where}).')
+    if code == _native.MDSX_E_CAPACITY:
+        return RuntimeError(f'ragged output capacity exceeded ({where}).')
+    return RuntimeError(f'mdsx device error {code} ({where}).')
+
+
+class BatchDecoder:
+    """Decode a :class:`DeviceBatch` on the device, reusing outputs across calls.
+
+    ``run()`` enqueues the scan + decode kernels on the current torch stream with no host sync
+    once the ragged capacities are known (first call, or given ``capacities``), so it can be
+    timed / captured. ``check()`` synchronizes and raises the first kernel-reported error.
+    """
+
+    def __init__(self, plan: Plan, batch: DeviceBatch,
+                 capacities: Optional[dict[str, int]] = None) -> None:
+        if plan.tile_rows != batch.tile_rows:
+            raise ValueError('batch was staged for a different tile size')
+        self.plan = plan
+        self.batch = batch
+        dev = batch.device
+        self.device = dev
+        rows = batch.total_rows
+        self.workspace = torch.zeros(max(plan.workspace_bytes(batch.ntiles), 256),
+                                     dtype=torch.uint8,
+                                     device=dev)
+        self.totals = torch.zeros(max(plan.num_var, 1), dtype=torch.int64, device=dev)
+        self.outputs: dict[str, Union[torch.Tensor, RaggedColumn]] = {}
+        self._fixed_raw: dict[str, torch.Tensor] = {}
+        for col in plan.columns:
+            if col.is_fixed:
+                raw = torch.empty((rows, col.row_bytes), dtype=torch.uint8, device=dev)
+                self._fixed_raw[col.name] = raw
+                dtype, shape = col.tensor_view()
+                self.outputs[col.name] = raw.view(dtype).reshape((rows,) + shape)
+            else:
+                offsets = torch.empty(rows + 1, dtype=torch.int64, device=dev)
+                flags = torch.zeros(rows, dtype=torch.uint8,
+                                    device=dev) if col.kind == KIND_STR else None
+                self.outputs[col.name] = RaggedColumn(torch.empty(0, dtype=torch.uint8,
+                                                                  device=dev), offsets, flags)
+        self._capacities = dict(capacities or {})
+        self._outs = (ColumnOut * max(len(plan.columns), 1))()
+        self._sized = plan.num_var == 0
+        if capacities:
+            self._resize(capacities)
+
+    def _resize(self, capacities: dict[str, int]) -> None:
+        for col in self.plan.columns:
+            if col.is_fixed:
+                continue
+            need = int(capacities[col.name])
+            rc = self.outputs[col.name]
+            if rc.values.numel() < need:
+                rc.values = torch.empty(max(need, 1), dtype=torch.uint8, device=self.device)
+        self._sized = True
+
+    def _fill_outs(self) -> None:
+        for col in self.plan.columns:
+            o = self._outs[col.index]
+            out = self.outputs[col.name]
+            if col.is_fixed:
+                o.data, o.offsets, o.flags, o.capacity = self._fixed_raw[col.name].data_ptr(
+                ), None, None, 0
+            else:
+                o.data = out.values.data_ptr() if out.values.numel() else None
+                o.offsets = out.offsets.data_ptr()
+                o.flags = out.flags.data_ptr() if out.flags is not None else None
+                o.capacity = int(out.values.numel())
+
+    def _scan(self, stream: int) -> None:
+        b = self.batch
+        _check(
+            self.plan._lib.mdsx_scan_shards(self.plan.handle, b.buffer.data_ptr(),
+                                            b.descs.data_ptr(), b.nshards,
+                                            b.tile_shard.data_ptr(), b.ntiles, b.total_rows,
+                                            self._outs, self.workspace.data_ptr(),
+                                            self.totals.data_ptr(), stream), 'mdsx_scan_shards')
+
+    def run(self, events: Optional[Sequence[torch.cuda.Event]] = None) -> DecodedBatch:
+        """Enqueue the decode of the whole batch; returns the (device) decoded columns.
+
+        ``events``: optional three CUDA events recorded on the stream before the scan pass,
+        between the scan and the decode kernel, and after the decode kernel (kernel timing).
+        """
+        b = self.batch
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        self._fill_outs()
+        if events is not None:
+            events[0].record()
+        self._scan(stream)  # resets the status record; ragged plans: offsets + totals
+        if self.plan.num_var and not self._sized:
+            totals = self.totals.cpu().tolist()  # host sync: size the ragged outputs once
+            caps, vi = {}, 0
+            for col in self.plan.columns:
+                if not col.is_fixed:
+                    caps[col.name] = int(totals[vi])
+                    vi += 1
+            self._capacities = caps
+            self._resize(caps)
+            self._fill_outs()
+        if events is not None:
+            events[1].record()
+        _check(
+            self.plan._lib.mdsx_decode_shards(self.plan.handle, b.buffer.data_ptr(),
+                                              b.descs.data_ptr(), b.nshards,
+                                              b.tile_shard.data_ptr(), b.ntiles, b.total_rows,
+                                              self._outs, self.workspace.data_ptr(), stream),
+            'mdsx_decode_shards')
+        if events is not None:
+            events[2].record()
+        return self.result()
+
+    def result(self) -> DecodedBatch:
+        cols: dict[str, Union[torch.Tensor, RaggedColumn]] = {}
+        for col in self.plan.columns:
+            out = self.outputs[col.name]
+            if isinstance(out, RaggedColumn):
+                cap = self._capacities.get(col.name, 0)
+                out = RaggedColumn(out.values[:cap], out.offsets, out.flags)
+            cols[col.name] = out
+        return DecodedBatch(cols, self.batch.total_rows, list(self.batch.row0))
+
+    @property
+    def capacities(self) -> dict[str, int]:
+        return dict(self._capacities)
+
+    def status(self) -> _native.Status:
+        raw = self.workspace[:16].cpu().numpy().tobytes()  # syncs the stream
+        return _native.Status.from_buffer_copy(raw)
+
+    def check(self) -> None:
+        st = self.status()
+        if st.code != 0:
+            raise _status_error(st, self.plan)
+
+
+def decode_batch(plan: Plan, batch: DeviceBatch, check: bool = True) -> DecodedBatch:
+    """Decode every shard of ``batch`` (scan + decode) and, by default, check the status."""
+    dec = BatchDecoder(plan, batch)
+    out = dec.run()
+    if check:
+        dec.check()
+    return out
+
+
+def output_bytes(plan: Plan, decoded: DecodedBatch) -> int:
+    """W of SURVEY.md §8(d): bytes the decode writes (values, offsets, flags)."""
+    total = 0
+    for col in plan.columns:
+        out = decoded.columns[col.name]
+        if isinstance(out, RaggedColumn):
+            total += int(out.values.numel()) + 8 * int(out.offsets.numel())
+            if out.flags is not None:
+                total += int(out.flags.numel())
+        else:
+            total += int(out.numel()) * out.element_size()
+    return total
+
+
+KINDS = {KIND_FIXED: 'fixed', KIND_BYTES: 'bytes', KIND_STR: 'str', KIND_NDARRAY: 'ndarray'}

@@ -1,0 +1,389 @@
+"""Device-backed MDS shard reader with the reference ``Reader`` / ``MDSReader`` interface.
+
+The reference reader (``streaming/base/format/base/reader.py:31-400``,
+``streaming/base/format/mds/reader.py:19-149``) decodes ONE sample per call with Python file
+I/O and numpy. :class:`MDSReader` keeps that interface -- ``from_json``, ``validate``,
+``get_sample_data``, ``decode_sample``, ``get_item``, fancy ``__getitem__``, ``__len__``,
+``size`` and the cache bookkeeping (``evict``, ``set_up_local``, size queries) -- but decodes
+the WHOLE shard on the GPU the first time any sample is asked for (:meth:`decode_shard`, through
+libmdsx.so), then serves samples from the decoded columns:
+
+* :meth:`decode_shard` -> device tensors (``DecodedBatch``): the hot path.
+* :meth:`get_item` -> a dict of host objects with the reference's types (Python ``int`` for
+  ``int``, numpy scalars, read-only ndarrays, ``bytes``, ``str``), materialised from one D2H copy
+  of the decoded shard. ``str`` rows are produced by ``bytes.decode('utf-8')`` of the
+  device-gathered bytes, so invalid UTF-8 raises the same ``UnicodeDecodeError``.
+* :meth:`decode_sample` decodes one sample's bytes on the device as a one-sample shard.
+
+A missing shard file raises ``FileNotFoundError`` from ``open`` exactly as the reference does
+(the caller's prepare-and-retry loop, ``dataset.py:1274-1291``, depends on it).
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import threading
+from copy import deepcopy
+from dataclasses import dataclass
+from typing import Any, Iterator, Optional, Union
+
+import numpy as np
+import torch
+
+from streaming_amd.array import Array
+from streaming_amd.decoder import DecodedBatch, Plan, RaggedColumn, decode_batch, stage_shards
+from streaming_amd.encodings import (host_object_decode, is_mds_encoding_safe,
+                                     ndarray_dyn_decode, parse_encoding)
+from streaming_amd.writer import bytes_to_int
+
+__all__ = ['FileInfo', 'Reader', 'JointReader', 'MDSReader', 'get_plan', 'reader_from_json']
+
+_plan_lock = threading.Lock()
+_plans: dict[tuple, Plan] = {}
+
+
+def get_plan(column_names, column_encodings, column_sizes) -> Plan:
+    """Compiled plan for a schema (one per distinct schema per process)."""
+    key = (tuple(column_names), tuple(column_encodings),
+           tuple(int(s) if s else 0 for s in column_sizes))
+    with _plan_lock:
+        plan = _plans.get(key)
+        if plan is None:
+            plan = Plan(column_names, column_encodings, column_sizes)
+            _plans[key] = plan
+    return plan
+
+
+@dataclass
+class FileInfo:
+    """File validation info (base/reader.py:17-28)."""
+    basename: str
+    bytes: int
+    hashes: dict[str, str]
+
+
+class Reader(Array):
+    """Random access to the samples of a shard (base/reader.py:31-330)."""
+
+    def __init__(self, dirname: str, split: Optional[str], compression: Optional[str],
+                 hashes: list[str], samples: int, size_limit: Optional[Union[int, str]]) -> None:
+        if size_limit:
+            if isinstance(size_limit, str):
+                size_limit = bytes_to_int(size_limit)
+            if size_limit < 0:
+                raise ValueError(f'`size_limit` must be greater than zero, instead, ' +
+                                 f'found as {size_limit}.')
+        self.dirname = dirname
+        self.split = split or ''
+        self.compression = compression
+        self.hashes = hashes
+        self.samples = samples
+        self.size_limit = size_limit
+        self.file_pairs: list[tuple[FileInfo, Optional[FileInfo]]] = []
+
+    def validate(self, allow_unsafe_types: bool) -> None:
+        pass
+
+    @property
+    def size(self) -> int:
+        return self.samples
+
+    def __len__(self) -> int:
+        return self.samples
+
+    def _path(self, basename: str) -> str:
+        return os.path.join(self.dirname, self.split, basename)
+
+    def _evict_raw(self) -> int:
+        size = 0
+        for raw_info, _ in self.file_pairs:
+            filename = self._path(raw_info.basename)
+            if os.path.exists(filename):
+                os.remove(filename)
+                size += raw_info.bytes
+        return size
+
+    def _evict_zip(self) -> int:
+        size = 0
+        for _, zip_info in self.file_pairs:
+            if zip_info:
+                filename = self._path(zip_info.basename)
+                if os.path.exists(filename):
+                    os.remove(filename)
+                    size += zip_info.bytes
+        return size
+
+    def evict(self) -> int:
+        return self._evict_raw() + self._evict_zip()
+
+    def set_up_local(self, listing: set[str], safe_keep_zip: bool) -> int:
+        """Normalise which of raw/zip are present; return cache bytes (base/reader.py:136-225)."""
+        raw_present = sum(1 for raw, _ in self.file_pairs if raw and self._path(raw.basename) in
+                          listing)
+        zip_present = sum(1 for _, z in self.file_pairs if z and self._path(z.basename) in listing)
+        has_raw = raw_present == len(self.file_pairs) and raw_present > 0
+        if 0 < raw_present < len(self.file_pairs):
+            self._evict_raw()
+        has_zip = zip_present == len(self.file_pairs) and zip_present > 0
+        if 0 < zip_present < len(self.file_pairs):
+            self._evict_zip()
+        if self.compression:
+            if safe_keep_zip:
+                if has_raw and not has_zip:
+                    has_raw = False
+                    self._evict_raw()
+            elif has_raw and has_zip:
+                has_zip = False
+                self._evict_raw()
+        elif has_zip:
+            raise ValueError('Shard is invalid: compression was not used, but has a ' +
+                             'compressed form.')
+        size = 0
+        if has_raw:
+            size += self.get_raw_size()
+        if has_zip:
+            size += self.get_zip_size() or 0
+        return size
+
+    def get_raw_size(self) -> int:
+        return sum(info.bytes for info, _ in self.file_pairs)
+
+    def get_zip_size(self) -> Optional[int]:
+        size = 0
+        for _, info in self.file_pairs:
+            if info is None:
+                return None
+            size += info.bytes
+        return size
+
+    def get_max_size(self) -> int:
+        return self.get_raw_size() + (self.get_zip_size() or 0)
+
+    def get_persistent_size(self, keep_zip: bool) -> int:
+        if self.compression and keep_zip:
+            return self.get_max_size()
+        return self.get_raw_size()
+
+    def decode_sample(self, data: bytes) -> dict[str, Any]:
+        raise NotImplementedError
+
+    def get_sample_data(self, idx: int) -> bytes:
+        raise NotImplementedError
+
+    def get_item(self, idx: int) -> dict[str, Any]:
+        data = self.get_sample_data(idx)
+        return self.decode_sample(data)
+
+    def __iter__(self) -> Iterator[dict[str, Any]]:
+        for i in range(len(self)):
+            yield self[i]
+
+
+class JointReader(Reader):
+    """A shard stored as one file (base/reader.py:323-361)."""
+
+    def __init__(self, dirname: str, split: Optional[str], compression: Optional[str],
+                 hashes: list[str], raw_data: FileInfo, samples: int,
+                 size_limit: Optional[Union[int, str]], zip_data: Optional[FileInfo]) -> None:
+        super().__init__(dirname, split, compression, hashes, samples, size_limit)
+        self.raw_data = raw_data
+        self.zip_data = zip_data
+        self.file_pairs.append((raw_data, zip_data))
+
+
+class _HostShard:
+    """Host copy of one decoded shard, for per-sample ``get_item``."""
+
+    def __init__(self, plan: Plan, decoded: DecodedBatch) -> None:
+        self.fixed: dict[str, np.ndarray] = {}
+        self.ragged: dict[str, tuple[np.ndarray, np.ndarray]] = {}
+        for col in plan.columns:
+            out = decoded.columns[col.name]
+            if isinstance(out, RaggedColumn):
+                self.ragged[col.name] = (out.values.cpu().numpy(), out.offsets.cpu().numpy())
+            else:
+                rows = out.shape[0]
+                raw = out.reshape(rows, -1).view(torch.uint8).cpu().numpy()
+                raw.setflags(write=False)
+                self.fixed[col.name] = raw
+
+
+class MDSReader(JointReader):
+    """Random access to the samples of an MDS shard, decoded on the GPU.
+
+    Same constructor as the reference (mds/reader.py:39-57) plus ``device``.
+    """
+
+    def __init__(self,
+                 dirname: str,
+                 split: Optional[str],
+                 column_encodings: list[str],
+                 column_names: list[str],
+                 column_sizes: list[Optional[int]],
+                 compression: Optional[str],
+                 hashes: list[str],
+                 raw_data: FileInfo,
+                 samples: int,
+                 size_limit: Optional[Union[int, str]],
+                 zip_data: Optional[FileInfo],
+                 device: Union[str, torch.device, None] = None) -> None:
+        super().__init__(dirname, split, compression, hashes, raw_data, samples, size_limit,
+                         zip_data)
+        self.column_encodings = column_encodings
+        self.column_names = column_names
+        self.column_sizes = column_sizes
+        self.device = device
+        self._infos = [parse_encoding(e) for e in column_encodings]
+        self._lock = threading.Lock()
+        self._decoded: Optional[DecodedBatch] = None
+        self._host: Optional[_HostShard] = None
+
+    @classmethod
+    def from_json(cls, dirname: str, split: Optional[str], obj: dict[str, Any],
+                  device: Union[str, torch.device, None] = None) -> 'MDSReader':
+        """Initialize from an ``index.json`` shard entry (mds/reader.py:59-86)."""
+        args = deepcopy(obj)
+        if args['version'] != 2:
+            raise ValueError(f'Unsupported streaming data version: {args["version"]}. '
+                             f'Expected version 2.')
+        del args['version']
+        if args['format'] != 'mds':
+            raise ValueError(f'Unsupported data format: {args["format"]}. Expected to be `mds`.')
+        del args['format']
+        args['dirname'] = dirname
+        args['split'] = split
+        for key in ['raw_data', 'zip_data']:
+            arg = args[key]
+            args[key] = FileInfo(**arg) if arg else None
+        return cls(**args, device=device)
+
+    def validate(self, allow_unsafe_types: bool) -> None:
+        """Reject unsafe encodings unless allowed (mds/reader.py:88-101)."""
+        if not allow_unsafe_types:
+            for column_id, encoding in enumerate(self.column_encodings):
+                if not is_mds_encoding_safe(encoding):
+                    name = self.column_names[column_id]
+                    raise ValueError(f'Column {name} contains an unsafe type: {encoding}. To ' +
+                                     f'proceed anyway, set ``allow_unsafe_types=True``.')
+
+    @property
+    def plan(self) -> Plan:
+        return get_plan(self.column_names, self.column_encodings, self.column_sizes)
+
+    def _filename(self) -> str:
+        return self._path(self.raw_data.basename)
+
+    def read_shard_bytes(self) -> bytes:
+        """The raw shard file (FileNotFoundError if it is not in the local cache)."""
+        with open(self._filename(), 'rb', 0) as fp:
+            return fp.read()
+
+    def decode_shard(self, check: bool = True) -> DecodedBatch:
+        """Decode every sample of this shard on the GPU (cached). Device tensors."""
+        with self._lock:
+            if self._decoded is None:
+                data = self.read_shard_bytes()
+                plan = self.plan
+                batch = stage_shards([data], [self.samples], plan, device=self.device)
+                self._decoded = decode_batch(plan, batch, check=check)
+            return self._decoded
+
+    def release(self) -> None:
+        """Drop the cached decoded shard (device and host copies)."""
+        with self._lock:
+            self._decoded = None
+            self._host = None
+
+    def get_sample_data(self, idx: int) -> bytes:
+        """Raw bytes of sample ``idx`` (mds/reader.py:128-149): file offsets table + range."""
+        offset = (1 + idx) * 4
+        with open(self._filename(), 'rb', 0) as fp:
+            fp.seek(offset)
+            pair = fp.read(8)
+            begin, end = np.frombuffer(pair, np.uint32)
+            fp.seek(begin)
+            data = fp.read(end - begin)
+        if not data:
+            raise IndexError(
+                f'Relative sample index {idx} is not present in the {self.raw_data.basename} file.')
+        return data
+
+    def _materialize(self, host: _HostShard, idx: int) -> dict[str, Any]:
+        sample: dict[str, Any] = {}
+        for col, enc, info in zip(self.plan.columns, self.column_encodings, self._infos):
+            if col.is_fixed:
+                raw = host.fixed[col.name][idx]
+                sample[col.name] = self._value(enc, info, raw, fixed=True)
+            else:
+                values, offsets = host.ragged[col.name]
+                data = values[offsets[idx]:offsets[idx + 1]].tobytes()
+                sample[col.name] = self._value(enc, info, data, fixed=False)
+        return sample
+
+    @staticmethod
+    def _value(encoding: str, info, raw, fixed: bool) -> Any:
+        """Reference value type of one decoded column value (encodings.py:62-397)."""
+        name = info.name if info is not None else None
+        if fixed and info is not None and info.size == len(raw) and info.dtype is not None:
+            arr = raw.view(info.dtype)
+            if name == 'int':
+                return int(arr[0])
+            if info.shape == ():
+                return arr[0]
+            return arr.reshape(info.shape)
+        data = raw.tobytes() if isinstance(raw, np.ndarray) else raw
+        if name == 'bytes':
+            return data
+        if name == 'str':
+            return data.decode('utf-8')
+        if name == 'ndarray':
+            return ndarray_dyn_decode(info, data)
+        if name == 'int':
+            return int(np.frombuffer(data, np.int64)[0])
+        if info is not None and info.dtype is not None and info.shape == ():
+            return np.frombuffer(data, info.dtype)[0]
+        return host_object_decode(encoding, data)
+
+    def get_item(self, idx: int) -> dict[str, Any]:
+        """Sample ``idx`` as a dict of host objects, from the device-decoded shard."""
+        if not (0 <= idx < self.samples):
+            raise IndexError(
+                f'Relative sample index {idx} is not present in the {self.raw_data.basename} file.')
+        host = self._host
+        if host is None:
+            decoded = self.decode_shard()
+            with self._lock:
+                if self._host is None:
+                    self._host = _HostShard(self.plan, decoded)
+                host = self._host
+        return self._materialize(host, idx)
+
+    def decode_sample(self, data: bytes) -> dict[str, Any]:
+        """Decode one sample's bytes on the device, as a one-sample shard."""
+        plan = self.plan
+        header = 4 + 8
+        shard = (np.uint32(1).tobytes() + np.array([header, header + len(data)], np.uint32).tobytes() +
+                 data)
+        batch = stage_shards([shard], [1], plan, device=self.device)
+        decoded = decode_batch(plan, batch)
+        return self._materialize(_HostShard(plan, decoded), 0)
+
+
+def reader_from_json(dirname: str, split: Optional[str], obj: dict[str, Any],
+                     device: Union[str, torch.device, None] = None) -> MDSReader:
+    """Reader for an index.json shard entry (format/__init__.py:29-42); MDS only."""
+    assert obj['version'] == 2
+    if obj['format'] != 'mds':
+        raise ValueError(f'streaming_amd decodes MDS shards only, got format {obj["format"]!r}')
+    return MDSReader.from_json(dirname, split, obj, device=device)
+
+
+def load_index(dirname: str, split: Optional[str] = None) -> dict[str, Any]:
+    filename = os.path.join(dirname, split or '', 'index.json')
+    with open(filename) as f:
+        obj = json.load(f)
+    if obj['version'] != 2:
+        raise ValueError(f'Unsupported streaming data version: {obj["version"]}. ' +
+                         f'Expected version 2.')
+    return obj

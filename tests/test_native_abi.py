@@ -1,0 +1,90 @@
+"""libmdsx.so loads on a CPU-only host, exports every symbol include/mdsx.h declares, and its
+host-side plan builder parses schemas like the reference's _get_coder (no GPU calls here)."""
+
+import ctypes
+import os
+import re
+
+import pytest
+
+from streaming_amd import _native
+from streaming_amd.decoder import Plan
+from tests import golden_util as gu
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'include',
+                      'mdsx.h')
+
+
+def _declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r'/\*.*?\*/', '', text, flags=re.S)
+    return sorted(set(re.findall(r'\b(mdsx_[a-z_]+)\s*\(', text)))
+
+
+def test_header_matches_binding_list():
+    assert _declared_functions() == sorted(_native.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _native.lib()
+    for name in _declared_functions():
+        assert hasattr(lib, name), name
+    assert lib.mdsx_version().startswith(b'mdsx')
+
+
+def test_struct_layouts():
+    assert ctypes.sizeof(_native.ShardDesc) == 32
+    assert ctypes.sizeof(_native.ColumnOut) == 32
+    assert ctypes.sizeof(_native.Status) == 16
+
+
+@pytest.mark.parametrize('name', gu.ALL_SETS)
+def test_plan_for_every_golden_schema(name):
+    info = gu.index(name)['shards'][0]
+    plan = Plan(info['column_names'], info['column_encodings'], info['column_sizes'])
+    assert len(plan.columns) == len(info['column_names'])
+    for col, size in zip(plan.columns, info['column_sizes']):
+        assert col.is_fixed == bool(size)
+        if size:
+            assert col.row_bytes == size
+    assert plan.num_var == sum(1 for s in info['column_sizes'] if not s)
+    assert plan.tile_rows in (64, 256)
+    if name == 'wide':
+        assert plan.tile_rows == 64
+
+
+def test_plan_kinds():
+    plan = Plan(['a', 'b', 'c', 'd', 'e', 'f'], ['int', 'bytes', 'str', 'ndarray', 'ndarray:int16',
+                                                  'json'], [8, None, None, None, None, None])
+    kinds = [c.kind for c in plan.columns]
+    assert kinds == [_native.KIND_FIXED, _native.KIND_BYTES, _native.KIND_STR,
+                     _native.KIND_NDARRAY, _native.KIND_NDARRAY, _native.KIND_BYTES]
+    assert plan.is_safe
+    assert not Plan(['p'], ['pkl'], [None]).is_safe
+
+
+@pytest.mark.parametrize('enc', ['foo', 'int:3', 'bytes:1', 'ndarray:float32:', 'ndarray:float33',
+                                 'ndarray:float32:0', 'ndarray:float32:2:3:4', 'ndarray:int8:-1'])
+def test_plan_rejects_unsupported_encodings(enc):
+    with pytest.raises(ValueError):
+        Plan(['a'], [enc], [None])
+
+
+@pytest.mark.parametrize('enc,size', [('ndarray:uint8:3', 3), ('ndarray:float32:1, 2', 8),
+                                      ('ndarray:int16:+2,3', 12), ('ndarray:uint8:1_0', 10),
+                                      ('ndarray:', None), ('ndarray:float64', None)])
+def test_plan_accepts_python_int_shapes(enc, size):
+    plan = Plan(['a'], [enc], [size])
+    assert plan.columns[0].is_fixed == (size is not None)
+
+
+def test_workspace_bytes():
+    plan = Plan(['b', 'n', 's'], ['bytes', 'int', 'str'], [None, 8, None])
+    assert plan.workspace_bytes(100) == 256 + ((2 * 2 * 100 * 8 + 255) // 256) * 256
+    fixed = Plan(['id', 'x'], ['int32', 'ndarray:float32:1024'], [4, 4096])
+    assert fixed.workspace_bytes(1000) == 256
+
+
+def test_too_many_columns():
+    with pytest.raises(ValueError):
+        Plan([f'c{i}' for i in range(65)], ['int'] * 65, [8] * 65)
