@@ -412,14 +412,6 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
       uint64_t len = col.row_bytes;
       if (col.var_index >= 0) {
         len = ok ? load_u32_any(v.shard + b + 4u * uint32_t(col.var_index)) : 0u;
-        const int64_t off = a.tile_prefix[uint64_t(col.var_index) * a.ntiles + blockIdx.x] +
-                            col.offsets[row];
-        col.offsets[row] = off;
-        s_vdst[col.var_index * TR + t] = uint64_t(off);
-        if (ok && uint64_t(off) + len > col.capacity) {
-          report(a.status, MDSX_E_CAPACITY, v.shard_idx, int(i), c);
-          ok = false;
-        }
         s_vlen[col.var_index * TR + t] = uint32_t(len);
       }
       s_src[c * TR + t] = uint32_t(pos);
@@ -428,6 +420,19 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
     if (ok && pos > e) {
       ok = false;
       rc = MDSX_E_BOUNDS;
+    }
+    // Ragged destinations: tile prefix + the local offset the scan pass left in offsets[row].
+    for (int c = 0; c < a.ncols; ++c) {
+      const DevCol& col = a.cols[c];
+      if (col.var_index < 0) continue;
+      const int vi = col.var_index;
+      const int64_t off = a.tile_prefix[uint64_t(vi) * a.ntiles + blockIdx.x] + col.offsets[row];
+      col.offsets[row] = off;
+      s_vdst[vi * TR + t] = uint64_t(off);
+      if (ok && uint64_t(off) + s_vlen[vi * TR + t] > col.capacity) {
+        report(a.status, MDSX_E_CAPACITY, v.shard_idx, int(i), c);
+        ok = false;
+      }
     }
     if (!ok && rc != MDSX_OK) report(a.status, rc, v.shard_idx, int(i), -1);
     s_ok[t] = ok ? 1 : 0;
