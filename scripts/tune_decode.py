@@ -1,0 +1,97 @@
+"""A/B the decode kernel's tuning knobs in ONE process on one GPU (interleaved rounds).
+
+    python scripts/tune_decode.py --config B --variants "tile=256" "tile=64" "unroll=8,nt=1"
+
+Each variant builds its own plan (MDSX_TUNE is read at plan creation) over the SAME resident
+shard batch (tile tables rebuilt for its tile size), is verified bit-exact, then all variants are
+timed round-robin for --rounds rounds with HIP events around the decode kernel. Also times a
+torch device-to-device copy of the shard bytes (the measured HBM copy ceiling on this box).
+"""
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from streaming_amd.decoder import BatchDecoder, DeviceBatch, Plan, _tables, output_bytes  # noqa
+from streaming_amd.synth import fixed_b_batch_on_device, var_c_shards  # noqa
+
+
+def retile(batch: DeviceBatch, plan: Plan) -> DeviceBatch:
+    raw, tile_shard, row0, rows, tiles = _tables(batch.sizes, batch.samples, batch.offsets,
+                                                 plan.tile_rows)
+    dev = batch.device
+    return DeviceBatch(batch.buffer, torch.from_numpy(raw).to(dev),
+                       torch.from_numpy(tile_shard).to(dev), batch.offsets, batch.sizes,
+                       batch.samples, row0, tiles, rows, plan.tile_rows)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--config', default='B')
+    ap.add_argument('--samples', type=int, default=1_000_000)
+    ap.add_argument('--rounds', type=int, default=5)
+    ap.add_argument('--iters', type=int, default=10)
+    ap.add_argument('--variants', nargs='+', default=['tile=256'])
+    args = ap.parse_args()
+    torch.cuda.set_device(0)
+    if args.config == 'B':
+        synth = fixed_b_batch_on_device(args.samples, seed=3)
+        base_batch, names = synth.batch, (['id', 'x'], ['int32', 'ndarray:float32:1024'],
+                                           [4, 4096])
+        src = synth.sources
+    else:
+        from streaming_amd.decoder import stage_shards
+        shards, counts, src = var_c_shards(args.samples, seed=4)
+        names = (['b', 'n', 's'], ['bytes', 'int', 'str'], [None, 8, None])
+        base_batch = stage_shards(shards, counts, Plan(*names))
+    decs = {}
+    for v in args.variants:
+        os.environ['MDSX_TUNE'] = v
+        plan = Plan(*names)
+        dec = BatchDecoder(plan, retile(base_batch, plan))
+        out = dec.run()
+        dec.check()
+        if args.config == 'B':
+            assert torch.equal(out['x'].view(torch.int32), src['x'].view(torch.int32)), v
+            assert torch.equal(out['id'], src['id']), v
+        else:
+            assert np.array_equal(out['b'].values.cpu().numpy(), src['b_pool']), v
+            assert np.array_equal(out['s'].values.cpu().numpy(), src['s_pool']), v
+            assert np.array_equal(out['n'].cpu().numpy(), src['n']), v
+        decs[v] = dec
+    R = base_batch.shard_bytes
+    W = output_bytes(decs[args.variants[0]].plan, decs[args.variants[0]].result())
+    copy_dst = torch.empty_like(base_batch.buffer)
+    times = {v: [] for v in args.variants}
+    times['torch_copy'] = []
+    for _ in range(args.rounds):
+        for v, dec in decs.items():
+            evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)]
+                   for _ in range(args.iters)]
+            for e in evs:
+                dec.run(e)
+            torch.cuda.synchronize()
+            times[v].extend(e[1].elapsed_time(e[2]) for e in evs)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(args.iters):
+            copy_dst.copy_(base_batch.buffer)
+        e.record()
+        torch.cuda.synchronize()
+        times['torch_copy'].append(s.elapsed_time(e) / args.iters)
+    res = {}
+    for v, ts in times.items():
+        ms = float(np.median(ts))
+        nbytes = 2 * base_batch.buffer.numel() if v == 'torch_copy' else R + W
+        res[v] = {'median_ms': ms, 'min_ms': float(np.min(ts)), 'GBps': nbytes / ms / 1e6}
+    print(json.dumps({'config': args.config, 'R': R, 'W': W, 'results': res}, indent=1))
+
+
+if __name__ == '__main__':
+    main()

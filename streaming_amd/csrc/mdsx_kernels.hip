@@ -31,7 +31,6 @@
 namespace mdsx_kernels {
 
 constexpr int kBlock = 256;   // 4 waves
-constexpr int kUnroll = 4;    // 16-byte chunks in flight per lane in wave_copy (4 KiB per wave)
 constexpr int kSmallMax = 16; // fixed columns up to this many bytes: one row per lane
 
 struct DevCol {
@@ -61,6 +60,29 @@ struct DevArgs {
   int32_t pad_;
   DevCol cols[MDSX_MAX_COLUMNS];
 };
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// 16-byte global load / store, optionally non-temporal (streamed once: no reuse in L2/MALL).
+template <bool kNT>
+__device__ __forceinline__ uint4 ld16(const uint4* p) {
+  if constexpr (kNT) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  } else {
+    return *p;
+  }
+}
+
+template <bool kNT>
+__device__ __forceinline__ void st16(uint64_t addr, const uint4 v) {
+  if constexpr (kNT) {
+    const u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(addr));
+  } else {
+    *reinterpret_cast<uint4*>(addr) = v;
+  }
+}
 
 __device__ __forceinline__ uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t r) {
   return __builtin_amdgcn_alignbyte(hi, lo, r);
@@ -270,7 +292,7 @@ __device__ __forceinline__ bool utf8_chunk_bad(const uint4 v, uint32_t pw, int64
 // the next step, or one extra load at the end of a batch). Partial chunks at the two ends are
 // written byte by byte. With kUtf8, returns whether the segment is not well-formed UTF-8
 // (wave-uniform).
-template <bool kUtf8>
+template <bool kUtf8, int kUnroll, bool kNT>
 __device__ __forceinline__ bool wave_copy(const uint8_t* src, uint8_t* dst, uint64_t len,
                                           int lane) {
   if (len == 0) return false;
@@ -289,12 +311,12 @@ __device__ __forceinline__ bool wave_copy(const uint8_t* src, uint8_t* dst, uint
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       const uint64_t k = base + uint64_t(u) * 64 + lane;
-      lo[u] = (k < nload) ? sal[k] : make_uint4(0, 0, 0, 0);
+      lo[u] = (k < nload) ? ld16<kNT>(sal + k) : make_uint4(0, 0, 0, 0);
     }
     uint4 tail = make_uint4(0, 0, 0, 0);
     if (sh != 0 && lane == 63) {
       const uint64_t k = base + 64 * kUnroll;
-      if (k < nload) tail = sal[k];
+      if (k < nload) tail = ld16<kNT>(sal + k);
     }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
@@ -325,7 +347,7 @@ __device__ __forceinline__ bool wave_copy(const uint8_t* src, uint8_t* dst, uint
       }
       if (k < nchunks) {
         if (D >= d0 && D + 16 <= dend) {
-          *reinterpret_cast<uint4*>(D) = out;
+          st16<kNT>(D, out);
         } else {
 #pragma unroll
           for (int j = 0; j < 16; ++j) {
@@ -371,6 +393,7 @@ __device__ __forceinline__ void gather_small(const uint8_t* p, uint8_t* dst, uin
 }
 
 // Pass 2: decode every column of every row of a tile.
+template <int kUnroll, bool kNT>
 __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int TR = a.tile_rows;
@@ -459,17 +482,17 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
       const uint8_t* src = v.shard + s_src[c * TR + r];
       if (col.var_index < 0) {
         if (col.row_bytes <= uint32_t(kSmallMax)) continue;
-        wave_copy<false>(src, static_cast<uint8_t*>(col.data) + row * col.row_bytes,
+        wave_copy<false, kUnroll, kNT>(src, static_cast<uint8_t*>(col.data) + row * col.row_bytes,
                          col.row_bytes, lane);
       } else {
         const int vi = col.var_index;
         uint8_t* dst = static_cast<uint8_t*>(col.data) + s_vdst[vi * TR + r];
         const uint64_t len = s_vlen[vi * TR + r];
         if (col.kind == MDSX_KIND_STR) {
-          const bool bad = wave_copy<true>(src, dst, len, lane);
+          const bool bad = wave_copy<true, kUnroll, kNT>(src, dst, len, lane);
           if (lane == 0 && col.flags) col.flags[row] = bad ? 1 : 0;
         } else {
-          wave_copy<false>(src, dst, len, lane);
+          wave_copy<false, kUnroll, kNT>(src, dst, len, lane);
         }
       }
     }
@@ -564,7 +587,19 @@ int mdsx_decode_shards(const mdsx_plan* plan, const uint8_t* d_batch,
   const size_t lds = size_t(plan->tile_rows) *
                          (8 * size_t(plan->nvar) + 4 * size_t(plan->ncols) + 4 * size_t(plan->nvar) + 1) +
                      16;
-  hipLaunchKernelGGL(decode_kernel, dim3(ntiles), dim3(kBlock), lds, s, a);
+  const int u = plan->unroll, nt = plan->nontemporal;
+  if (u == 8 && nt)
+    hipLaunchKernelGGL((decode_kernel<8, true>), dim3(ntiles), dim3(kBlock), lds, s, a);
+  else if (u == 8)
+    hipLaunchKernelGGL((decode_kernel<8, false>), dim3(ntiles), dim3(kBlock), lds, s, a);
+  else if (u == 2 && nt)
+    hipLaunchKernelGGL((decode_kernel<2, true>), dim3(ntiles), dim3(kBlock), lds, s, a);
+  else if (u == 2)
+    hipLaunchKernelGGL((decode_kernel<2, false>), dim3(ntiles), dim3(kBlock), lds, s, a);
+  else if (nt)
+    hipLaunchKernelGGL((decode_kernel<4, true>), dim3(ntiles), dim3(kBlock), lds, s, a);
+  else
+    hipLaunchKernelGGL((decode_kernel<4, false>), dim3(ntiles), dim3(kBlock), lds, s, a);
   return hip_check(hipGetLastError(), "decode_kernel launch");
 }
 

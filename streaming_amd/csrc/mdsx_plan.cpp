@@ -167,6 +167,27 @@ int parse_encoding(const std::string& enc, ColumnSpec* c) {
   return MDSX_OK;
 }
 
+// Tuning knobs for measurements: MDSX_TUNE="tile=64,unroll=8,nt=1" (read at plan creation).
+void apply_tuning(mdsx_plan* p) {
+  const char* env = std::getenv("MDSX_TUNE");
+  if (!env) return;
+  for (const std::string& kv : split(env, ',')) {
+    size_t eq = kv.find('=');
+    if (eq == std::string::npos) continue;
+    std::string key = strip(kv.substr(0, eq));
+    int64_t v = 0;
+    if (!parse_py_int(kv.substr(eq + 1), &v)) continue;
+    if (key == "tile" && (v == 64 || v == 128 || v == 256)) {
+      int64_t per_row = 4 * int64_t(p->ncols) + 12 * int64_t(p->nvar);
+      if (per_row * v <= 64 * 1024) p->tile_rows = int(v);
+    } else if (key == "unroll" && (v == 2 || v == 4 || v == 8)) {
+      p->unroll = int(v);
+    } else if (key == "nt") {
+      p->nontemporal = v ? 1 : 0;
+    }
+  }
+}
+
 }  // namespace
 }  // namespace mdsx
 
@@ -233,6 +254,7 @@ int mdsx_plan_create(const char* const* encodings, const int64_t* column_sizes, 
   // and a u64 destination offset per row. Wide schemas get a smaller tile.
   int64_t per_row = 4 * int64_t(ncols) + 12 * int64_t(p->nvar);
   p->tile_rows = (per_row * 256 <= 48 * 1024) ? 256 : 64;
+  apply_tuning(p);
   *out = p;
   return MDSX_OK;
 }
