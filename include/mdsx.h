@@ -155,6 +155,12 @@ int mdsx_decode_shards(const mdsx_plan* plan, const uint8_t* d_batch,
                        uint32_t ntiles, uint64_t total_rows, const mdsx_column_out* outs,
                        void* d_workspace, void* stream);
 
+/* ---- diagnostics ---------------------------------------------------------------------------
+ * HBM roofline probe: a streaming 16-byte-per-lane device-to-device copy of `bytes` (multiple of
+ * 16, 16-byte aligned pointers) on `stream`. Not part of the decode path: it measures what a
+ * pure stream of the same bytes reaches on the device, reported beside the decode rate. */
+int mdsx_copy_probe(const void* d_src, void* d_dst, uint64_t bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

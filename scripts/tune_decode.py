@@ -70,6 +70,10 @@ def main():
     copy_dst = torch.empty_like(base_batch.buffer)
     times = {v: [] for v in args.variants}
     times['torch_copy'] = []
+    times['mdsx_copy_probe'] = []
+    from streaming_amd import _native
+    lib = _native.lib()
+    nprobe = (base_batch.buffer.numel() // 16) * 16
     for _ in range(args.rounds):
         for v, dec in decs.items():
             evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)]
@@ -85,10 +89,17 @@ def main():
         e.record()
         torch.cuda.synchronize()
         times['torch_copy'].append(s.elapsed_time(e) / args.iters)
+        stream = torch.cuda.current_stream().cuda_stream
+        s.record()
+        for _ in range(args.iters):
+            lib.mdsx_copy_probe(base_batch.buffer.data_ptr(), copy_dst.data_ptr(), nprobe, stream)
+        e.record()
+        torch.cuda.synchronize()
+        times['mdsx_copy_probe'].append(s.elapsed_time(e) / args.iters)
     res = {}
     for v, ts in times.items():
         ms = float(np.median(ts))
-        nbytes = 2 * base_batch.buffer.numel() if v == 'torch_copy' else R + W
+        nbytes = 2 * base_batch.buffer.numel() if v in ('torch_copy', 'mdsx_copy_probe') else R + W
         res[v] = {'median_ms': ms, 'min_ms': float(np.min(ts)), 'GBps': nbytes / ms / 1e6}
     print(json.dumps({'config': args.config, 'R': R, 'W': W, 'results': res}, indent=1))
 

@@ -54,6 +54,7 @@ EXPORTED_SYMBOLS = (
     'mdsx_workspace_bytes',
     'mdsx_scan_shards',
     'mdsx_decode_shards',
+    'mdsx_copy_probe',
 )
 
 
@@ -127,6 +128,8 @@ def _declare(handle: ctypes.CDLL) -> None:
         vp, vp, vp, c_int, vp, c_u32, c_u64,
         ctypes.POINTER(ColumnOut), vp, vp
     ]
+    handle.mdsx_copy_probe.restype = c_int
+    handle.mdsx_copy_probe.argtypes = [vp, vp, c_u64, vp]
 
 
 def lib() -> ctypes.CDLL:

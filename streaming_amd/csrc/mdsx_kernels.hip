@@ -546,6 +546,23 @@ int hip_check(hipError_t e, const char* what) {
   return mdsx::fail(MDSX_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// HBM roofline probe: a grid-stride 16-byte-per-lane copy (what a pure stream of the same bytes
+// achieves on this device), used to report the measured copy ceiling next to the decode rate.
+__global__ __launch_bounds__(kBlock) void copy_probe_kernel(const uint4* __restrict__ src,
+                                                            uint4* __restrict__ dst, uint64_t n) {
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    const uint4 a = ld16<true>(src + i), b = ld16<true>(src + i + stride),
+                c = ld16<true>(src + i + 2 * stride), d = ld16<true>(src + i + 3 * stride);
+    st16<true>(reinterpret_cast<uint64_t>(dst + i), a);
+    st16<true>(reinterpret_cast<uint64_t>(dst + i + stride), b);
+    st16<true>(reinterpret_cast<uint64_t>(dst + i + 2 * stride), c);
+    st16<true>(reinterpret_cast<uint64_t>(dst + i + 3 * stride), d);
+  }
+  for (; i < n; i += stride) st16<true>(reinterpret_cast<uint64_t>(dst + i), ld16<true>(src + i));
+}
+
 }  // namespace mdsx_kernels
 
 using namespace mdsx_kernels;
@@ -601,6 +618,20 @@ int mdsx_decode_shards(const mdsx_plan* plan, const uint8_t* d_batch,
   else
     hipLaunchKernelGGL((decode_kernel<4, false>), dim3(ntiles), dim3(kBlock), lds, s, a);
   return hip_check(hipGetLastError(), "decode_kernel launch");
+}
+
+int mdsx_copy_probe(const void* d_src, void* d_dst, uint64_t bytes, void* stream) {
+  if (!d_src || !d_dst || (bytes & 15) || (reinterpret_cast<uint64_t>(d_src) & 15) ||
+      (reinterpret_cast<uint64_t>(d_dst) & 15))
+    return mdsx::fail(MDSX_E_ARG, "mdsx_copy_probe: 16-byte aligned pointers and size required");
+  const uint64_t n = bytes / 16;
+  if (n == 0) return MDSX_OK;
+  const uint64_t want = (n + kBlock - 1) / kBlock;
+  const unsigned grid = unsigned(want < 256 * 8 ? want : 256 * 8);
+  hipLaunchKernelGGL(copy_probe_kernel, dim3(grid), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), static_cast<const uint4*>(d_src),
+                     static_cast<uint4*>(d_dst), n);
+  return hip_check(hipGetLastError(), "copy_probe_kernel launch");
 }
 
 }  // extern "C"
