@@ -106,7 +106,7 @@ int mdsx_plan_create(const char* const* encodings, const int64_t* column_sizes, 
 void mdsx_plan_destroy(mdsx_plan* plan);
 int mdsx_plan_num_columns(const mdsx_plan* plan);
 int mdsx_plan_num_var(const mdsx_plan* plan);
-/* Rows per tile for this schema (256, or 64 for very wide schemas). Tile t of shard s covers rows
+/* Rows per tile for this schema (64 by default). Tile t of shard s covers rows
  * [(t - tile0) * tile_rows, ...) of that shard; a shard has ceil(samples / tile_rows) tiles. */
 int mdsx_plan_tile_rows(const mdsx_plan* plan);
 /* kind (MDSX_KIND_*), bytes per row for FIXED (0 for var), element size in bytes (dtype size;

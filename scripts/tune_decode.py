@@ -52,8 +52,11 @@ def main():
         base_batch = stage_shards(shards, counts, Plan(*names))
     decs = {}
     for v in args.variants:
-        os.environ['MDSX_TUNE'] = v
-        plan = Plan(*names)
+        # 'enc=a|b|c' overrides the column encodings (e.g. read a str column as bytes)
+        knobs = [kv for kv in v.split(',') if not kv.startswith('enc=')]
+        encs = [kv[4:].split('|') for kv in v.split(',') if kv.startswith('enc=')]
+        os.environ['MDSX_TUNE'] = ','.join(knobs)
+        plan = Plan(names[0], encs[0] if encs else names[1], names[2])
         dec = BatchDecoder(plan, retile(base_batch, plan))
         out = dec.run()
         dec.check()
@@ -63,6 +66,8 @@ def main():
         else:
             assert np.array_equal(out['b'].values.cpu().numpy(), src['b_pool']), v
             assert np.array_equal(out['s'].values.cpu().numpy(), src['s_pool']), v
+            if out['s'].flags is not None:
+                assert int(out['s'].flags.sum()) == 0, v
             assert np.array_equal(out['n'].cpu().numpy(), src['n']), v
         decs[v] = dec
     R = base_batch.shard_bytes

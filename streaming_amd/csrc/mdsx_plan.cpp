@@ -178,7 +178,7 @@ void apply_tuning(mdsx_plan* p) {
     int64_t v = 0;
     if (!parse_py_int(kv.substr(eq + 1), &v)) continue;
     if (key == "tile" && (v == 64 || v == 128 || v == 256)) {
-      int64_t per_row = 4 * int64_t(p->ncols) + 12 * int64_t(p->nvar);
+      const int64_t per_row = 4 * int64_t(p->ncols) + 12 * int64_t(p->nvar);
       if (per_row * v <= 64 * 1024) p->tile_rows = int(v);
     } else if (key == "unroll" && (v == 2 || v == 4 || v == 8)) {
       p->unroll = int(v);
@@ -250,10 +250,12 @@ int mdsx_plan_create(const char* const* encodings, const int64_t* column_sizes, 
         c.kind = MDSX_KIND_BYTES;
     }
   }
-  // LDS per tile: a u32 source offset per (row, column), and for each ragged column a u32 length
-  // and a u64 destination offset per row. Wide schemas get a smaller tile.
-  int64_t per_row = 4 * int64_t(ncols) + 12 * int64_t(p->nvar);
-  p->tile_rows = (per_row * 256 <= 48 * 1024) ? 256 : 64;
+  // 64-row tiles (one workgroup each): 16 rows per wave, a fine enough grain that the last
+  // wave of workgroups leaves little of the chip idle (measured: scripts/tune_decode.py). LDS per
+  // tile: a u32 source offset per (row, column), and per ragged column a u32 length and a u64
+  // destination offset per row (<= 16.4 KiB at 64 columns).
+  p->tile_rows = 64;
+  p->nontemporal = 1;  // shard bytes are read once and outputs written once: stream them
   apply_tuning(p);
   *out = p;
   return MDSX_OK;

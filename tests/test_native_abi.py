@@ -48,9 +48,7 @@ def test_plan_for_every_golden_schema(name):
         if size:
             assert col.row_bytes == size
     assert plan.num_var == sum(1 for s in info['column_sizes'] if not s)
-    assert plan.tile_rows in (64, 256)
-    if name == 'wide':
-        assert plan.tile_rows == 64
+    assert plan.tile_rows in (64, 128, 256)
 
 
 def test_plan_kinds():
