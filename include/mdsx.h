@@ -61,9 +61,7 @@ extern "C" {
 
 typedef struct mdsx_plan mdsx_plan; /* opaque, host-side, immutable after creation               */
 
-/* One shard of a device batch. A batch is a single device buffer holding several shard files,
- * each starting at a 256-byte-aligned `offset`, with at least MDSX_BATCH_PAD bytes of readable
- * slack before the first and after the last shard. */
+/* One shard of a device batch (see mdsx_batch). */
 typedef struct mdsx_shard_desc {
   uint64_t offset;  /* byte offset of the shard file inside the batch buffer (multiple of 256)   */
   uint64_t bytes;   /* shard file size: index.json raw_data.bytes                               */
@@ -117,43 +115,54 @@ int mdsx_plan_column(const mdsx_plan* plan, int col, int* kind, int64_t* row_byt
  * returns 1 if every column is safe ('pkl' is not), 0 otherwise. */
 int mdsx_plan_is_safe(const mdsx_plan* plan);
 
+/* A device batch: one device buffer holding several shard files (each at a 256-byte-aligned
+ * offset, at least MDSX_BATCH_PAD bytes of readable slack before the first and after the last
+ * shard) plus its descriptor and tile tables. Host struct; the pointers are device pointers. */
+typedef struct mdsx_batch {
+  const uint8_t* data;            /* batch buffer                                                */
+  uint64_t bytes;                 /* its size in bytes                                           */
+  const mdsx_shard_desc* shards;  /* nshards descriptors                                         */
+  const uint32_t* tile_shard;     /* ntiles entries: the shard of each tile. Tiles never cross
+                                     shards: shard s owns tiles [tile0, tile0 + ceil(samples /
+                                     tile_rows)) and tile t covers rows (t - tile0) * tile_rows.. */
+  int32_t nshards;
+  uint32_t ntiles;
+  uint64_t rows;                  /* rows of the batch (sum of samples)                          */
+} mdsx_batch;
+
 /* ---- workspace ----------------------------------------------------------------------------- */
-/* Bytes of device workspace a scan/decode of `ntiles` tiles needs (status record + per-tile
- * ragged-column sums). 256-byte aligned pointer expected. */
-uint64_t mdsx_workspace_bytes(const mdsx_plan* plan, uint32_t ntiles);
+/* Bytes of device workspace (256-byte aligned) the scan and decode of `batch` need: the status
+ * record, per-tile ragged sums, per-row source addresses and the gather-tile row map of every
+ * ragged column. */
+uint64_t mdsx_workspace_bytes(const mdsx_plan* plan, const mdsx_batch* batch);
 
 /* ---- the hot path ---------------------------------------------------------------------------
  * Pass 1. Resets the status record in the workspace (for an all-fixed plan that is all it
- * does), then, for variable-size columns, replaces the per-sample head
- * parse of MDSReader.decode_sample (mds/reader.py:111-118) and the offsets-table read of
+ * does), then, for variable-size columns, replaces the per-sample head parse of
+ * MDSReader.decode_sample (mds/reader.py:111-118) and the offsets-table read of
  * MDSReader.get_sample_data (mds/reader.py:128-149), over whole shards: reads offsets[] and every
- * sample's u32 size head, checks the ranges, and writes, for every ragged column, the per-row
- * byte offsets (outs[c].offsets, int64[rows+1]) and the column total (d_totals[v] for the v-th
- * variable column, int64, device) so the caller can size the value buffers.
- *   d_batch     : device batch buffer (shard files at desc.offset)
- *   d_shards    : device array of nshards descriptors
- *   d_tile_shard: device uint32[ntiles], the shard of each tile (tiles never cross shards;
- *                 shard s owns tiles [tile0, tile0 + ceil(samples / tile_rows)))
- *   total_rows  : rows of the batch (sum of samples); offsets[total_rows] receives the total
+ * sample's u32 size head, checks the ranges, and writes, for every ragged column, per-row local
+ * offsets into outs[c].offsets (int64[rows + 1]; made final by pass 2) and the column total
+ * (d_totals[v] for the v-th variable column, int64, device; outs[c].offsets[rows] as well) so
+ * the caller can size the value buffers.
  *   outs        : HOST array of plan->ncols column outputs (device pointers inside); only
  *                 .offsets of variable columns is used by this pass
- *   d_workspace : device scratch of mdsx_workspace_bytes(plan, ntiles) bytes
- *   d_totals    : device int64[num_var] (may be NULL if the caller does not need the totals)  */
-int mdsx_scan_shards(const mdsx_plan* plan, const uint8_t* d_batch,
-                     const mdsx_shard_desc* d_shards, int nshards, const uint32_t* d_tile_shard,
-                     uint32_t ntiles, uint64_t total_rows, const mdsx_column_out* outs,
-                     void* d_workspace, int64_t* d_totals, void* stream);
+ *   d_workspace : device scratch of at least mdsx_workspace_bytes(plan, batch) bytes
+ *   d_totals    : device int64[num_var] (may be NULL)                                          */
+int mdsx_scan_shards(const mdsx_plan* plan, const mdsx_batch* batch, const mdsx_column_out* outs,
+                     void* d_workspace, uint64_t workspace_bytes, int64_t* d_totals,
+                     void* stream);
 
 /* Pass 2. Replaces MDSReader.get_sample_data + decode_sample + mds_decode for every sample of
  * every shard in the batch (mds/reader.py:103-149, encodings.py:62-397,760-773): gathers each
- * column's bytes of every sample into its output (fixed columns as dtype rows, ragged columns as
- * packed values at the offsets from pass 1) and flags invalid UTF-8 rows of str columns.
- * mdsx_scan_shards must have run on the same stream with the same arguments and workspace
- * (every plan: it resets the status record this pass reports into). */
-int mdsx_decode_shards(const mdsx_plan* plan, const uint8_t* d_batch,
-                       const mdsx_shard_desc* d_shards, int nshards, const uint32_t* d_tile_shard,
-                       uint32_t ntiles, uint64_t total_rows, const mdsx_column_out* outs,
-                       void* d_workspace, void* stream);
+ * column's bytes of every sample into its output -- fixed columns as dtype rows, ragged columns
+ * as packed values at the final offsets -- and flags the str rows that are not well-formed UTF-8
+ * (where the reference's bytes.decode('utf-8') raises). outs[c].capacity of a ragged column must
+ * be at least its scanned total. mdsx_scan_shards must have run on the same stream with the same
+ * batch and workspace (every plan: it resets the status record this pass reports into). */
+int mdsx_decode_shards(const mdsx_plan* plan, const mdsx_batch* batch,
+                       const mdsx_column_out* outs, void* d_workspace, uint64_t workspace_bytes,
+                       void* stream);
 
 /* ---- diagnostics ---------------------------------------------------------------------------
  * HBM roofline probe: a streaming 16-byte-per-lane device-to-device copy of `bytes` (multiple of

@@ -19,7 +19,7 @@ import torch  # noqa: F401  (must be loaded before libmdsx.so, see module docstr
 __all__ = [
     'NativeLibraryError', 'MDSX_OK', 'MDSX_E_ARG', 'MDSX_E_ENCODING', 'MDSX_E_HEADER',
     'MDSX_E_BOUNDS', 'MDSX_E_HIP', 'MDSX_E_CAPACITY', 'MDSX_E_EMPTY', 'KIND_FIXED', 'KIND_BYTES',
-    'KIND_STR', 'KIND_NDARRAY', 'ShardDesc', 'ColumnOut', 'Status', 'lib', 'lib_path',
+    'KIND_STR', 'KIND_NDARRAY', 'ShardDesc', 'ColumnOut', 'Batch', 'Status', 'lib', 'lib_path',
     'EXPORTED_SYMBOLS', 'raise_for_code'
 ]
 
@@ -74,6 +74,13 @@ class ColumnOut(ctypes.Structure):
                 ('capacity', ctypes.c_uint64)]
 
 
+class Batch(ctypes.Structure):
+    """``mdsx_batch``."""
+    _fields_ = [('data', ctypes.c_void_p), ('bytes', ctypes.c_uint64), ('shards', ctypes.c_void_p),
+                ('tile_shard', ctypes.c_void_p), ('nshards', ctypes.c_int32),
+                ('ntiles', ctypes.c_uint32), ('rows', ctypes.c_uint64)]
+
+
 class Status(ctypes.Structure):
     """``mdsx_status``."""
     _fields_ = [('code', ctypes.c_int32), ('shard', ctypes.c_int32), ('row', ctypes.c_int32),
@@ -82,6 +89,7 @@ class Status(ctypes.Structure):
 
 assert ctypes.sizeof(ShardDesc) == 32
 assert ctypes.sizeof(ColumnOut) == 32
+assert ctypes.sizeof(Batch) == 48
 
 _here = os.path.dirname(os.path.abspath(__file__))
 lib_path = os.path.join(_here, 'lib', 'libmdsx.so')
@@ -116,18 +124,13 @@ def _declare(handle: ctypes.CDLL) -> None:
         ctypes.POINTER(ctypes.c_int64),
         ctypes.POINTER(c_int)
     ]
+    pb = ctypes.POINTER(Batch)
     handle.mdsx_workspace_bytes.restype = c_u64
-    handle.mdsx_workspace_bytes.argtypes = [vp, c_u32]
+    handle.mdsx_workspace_bytes.argtypes = [vp, pb]
     handle.mdsx_scan_shards.restype = c_int
-    handle.mdsx_scan_shards.argtypes = [
-        vp, vp, vp, c_int, vp, c_u32, c_u64,
-        ctypes.POINTER(ColumnOut), vp, vp, vp
-    ]
+    handle.mdsx_scan_shards.argtypes = [vp, pb, ctypes.POINTER(ColumnOut), vp, c_u64, vp, vp]
     handle.mdsx_decode_shards.restype = c_int
-    handle.mdsx_decode_shards.argtypes = [
-        vp, vp, vp, c_int, vp, c_u32, c_u64,
-        ctypes.POINTER(ColumnOut), vp, vp
-    ]
+    handle.mdsx_decode_shards.argtypes = [vp, pb, ctypes.POINTER(ColumnOut), vp, c_u64, vp]
     handle.mdsx_copy_probe.restype = c_int
     handle.mdsx_copy_probe.argtypes = [vp, vp, c_u64, vp]
 

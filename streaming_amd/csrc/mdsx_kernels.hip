@@ -11,12 +11,18 @@
 //                        per-row lengths of every ragged column, block exclusive scan (wave64
 //                        shuffles + LDS), per-tile totals.                      (ragged plans only)
 //   scan_totals_kernel   one workgroup per ragged column: exclusive scan of the tile totals.
-//   decode_kernel        one workgroup per tile: per-row column boundaries into LDS, small fixed
-//                        columns gathered one row per lane, every other column copied one row per
-//                        wave with 16-byte aligned loads and stores: the source is realigned in
-//                        registers (v_alignbyte funnel over the neighbour lane's chunk), so HBM is
-//                        read and written in whole 1 KiB wave transactions whatever the byte
-//                        alignment of the sample. str columns are UTF-8 validated in the same pass.
+//   decode_kernel        one workgroup per tile: per-row column boundaries into LDS; fixed columns
+//                        of <= 16 bytes gathered one row per lane; larger fixed columns copied one
+//                        row per wave with 16-byte aligned loads and stores, the source realigned in
+//                        registers (v_alignbyte funnel over the neighbour lane's chunk); for ragged
+//                        columns: final offsets, each row's source address and the row that starts
+//                        every 8 KiB output tile.
+//   gather_ragged_kernel one workgroup per 8 KiB tile of a ragged column's packed output
+//                        (destination-major): every lane writes whole aligned 16-byte chunks,
+//                        assembled from the row(s) that cover them (binary search over the tile's
+//                        rows staged in LDS), so short and long rows keep all 64 lanes busy; str
+//                        columns are UTF-8 validated in the same pass, flagging rows Python's
+//                        strict decoder would reject.
 //
 // Every load stays inside [shard - 32, shard + bytes + 32): the batch buffer carries
 // MDSX_BATCH_PAD bytes of slack around its shards, and every sample range is checked against
@@ -30,8 +36,11 @@
 
 namespace mdsx_kernels {
 
-constexpr int kBlock = 256;   // 4 waves
-constexpr int kSmallMax = 16; // fixed columns up to this many bytes: one row per lane
+constexpr int kBlock = 256;                     // 4 waves
+constexpr int kSmallMax = 16;                   // fixed columns <= 16 B: one row per lane
+constexpr int kGatherChunks = 2;                // 16-byte chunks per lane in gather_ragged_kernel
+constexpr uint64_t kGatherTile = uint64_t(kBlock) * 16 * kGatherChunks;  // 8 KiB per workgroup
+constexpr int kGatherRows = 1024;               // rows of a gather tile staged in LDS
 
 struct DevCol {
   void* data;
@@ -51,13 +60,17 @@ struct DevArgs {
   int64_t* tile_total;   // [nvar][ntiles]
   int64_t* tile_prefix;  // [nvar][ntiles]
   int64_t* totals;       // [nvar] or null
-  uint64_t total_rows;
+  uint64_t* src_abs;     // [nvar][rows]  byte index into the batch of each row's ragged value
+  uint32_t* row_map;     // [nvar][map_len] first row of every gather tile
+  uint64_t map_len;
+  uint64_t rows;
   uint32_t ntiles;
   int32_t nshards;
   int32_t ncols;
   int32_t nvar;
   int32_t tile_rows;
   int32_t pad_;
+  uint32_t gather_block0[MDSX_MAX_COLUMNS + 1];  // first gather workgroup of each ragged column
   DevCol cols[MDSX_MAX_COLUMNS];
 };
 
@@ -217,7 +230,7 @@ __global__ __launch_bounds__(kBlock) void scan_totals_kernel(const DevArgs a) {
   if (threadIdx.x == 0) {
     if (a.totals) a.totals[vi] = carry;
     for (int c = 0; c < a.ncols; ++c)
-      if (a.cols[c].var_index == vi) a.cols[c].offsets[a.total_rows] = carry;
+      if (a.cols[c].var_index == vi) a.cols[c].offsets[a.rows] = carry;
   }
 }
 
@@ -241,6 +254,18 @@ __device__ __forceinline__ uint4 funnel16(const uint4 lo, const uint4 hi, uint32
   }
 }
 
+// The same with a per-lane shift (selects instead of a uniform branch).
+__device__ __forceinline__ uint4 funnel16_lane(const uint4 lo, const uint4 hi, uint32_t sh) {
+  const uint32_t q = sh >> 2, r = sh & 3;
+  const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  uint32_t s[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k)
+    s[k] = q == 0 ? w[k] : q == 1 ? w[k + 1] : q == 2 ? w[k + 2] : w[k + 3];
+  return make_uint4(alignbyte(s[1], s[0], r), alignbyte(s[2], s[1], r), alignbyte(s[3], s[2], r),
+                    alignbyte(s[4], s[3], r));
+}
+
 __device__ __forceinline__ uint32_t byte_of(const uint4& v, int j) {
   const uint32_t w = (j < 4) ? v.x : (j < 8) ? v.y : (j < 12) ? v.z : v.w;
   return (w >> (8 * (j & 3))) & 0xffu;
@@ -256,46 +281,27 @@ __device__ __forceinline__ uint4 readlane0(const uint4 v) {
                     __builtin_amdgcn_readlane(v.z, 0), __builtin_amdgcn_readlane(v.w, 0));
 }
 
-// Strict UTF-8 well-formedness (what bytes.decode('utf-8') accepts, encodings.py:80-81) of the
-// 16 bytes of `v` at segment positions pos0 .. pos0+15, given the 3 bytes before them in pw
-// (bytes 1..3 of the previous chunk's last dword). Bytes at negative positions are zero.
-__device__ __forceinline__ bool utf8_chunk_bad(const uint4 v, uint32_t pw, int64_t pos0,
-                                               int64_t len) {
-  uint32_t p1 = (pw >> 24) & 0xffu, p2 = (pw >> 16) & 0xffu, p3 = (pw >> 8) & 0xffu;
-  const bool ascii = ((v.x | v.y | v.z | v.w) & 0x80808080u) == 0;
-  if (ascii && p1 < 0xC0u && p2 < 0xE0u && p3 < 0xF0u) return false;
-  bool bad = false;
+// Byte mask of bytes [a, b) of a 16-byte chunk (0 <= a <= b <= 16).
+__device__ __forceinline__ uint4 byte_mask(uint32_t a, uint32_t b) {
+  uint32_t m[4];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const uint32_t b = byte_of(v, j);
-    const int64_t pos = pos0 + j;
-    if (pos >= 0 && pos < len) {
-      const bool cont = (b & 0xC0u) == 0x80u;
-      const bool need = p1 >= 0xC0u || p2 >= 0xE0u || p3 >= 0xF0u;
-      bad |= cont != need;
-      bad |= b == 0xC0u || b == 0xC1u || b >= 0xF5u;
-      bad |= (p1 == 0xE0u && b < 0xA0u) || (p1 == 0xEDu && b > 0x9Fu) ||
-             (p1 == 0xF0u && b < 0x90u) || (p1 == 0xF4u && b > 0x8Fu);
-      bad |= (b >= 0xC0u && pos + 1 >= len) || (b >= 0xE0u && pos + 2 >= len) ||
-             (b >= 0xF0u && pos + 3 >= len);
-    }
-    p3 = p2;
-    p2 = p1;
-    p1 = b;
+  for (int j = 0; j < 4; ++j) {
+    const int lo = min(max(int(a) - 4 * j, 0), 4), hi = min(max(int(b) - 4 * j, 0), 4);
+    const uint64_t mh = (uint64_t(1) << (8 * hi)) - 1, ml = (uint64_t(1) << (8 * lo)) - 1;
+    m[j] = uint32_t(mh & ~ml);
   }
-  return bad;
+  return make_uint4(m[0], m[1], m[2], m[3]);
 }
 
 // One wave copies `len` bytes from src to dst (any alignment of either). Destination chunks are
 // 16-byte aligned; lane k of a step owns chunk k. Its source bytes straddle two aligned 16-byte
 // source chunks: it loads the first and takes the second from lane k+1 (lane 63 from lane 0 of
 // the next step, or one extra load at the end of a batch). Partial chunks at the two ends are
-// written byte by byte. With kUtf8, returns whether the segment is not well-formed UTF-8
-// (wave-uniform).
-template <bool kUtf8, int kUnroll, bool kNT>
-__device__ __forceinline__ bool wave_copy(const uint8_t* src, uint8_t* dst, uint64_t len,
+// written byte by byte.
+template <int kUnroll, bool kNT>
+__device__ __forceinline__ void wave_copy(const uint8_t* src, uint8_t* dst, uint64_t len,
                                           int lane) {
-  if (len == 0) return false;
+  if (len == 0) return;
   const uint64_t d0 = reinterpret_cast<uint64_t>(dst);
   const uint64_t dend = d0 + len;
   const uint64_t dbeg = d0 & ~uint64_t(15);
@@ -304,8 +310,6 @@ __device__ __forceinline__ bool wave_copy(const uint8_t* src, uint8_t* dst, uint
   const uint32_t sh = uint32_t(sfirst & 15);
   const uint4* sal = reinterpret_cast<const uint4*>(sfirst & ~uint64_t(15));
   const uint64_t nload = nchunks + (sh ? 1 : 0);
-  bool bad = false;
-  uint32_t carry = 0;  // last dword of the previous chunk (UTF-8 look-back)
   for (uint64_t base = 0; base < nchunks; base += 64 * kUnroll) {
     uint4 lo[kUnroll];
 #pragma unroll
@@ -329,23 +333,8 @@ __device__ __forceinline__ bool wave_copy(const uint8_t* src, uint8_t* dst, uint
         if (lane == 63) hi = nxt;
         out = funnel16(lo[u], hi, sh);
       }
-      const uint64_t D = dbeg + 16 * k;
-      if (kUtf8) {
-        uint4 vout = out;
-        if (k == 0 && D < d0) {  // zero the bytes before the segment start
-          const uint32_t head = uint32_t(d0 - D);
-          const uint32_t m0 = head >= 4 ? 0u : (0xffffffffu << (8 * head));
-          const uint32_t m1 = head >= 8 ? 0u : head <= 4 ? 0xffffffffu : (0xffffffffu << (8 * (head - 4)));
-          const uint32_t m2 = head >= 12 ? 0u : head <= 8 ? 0xffffffffu : (0xffffffffu << (8 * (head - 8)));
-          const uint32_t m3 = head <= 12 ? 0xffffffffu : (0xffffffffu << (8 * (head - 12)));
-          vout = make_uint4(vout.x & m0, vout.y & m1, vout.z & m2, vout.w & m3);
-        }
-        uint32_t pw = __shfl_up(vout.w, 1);
-        if (lane == 0) pw = carry;
-        carry = __shfl(vout.w, 63);
-        if (k < nchunks) bad |= utf8_chunk_bad(vout, pw, int64_t(D) - int64_t(d0), int64_t(len));
-      }
       if (k < nchunks) {
+        const uint64_t D = dbeg + 16 * k;
         if (D >= d0 && D + 16 <= dend) {
           st16<kNT>(D, out);
         } else {
@@ -358,8 +347,6 @@ __device__ __forceinline__ bool wave_copy(const uint8_t* src, uint8_t* dst, uint
       }
     }
   }
-  if (kUtf8) return __any(bad);
-  return false;
 }
 
 // Fixed column of 1..16 bytes: one row per lane. dst is aligned to the largest power of two
@@ -392,15 +379,14 @@ __device__ __forceinline__ void gather_small(const uint8_t* p, uint8_t* dst, uin
   }
 }
 
-// Pass 2: decode every column of every row of a tile.
+// Pass 2: per-row column boundaries; fixed columns decoded; ragged columns prepared for the
+// destination-major gather (final offsets, per-row source addresses, gather-tile row map).
 template <int kUnroll, bool kNT>
 __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int TR = a.tile_rows;
-  uint64_t* s_vdst = reinterpret_cast<uint64_t*>(smem);       // [nvar][TR] destination offsets
-  uint32_t* s_src = reinterpret_cast<uint32_t*>(s_vdst + a.nvar * TR);  // [ncols][TR] src offsets
-  uint32_t* s_vlen = s_src + a.ncols * TR;                      // [nvar][TR] ragged lengths
-  uint8_t* s_ok = reinterpret_cast<uint8_t*>(s_vlen + a.nvar * TR);     // [TR]
+  uint32_t* s_src = reinterpret_cast<uint32_t*>(smem);  // [ncols][TR] src offsets in the shard
+  uint8_t* s_ok = reinterpret_cast<uint8_t*>(s_src + a.ncols * TR);  // [TR]
 
   const TileView v = tile_view(a);
   const int t = threadIdx.x;
@@ -432,11 +418,9 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
     uint64_t pos = uint64_t(b) + 4ull * a.nvar;
     for (int c = 0; c < a.ncols; ++c) {
       const DevCol& col = a.cols[c];
-      uint64_t len = col.row_bytes;
-      if (col.var_index >= 0) {
-        len = ok ? load_u32_any(v.shard + b + 4u * uint32_t(col.var_index)) : 0u;
-        s_vlen[col.var_index * TR + t] = uint32_t(len);
-      }
+      const uint64_t len = col.var_index < 0 ? uint64_t(col.row_bytes)
+                           : ok ? load_u32_any(v.shard + b + 4u * uint32_t(col.var_index))
+                                : 0u;
       s_src[c * TR + t] = uint32_t(pos);
       pos += len;
     }
@@ -444,17 +428,28 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
       ok = false;
       rc = MDSX_E_BOUNDS;
     }
-    // Ragged destinations: tile prefix + the local offset the scan pass left in offsets[row].
+    // Ragged columns: final offset = tile prefix + the local offset the scan pass left in
+    // offsets[row]; the row's source address; the gather tiles whose first byte it holds.
     for (int c = 0; c < a.ncols; ++c) {
       const DevCol& col = a.cols[c];
       if (col.var_index < 0) continue;
       const int vi = col.var_index;
       const int64_t off = a.tile_prefix[uint64_t(vi) * a.ntiles + blockIdx.x] + col.offsets[row];
       col.offsets[row] = off;
-      s_vdst[vi * TR + t] = uint64_t(off);
-      if (ok && uint64_t(off) + s_vlen[vi * TR + t] > col.capacity) {
+      if (col.flags) col.flags[row] = 0;
+      if (!ok) continue;
+      const uint64_t len = load_u32_any(v.shard + b + 4u * uint32_t(vi));
+      if (uint64_t(off) + len > col.capacity) {
         report(a.status, MDSX_E_CAPACITY, v.shard_idx, int(i), c);
         ok = false;
+        continue;
+      }
+      a.src_abs[uint64_t(vi) * a.rows + row] = v.d.offset + s_src[c * TR + t];
+      if (len) {
+        uint32_t* map = a.row_map + uint64_t(vi) * a.map_len;
+        for (uint64_t g = (uint64_t(off) + kGatherTile - 1) / kGatherTile;
+             g * kGatherTile < uint64_t(off) + len && g < a.map_len; ++g)
+          map[g] = uint32_t(row);
       }
     }
     if (!ok && rc != MDSX_OK) report(a.status, rc, v.shard_idx, int(i), -1);
@@ -473,54 +468,245 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
     }
   }
 
-  // ---- large fixed and ragged columns: one row per wave
+  // ---- large fixed columns: one row per wave
   for (int r = wave; r < int(v.nrows); r += kBlock / 64) {
     if (!s_ok[r]) continue;  // wave-uniform
     const uint64_t row = v.d.row0 + v.r0 + r;
     for (int c = 0; c < a.ncols; ++c) {
       const DevCol& col = a.cols[c];
-      const uint8_t* src = v.shard + s_src[c * TR + r];
-      if (col.var_index < 0) {
-        if (col.row_bytes <= uint32_t(kSmallMax)) continue;
-        wave_copy<false, kUnroll, kNT>(src, static_cast<uint8_t*>(col.data) + row * col.row_bytes,
-                         col.row_bytes, lane);
-      } else {
-        const int vi = col.var_index;
-        uint8_t* dst = static_cast<uint8_t*>(col.data) + s_vdst[vi * TR + r];
-        const uint64_t len = s_vlen[vi * TR + r];
-        if (col.kind == MDSX_KIND_STR) {
-          const bool bad = wave_copy<true, kUnroll, kNT>(src, dst, len, lane);
-          if (lane == 0 && col.flags) col.flags[row] = bad ? 1 : 0;
-        } else {
-          wave_copy<false, kUnroll, kNT>(src, dst, len, lane);
-        }
-      }
+      if (col.var_index >= 0 || col.row_bytes <= uint32_t(kSmallMax)) continue;
+      wave_copy<kUnroll, kNT>(v.shard + s_src[c * TR + r],
+                              static_cast<uint8_t*>(col.data) + row * col.row_bytes,
+                              col.row_bytes, lane);
     }
   }
 }
 
 // ---------------------------------------------------------------------------------------------
-int build_args(const mdsx_plan* plan, const uint8_t* d_batch, const mdsx_shard_desc* d_shards,
-               int nshards, const uint32_t* d_tile_shard, uint32_t ntiles,
-               const mdsx_column_out* outs, void* d_workspace, int64_t* d_totals,
-               DevArgs* a) {
-  if (!plan || !d_batch || !d_shards || !d_tile_shard || !d_workspace || nshards <= 0)
+// Pass 3: ragged columns, destination-major. Rows of a gather tile are addressed through an
+// accessor: staged in LDS when they fit (the common case), else read from global memory.
+struct RowsLds {
+  const int64_t* off;    // [n + 1]
+  const uint64_t* src;   // [n]
+  __device__ __forceinline__ int64_t o(int i) const { return off[i]; }
+  __device__ __forceinline__ uint64_t s(int i) const { return src[i]; }
+};
+
+struct RowsGlobal {
+  const int64_t* off;    // offsets + r0
+  const uint64_t* src;   // src_abs + r0
+  __device__ __forceinline__ int64_t o(int i) const { return off[i]; }
+  __device__ __forceinline__ uint64_t s(int i) const { return src[i]; }
+};
+
+// Index (in [0, n)) of the row holding byte D: the last i with o(i) <= D.
+template <class Rows>
+__device__ __forceinline__ int find_row(const Rows& R, int n, int64_t D) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (R.o(mid) <= D) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// The 16 output bytes at column position D (D % 16 == 0), assembled from the rows covering them
+// starting at row index j. Bytes past the column end are zero.
+template <bool kNT, class Rows>
+__device__ __forceinline__ uint4 assemble(const Rows& R, int n, int j, int64_t D,
+                                          const uint8_t* batch) {
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  for (; j < n && R.o(j) < D + 16; ++j) {
+    const int64_t ro = R.o(j), re = R.o(j + 1);
+    const int64_t a = max(D, ro), b = min(D + 16, re);
+    if (b <= a) continue;
+    const uint64_t s0 = reinterpret_cast<uint64_t>(batch) + R.s(j) + uint64_t(D - ro);
+    const uint4* al = reinterpret_cast<const uint4*>(s0 & ~uint64_t(15));
+    const uint32_t sh = uint32_t(s0 & 15);
+    const uint4 lo = ld16<kNT>(al);
+    const uint4 hi = sh ? ld16<kNT>(al + 1) : make_uint4(0, 0, 0, 0);
+    const uint4 val = sh ? funnel16_lane(lo, hi, sh) : lo;
+    const uint4 m = byte_mask(uint32_t(a - D), uint32_t(b - D));
+    acc = make_uint4((acc.x & ~m.x) | (val.x & m.x), (acc.y & ~m.y) | (val.y & m.y),
+                     (acc.z & ~m.z) | (val.z & m.z), (acc.w & ~m.w) | (val.w & m.w));
+  }
+  return acc;
+}
+
+// Strict UTF-8 well-formedness (what bytes.decode('utf-8') accepts, encodings.py:80-81) of the
+// 16 bytes at column position D, rows tracked from row index j; pw holds the 4 bytes before D.
+// Flags every row with an invalid byte (rows are flagged 0 beforehand by decode_kernel).
+template <class Rows>
+__device__ __forceinline__ void utf8_check(const Rows& R, int n, int j, int64_t D, int64_t tot,
+                                           const uint4 v, uint32_t pw, uint8_t* flags,
+                                           uint64_t row0) {
+  uint32_t p1 = (pw >> 24) & 0xffu, p2 = (pw >> 16) & 0xffu, p3 = (pw >> 8) & 0xffu;
+  const bool ascii = ((v.x | v.y | v.z | v.w) & 0x80808080u) == 0;
+  if (ascii && p1 < 0xC0u && p2 < 0xE0u && p3 < 0xF0u) return;
+  // look-back bytes that precede the row start are not part of the row
+  const int64_t dist = D - R.o(j);
+  if (dist < 3) p3 = 0;
+  if (dist < 2) p2 = 0;
+  if (dist < 1) p1 = 0;
+  int64_t rend = R.o(j + 1);
+  bool bad = false;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int64_t P = D + k;
+    if (P >= tot) break;
+    if (P >= rend) {  // next non-empty row: flush the previous row's verdict, reset look-back
+      if (bad) flags[row0 + j] = 1;
+      bad = false;
+      do {
+        ++j;
+        rend = R.o(j + 1);
+      } while (P >= rend && j + 1 < n);
+      p1 = p2 = p3 = 0;
+    }
+    const uint32_t b = byte_of(v, k);
+    const bool cont = (b & 0xC0u) == 0x80u;
+    const bool need = p1 >= 0xC0u || p2 >= 0xE0u || p3 >= 0xF0u;
+    const int64_t left = rend - P;  // bytes from P to the row end, >= 1
+    bad |= cont != need;
+    bad |= b == 0xC0u || b == 0xC1u || b >= 0xF5u;
+    bad |= (p1 == 0xE0u && b < 0xA0u) || (p1 == 0xEDu && b > 0x9Fu) ||
+           (p1 == 0xF0u && b < 0x90u) || (p1 == 0xF4u && b > 0x8Fu);
+    bad |= (b >= 0xC0u && left <= 1) || (b >= 0xE0u && left <= 2) || (b >= 0xF0u && left <= 3);
+    p3 = p2;
+    p2 = p1;
+    p1 = b;
+  }
+  if (bad) flags[row0 + j] = 1;
+}
+
+template <bool kNT, class Rows>
+__device__ __forceinline__ void gather_tile(const DevArgs& a, const DevCol& col, const Rows& R,
+                                            int n, uint64_t r0, int64_t T0, int64_t tot,
+                                            uint32_t* s_last) {
+  const bool utf8 = col.kind == MDSX_KIND_STR && col.flags;
+  uint8_t* out = static_cast<uint8_t*>(col.data);
+  uint4 val[kGatherChunks];
+  int jrow[kGatherChunks];
+#pragma unroll
+  for (int k = 0; k < kGatherChunks; ++k) {
+    const int c = threadIdx.x + kBlock * k;
+    const int64_t D = T0 + 16 * c;
+    val[k] = make_uint4(0, 0, 0, 0);
+    jrow[k] = 0;
+    if (D < tot) {
+      jrow[k] = find_row(R, n, D);
+      val[k] = assemble<kNT>(R, n, jrow[k], D, a.batch);
+      const uint64_t dst = reinterpret_cast<uint64_t>(out) + uint64_t(D);
+      if (uint64_t(D) + 16 <= col.capacity) {
+        st16<kNT>(dst, val[k]);
+      } else {
+        for (int b = 0; b < 16 && uint64_t(D) + b < col.capacity; ++b)
+          out[D + b] = uint8_t(byte_of(val[k], b));
+      }
+    }
+    if (utf8) s_last[c] = val[k].w;
+  }
+  if (!utf8) return;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kGatherChunks; ++k) {
+    const int c = threadIdx.x + kBlock * k;
+    const int64_t D = T0 + 16 * c;
+    if (D >= tot) continue;
+    uint32_t pw;
+    if (c > 0) {
+      pw = s_last[c - 1];
+    } else if (D > R.o(0)) {  // bytes before the tile inside the tile's first row
+      const uint4 prev = assemble<kNT>(R, 1, 0, D - 16, a.batch);
+      pw = prev.w;
+    } else {
+      pw = 0;
+    }
+    utf8_check(R, n, jrow[k], D, tot, val[k], pw, col.flags, r0);
+  }
+}
+
+template <bool kNT>
+__global__ __launch_bounds__(kBlock) void gather_ragged_kernel(const DevArgs a) {
+  __shared__ __attribute__((aligned(16))) int64_t s_off[kGatherRows + 1];
+  __shared__ uint64_t s_src[kGatherRows];
+  __shared__ uint32_t s_last[kBlock * kGatherChunks];
+  // which ragged column / tile (block-uniform)
+  int vi = 0;
+  while (vi + 1 < a.nvar && blockIdx.x >= a.gather_block0[vi + 1]) ++vi;
+  int ci = 0;
+  while (a.cols[ci].var_index != vi) ++ci;
+  const DevCol& col = a.cols[ci];
+  const uint64_t g = blockIdx.x - a.gather_block0[vi];
+  const int64_t tot = col.offsets[a.rows];
+  const int64_t T0 = int64_t(g * kGatherTile);
+  if (T0 >= tot) return;
+  if (a.status->code != 0 || g + 1 >= a.map_len) return;  // decode failed: outputs are void
+  const uint32_t* map = a.row_map + uint64_t(vi) * a.map_len;
+  const uint64_t r0 = map[g];
+  const uint64_t r1 = (T0 + int64_t(kGatherTile) < tot) ? uint64_t(map[g + 1]) : a.rows - 1;
+  if (r0 >= a.rows || r1 >= a.rows || r1 < r0) return;  // never for a status-clean decode
+  const int n = int(r1 - r0 + 1);
+  const uint64_t* src = a.src_abs + uint64_t(vi) * a.rows;
+  if (n <= kGatherRows) {
+    for (int i = threadIdx.x; i <= n; i += kBlock) {
+      s_off[i] = col.offsets[r0 + i];
+      if (i < n) s_src[i] = src[r0 + i];
+    }
+    __syncthreads();
+    gather_tile<kNT>(a, col, RowsLds{s_off, s_src}, n, r0, T0, tot, s_last);
+  } else {
+    gather_tile<kNT>(a, col, RowsGlobal{col.offsets + r0, src + r0}, n, r0, T0, tot, s_last);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+struct Layout {
+  uint64_t tile_total, tile_prefix, src_abs, row_map, map_len, total;
+};
+
+__host__ uint64_t round256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
+
+Layout workspace_layout(const mdsx_plan* plan, const mdsx_batch* b) {
+  Layout L;
+  const uint64_t nv = uint64_t(plan->nvar);
+  L.map_len = b->bytes / kGatherTile + 2;
+  L.tile_total = 256;
+  L.tile_prefix = L.tile_total + round256(nv * b->ntiles * 8);
+  L.src_abs = L.tile_prefix + round256(nv * b->ntiles * 8);
+  L.row_map = L.src_abs + round256(nv * b->rows * 8);
+  L.total = L.row_map + round256(nv * L.map_len * 4);
+  return L;
+}
+
+int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out* outs,
+               void* d_workspace, uint64_t workspace_bytes, int64_t* d_totals, DevArgs* a) {
+  if (!plan || !b || !b->data || !b->shards || !b->tile_shard || !d_workspace ||
+      b->nshards <= 0)
     return mdsx::fail(MDSX_E_ARG, "mdsx: null argument or empty batch");
   if (plan->ncols > 0 && !outs) return mdsx::fail(MDSX_E_ARG, "mdsx: outs is NULL");
+  const Layout L = workspace_layout(plan, b);
+  if (workspace_bytes < L.total)
+    return mdsx::fail(MDSX_E_ARG, "mdsx: workspace smaller than mdsx_workspace_bytes()");
   std::memset(a, 0, sizeof(*a));
-  a->batch = d_batch;
-  a->shards = d_shards;
-  a->tile_shard = d_tile_shard;
+  a->batch = b->data;
+  a->shards = b->shards;
+  a->tile_shard = b->tile_shard;
   uint8_t* ws = static_cast<uint8_t*>(d_workspace);
   a->status = reinterpret_cast<mdsx_status*>(ws);
-  a->tile_total = reinterpret_cast<int64_t*>(ws + 256);
-  a->tile_prefix = a->tile_total + uint64_t(plan->nvar) * ntiles;
+  a->tile_total = reinterpret_cast<int64_t*>(ws + L.tile_total);
+  a->tile_prefix = reinterpret_cast<int64_t*>(ws + L.tile_prefix);
+  a->src_abs = reinterpret_cast<uint64_t*>(ws + L.src_abs);
+  a->row_map = reinterpret_cast<uint32_t*>(ws + L.row_map);
+  a->map_len = L.map_len;
   a->totals = d_totals;
-  a->ntiles = ntiles;
-  a->nshards = nshards;
+  a->rows = b->rows;
+  a->ntiles = b->ntiles;
+  a->nshards = b->nshards;
   a->ncols = plan->ncols;
   a->nvar = plan->nvar;
   a->tile_rows = plan->tile_rows;
+  uint32_t gblocks = 0;
   for (int c = 0; c < plan->ncols; ++c) {
     const mdsx::ColumnSpec& s = plan->cols[c];
     DevCol& d = a->cols[c];
@@ -538,6 +724,13 @@ int build_args(const mdsx_plan* plan, const uint8_t* d_batch, const mdsx_shard_d
         return mdsx::fail(MDSX_E_ARG, "mdsx: null offsets/data for a ragged column");
     }
   }
+  for (int v = 0; v < plan->nvar; ++v) {  // gather workgroups of each ragged column, in order
+    a->gather_block0[v] = gblocks;
+    for (int c = 0; c < plan->ncols; ++c)
+      if (plan->cols[c].var_index == v)
+        gblocks += uint32_t((outs[c].capacity + kGatherTile - 1) / kGatherTile);
+  }
+  a->gather_block0[plan->nvar] = gblocks;
   return MDSX_OK;
 }
 
@@ -569,20 +762,22 @@ using namespace mdsx_kernels;
 
 extern "C" {
 
-int mdsx_scan_shards(const mdsx_plan* plan, const uint8_t* d_batch,
-                     const mdsx_shard_desc* d_shards, int nshards, const uint32_t* d_tile_shard,
-                     uint32_t ntiles, uint64_t total_rows, const mdsx_column_out* outs,
-                     void* d_workspace, int64_t* d_totals, void* stream) {
+uint64_t mdsx_workspace_bytes(const mdsx_plan* plan, const mdsx_batch* batch) {
+  if (!plan || !batch) return 0;
+  return workspace_layout(plan, batch).total;
+}
+
+int mdsx_scan_shards(const mdsx_plan* plan, const mdsx_batch* batch, const mdsx_column_out* outs,
+                     void* d_workspace, uint64_t workspace_bytes, int64_t* d_totals,
+                     void* stream) {
   DevArgs a;
-  int rc = build_args(plan, d_batch, d_shards, nshards, d_tile_shard, ntiles, outs, d_workspace,
-                      d_totals, &a);
+  int rc = build_args(plan, batch, outs, d_workspace, workspace_bytes, d_totals, &a);
   if (rc != MDSX_OK) return rc;
-  a.total_rows = total_rows;
   hipStream_t s = static_cast<hipStream_t>(stream);
   rc = hip_check(hipMemsetAsync(d_workspace, 0, sizeof(mdsx_status), s), "hipMemsetAsync");
   if (rc != MDSX_OK || plan->nvar == 0) return rc;
-  if (ntiles > 0) {
-    hipLaunchKernelGGL(scan_tiles_kernel, dim3(ntiles), dim3(kBlock), 0, s, a);
+  if (a.ntiles > 0) {
+    hipLaunchKernelGGL(scan_tiles_kernel, dim3(a.ntiles), dim3(kBlock), 0, s, a);
     rc = hip_check(hipGetLastError(), "scan_tiles_kernel launch");
     if (rc != MDSX_OK) return rc;
   }
@@ -590,34 +785,37 @@ int mdsx_scan_shards(const mdsx_plan* plan, const uint8_t* d_batch,
   return hip_check(hipGetLastError(), "scan_totals_kernel launch");
 }
 
-int mdsx_decode_shards(const mdsx_plan* plan, const uint8_t* d_batch,
-                       const mdsx_shard_desc* d_shards, int nshards, const uint32_t* d_tile_shard,
-                       uint32_t ntiles, uint64_t total_rows, const mdsx_column_out* outs,
-                       void* d_workspace, void* stream) {
+int mdsx_decode_shards(const mdsx_plan* plan, const mdsx_batch* batch,
+                       const mdsx_column_out* outs, void* d_workspace, uint64_t workspace_bytes,
+                       void* stream) {
   DevArgs a;
-  int rc = build_args(plan, d_batch, d_shards, nshards, d_tile_shard, ntiles, outs, d_workspace,
-                      nullptr, &a);
+  int rc = build_args(plan, batch, outs, d_workspace, workspace_bytes, nullptr, &a);
   if (rc != MDSX_OK) return rc;
-  a.total_rows = total_rows;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (ntiles == 0) return MDSX_OK;
-  const size_t lds = size_t(plan->tile_rows) *
-                         (8 * size_t(plan->nvar) + 4 * size_t(plan->ncols) + 4 * size_t(plan->nvar) + 1) +
-                     16;
+  if (a.ntiles == 0) return MDSX_OK;
+  const size_t lds = size_t(plan->tile_rows) * (4 * size_t(plan->ncols) + 1) + 16;
   const int u = plan->unroll, nt = plan->nontemporal;
   if (u == 8 && nt)
-    hipLaunchKernelGGL((decode_kernel<8, true>), dim3(ntiles), dim3(kBlock), lds, s, a);
+    hipLaunchKernelGGL((decode_kernel<8, true>), dim3(a.ntiles), dim3(kBlock), lds, s, a);
   else if (u == 8)
-    hipLaunchKernelGGL((decode_kernel<8, false>), dim3(ntiles), dim3(kBlock), lds, s, a);
+    hipLaunchKernelGGL((decode_kernel<8, false>), dim3(a.ntiles), dim3(kBlock), lds, s, a);
   else if (u == 2 && nt)
-    hipLaunchKernelGGL((decode_kernel<2, true>), dim3(ntiles), dim3(kBlock), lds, s, a);
+    hipLaunchKernelGGL((decode_kernel<2, true>), dim3(a.ntiles), dim3(kBlock), lds, s, a);
   else if (u == 2)
-    hipLaunchKernelGGL((decode_kernel<2, false>), dim3(ntiles), dim3(kBlock), lds, s, a);
+    hipLaunchKernelGGL((decode_kernel<2, false>), dim3(a.ntiles), dim3(kBlock), lds, s, a);
   else if (nt)
-    hipLaunchKernelGGL((decode_kernel<4, true>), dim3(ntiles), dim3(kBlock), lds, s, a);
+    hipLaunchKernelGGL((decode_kernel<4, true>), dim3(a.ntiles), dim3(kBlock), lds, s, a);
   else
-    hipLaunchKernelGGL((decode_kernel<4, false>), dim3(ntiles), dim3(kBlock), lds, s, a);
-  return hip_check(hipGetLastError(), "decode_kernel launch");
+    hipLaunchKernelGGL((decode_kernel<4, false>), dim3(a.ntiles), dim3(kBlock), lds, s, a);
+  rc = hip_check(hipGetLastError(), "decode_kernel launch");
+  if (rc != MDSX_OK || plan->nvar == 0) return rc;
+  const uint32_t gblocks = a.gather_block0[plan->nvar];
+  if (gblocks == 0) return MDSX_OK;
+  if (nt)
+    hipLaunchKernelGGL((gather_ragged_kernel<true>), dim3(gblocks), dim3(kBlock), 0, s, a);
+  else
+    hipLaunchKernelGGL((gather_ragged_kernel<false>), dim3(gblocks), dim3(kBlock), 0, s, a);
+  return hip_check(hipGetLastError(), "gather_ragged_kernel launch");
 }
 
 int mdsx_copy_probe(const void* d_src, void* d_dst, uint64_t bytes, void* stream) {

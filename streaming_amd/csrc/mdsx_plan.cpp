@@ -282,11 +282,4 @@ int mdsx_plan_column(const mdsx_plan* plan, int col, int* kind, int64_t* row_byt
 
 int mdsx_plan_is_safe(const mdsx_plan* plan) { return plan && plan->safe ? 1 : 0; }
 
-uint64_t mdsx_workspace_bytes(const mdsx_plan* plan, uint32_t ntiles) {
-  if (!plan) return 0;
-  // [status: 256 B][tile totals: nvar * ntiles * 8][tile prefixes: nvar * ntiles * 8]
-  uint64_t per = uint64_t(plan->nvar) * ntiles * 8;
-  return 256 + ((2 * per + 255) & ~uint64_t(255));
-}
-
 }  // extern "C"

@@ -29,7 +29,7 @@ import torch
 
 from streaming_amd import _native
 from streaming_amd._native import (BATCH_PAD, KIND_BYTES, KIND_FIXED, KIND_NDARRAY, KIND_STR,
-                                   ColumnOut, ShardDesc)
+                                   Batch, ColumnOut, ShardDesc)
 from streaming_amd.encodings import EncodingInfo, parse_encoding
 
 __all__ = [
@@ -132,8 +132,8 @@ class Plan:
     def names(self) -> list[str]:
         return [c.name for c in self.columns]
 
-    def workspace_bytes(self, ntiles: int) -> int:
-        return int(self._lib.mdsx_workspace_bytes(self._handle, ntiles))
+    def workspace_bytes(self, batch: 'DeviceBatch') -> int:
+        return int(self._lib.mdsx_workspace_bytes(self._handle, ctypes.byref(batch.abi())))
 
     def fixed_row_bytes(self) -> int:
         return sum(c.row_bytes for c in self.columns if c.is_fixed)
@@ -179,6 +179,18 @@ class DeviceBatch:
     @property
     def device(self) -> torch.device:
         return self.buffer.device
+
+    def abi(self) -> Batch:
+        """The ``mdsx_batch`` view of this batch (device pointers)."""
+        b = Batch()
+        b.data = self.buffer.data_ptr()
+        b.bytes = int(self.buffer.numel())
+        b.shards = self.descs.data_ptr()
+        b.tile_shard = self.tile_shard.data_ptr()
+        b.nshards = self.nshards
+        b.ntiles = self.ntiles
+        b.rows = self.total_rows
+        return b
 
 
 def _layout(sizes: Sequence[int]) -> tuple[list[int], int]:
@@ -325,8 +337,8 @@ class BatchDecoder:
         dev = batch.device
         self.device = dev
         rows = batch.total_rows
-        self.workspace = torch.zeros(max(plan.workspace_bytes(batch.ntiles), 256),
-                                     dtype=torch.uint8,
+        self._abi = batch.abi()
+        self.workspace = torch.zeros(max(plan.workspace_bytes(batch), 256), dtype=torch.uint8,
                                      device=dev)
         self.totals = torch.zeros(max(plan.num_var, 1), dtype=torch.int64, device=dev)
         self.outputs: dict[str, Union[torch.Tensor, RaggedColumn]] = {}
@@ -373,12 +385,9 @@ class BatchDecoder:
                 o.capacity = int(out.values.numel())
 
     def _scan(self, stream: int) -> None:
-        b = self.batch
         _check(
-            self.plan._lib.mdsx_scan_shards(self.plan.handle, b.buffer.data_ptr(),
-                                            b.descs.data_ptr(), b.nshards,
-                                            b.tile_shard.data_ptr(), b.ntiles, b.total_rows,
-                                            self._outs, self.workspace.data_ptr(),
+            self.plan._lib.mdsx_scan_shards(self.plan.handle, ctypes.byref(self._abi), self._outs,
+                                            self.workspace.data_ptr(), self.workspace.numel(),
                                             self.totals.data_ptr(), stream), 'mdsx_scan_shards')
 
     def run(self, events: Optional[Sequence[torch.cuda.Event]] = None) -> DecodedBatch:
@@ -387,7 +396,6 @@ class BatchDecoder:
         ``events``: optional three CUDA events recorded on the stream before the scan pass,
         between the scan and the decode kernel, and after the decode kernel (kernel timing).
         """
-        b = self.batch
         stream = torch.cuda.current_stream(self.device).cuda_stream
         self._fill_outs()
         if events is not None:
@@ -406,10 +414,9 @@ class BatchDecoder:
         if events is not None:
             events[1].record()
         _check(
-            self.plan._lib.mdsx_decode_shards(self.plan.handle, b.buffer.data_ptr(),
-                                              b.descs.data_ptr(), b.nshards,
-                                              b.tile_shard.data_ptr(), b.ntiles, b.total_rows,
-                                              self._outs, self.workspace.data_ptr(), stream),
+            self.plan._lib.mdsx_decode_shards(self.plan.handle, ctypes.byref(self._abi),
+                                              self._outs, self.workspace.data_ptr(),
+                                              self.workspace.numel(), stream),
             'mdsx_decode_shards')
         if events is not None:
             events[2].record()

@@ -348,3 +348,46 @@ def test_missing_shard_file_raises_file_not_found(tmp_path):
     os.remove(d / 'shard.00000.mds')
     with pytest.raises(FileNotFoundError):
         ds[0]
+
+
+def _decode_rows(tmp_path, cols, rows, **kw):
+    with MDSWriter(columns=cols, out=str(tmp_path / 'ds'), **kw) as w:
+        for r in rows:
+            w.write(r)
+    ds = LocalDataset(str(tmp_path / 'ds'))
+    return ds, ds.decode_all()
+
+
+def test_ragged_many_tiny_rows(tmp_path):
+    """Gather tiles holding thousands of empty / 1-byte rows (rows read from global memory)."""
+    rng = np.random.default_rng(9)
+    pieces = [b'', b'a', 'é'.encode(), b'\xc3', b'\x80', '€'.encode()]
+    rows = []
+    for i in range(6000):
+        k = int(rng.integers(0, len(pieces))) if i % 7 == 0 else 0
+        rows.append({'s': pieces[k], 'b': pieces[(k + 1) % len(pieces)] * (i % 3)})
+    ds, dec = _decode_rows(tmp_path, {'s': 'str', 'b': 'bytes'}, rows, size_limit=None)
+    s, b = dec['s'], dec['b']
+    sv, so = s.values.cpu().numpy(), s.offsets.cpu().numpy()
+    bv, bo = b.values.cpu().numpy(), b.offsets.cpu().numpy()
+    flags = s.flags.cpu().numpy()
+    for i, r in enumerate(rows):
+        assert sv[so[i]:so[i + 1]].tobytes() == r['s']
+        assert bv[bo[i]:bo[i + 1]].tobytes() == r['b']
+        assert flags[i] == (0 if mds_oracle.utf8_is_valid(r['s']) else 1), i
+
+
+def test_ragged_row_spanning_many_tiles(tmp_path):
+    """One 200 KiB str row (25 gather tiles) with an error deep inside, between valid rows."""
+    big = ('ab€' * 30000).encode()
+    bad = bytearray(big)
+    bad[150001] = 0xFF
+    rows = [{'s': 'x' * 5}, {'s': big}, {'s': bytes(bad)}, {'s': big[:-1]}, {'s': 'ok'}]
+    ds, dec = _decode_rows(tmp_path, {'s': 'str'}, rows, size_limit=None)
+    s = dec['s']
+    sv, so = s.values.cpu().numpy(), s.offsets.cpu().numpy()
+    for i, r in enumerate(rows):
+        want = r['s'] if isinstance(r['s'], bytes) else r['s'].encode()
+        assert sv[so[i]:so[i + 1]].tobytes() == want
+    # big[:-1] cuts a 3-byte euro sign: truncated sequence at the row end
+    assert s.flags.cpu().tolist() == [0, 0, 1, 1, 0]

@@ -36,6 +36,7 @@ def test_struct_layouts():
     assert ctypes.sizeof(_native.ShardDesc) == 32
     assert ctypes.sizeof(_native.ColumnOut) == 32
     assert ctypes.sizeof(_native.Status) == 16
+    assert ctypes.sizeof(_native.Batch) == 48
 
 
 @pytest.mark.parametrize('name', gu.ALL_SETS)
@@ -77,10 +78,16 @@ def test_plan_accepts_python_int_shapes(enc, size):
 
 
 def test_workspace_bytes():
+    lib = _native.lib()
     plan = Plan(['b', 'n', 's'], ['bytes', 'int', 'str'], [None, 8, None])
-    assert plan.workspace_bytes(100) == 256 + ((2 * 2 * 100 * 8 + 255) // 256) * 256
+    b = _native.Batch()
+    b.data, b.shards, b.tile_shard = 1, 1, 1
+    b.bytes, b.nshards, b.ntiles, b.rows = 1 << 20, 1, 100, 6400
+    r = lambda x: (x + 255) // 256 * 256
+    want = 256 + 2 * r(2 * 100 * 8) + r(2 * 6400 * 8) + r(2 * ((1 << 20) // 8192 + 2) * 4)
+    assert lib.mdsx_workspace_bytes(plan.handle, ctypes.byref(b)) == want
     fixed = Plan(['id', 'x'], ['int32', 'ndarray:float32:1024'], [4, 4096])
-    assert fixed.workspace_bytes(1000) == 256
+    assert lib.mdsx_workspace_bytes(fixed.handle, ctypes.byref(b)) == 256
 
 
 def test_too_many_columns():
