@@ -378,10 +378,10 @@ def test_ragged_many_tiny_rows(tmp_path):
 
 
 def test_ragged_row_spanning_many_tiles(tmp_path):
-    """One 200 KiB str row (25 gather tiles) with an error deep inside, between valid rows."""
+    """One 150 KB str row (19 gather tiles) with an error deep inside, between valid rows."""
     big = ('ab€' * 30000).encode()
     bad = bytearray(big)
-    bad[150001] = 0xFF
+    bad[100001] = 0xFF
     rows = [{'s': 'x' * 5}, {'s': big}, {'s': bytes(bad)}, {'s': big[:-1]}, {'s': 'ok'}]
     ds, dec = _decode_rows(tmp_path, {'s': 'str'}, rows, size_limit=None)
     s = dec['s']
