@@ -16,8 +16,8 @@
 //                        row per wave with 16-byte aligned loads and stores, the source realigned in
 //                        registers (v_alignbyte funnel over the neighbour lane's chunk); for ragged
 //                        columns: final offsets, each row's source address and the row that starts
-//                        every 8 KiB output tile.
-//   gather_ragged_kernel one workgroup per 8 KiB tile of a ragged column's packed output
+//                        every 16 KiB output tile.
+//   gather_ragged_kernel one workgroup per 16 KiB tile of a ragged column's packed output
 //                        (destination-major): every lane writes whole aligned 16-byte chunks,
 //                        assembled from the row(s) that cover them (binary search over the tile's
 //                        rows staged in LDS), so short and long rows keep all 64 lanes busy; str
@@ -38,8 +38,8 @@ namespace mdsx_kernels {
 
 constexpr int kBlock = 256;                     // 4 waves
 constexpr int kSmallMax = 16;                   // fixed columns <= 16 B: one row per lane
-constexpr int kGatherChunks = 2;                // 16-byte chunks per lane in gather_ragged_kernel
-constexpr uint64_t kGatherTile = uint64_t(kBlock) * 16 * kGatherChunks;  // 8 KiB per workgroup
+constexpr int kGatherChunks = 4;                // 16-byte chunks per lane in gather_ragged_kernel
+constexpr uint64_t kGatherTile = uint64_t(kBlock) * 16 * kGatherChunks;  // 16 KiB per workgroup
 constexpr int kGatherRows = 1024;               // rows of a gather tile staged in LDS
 
 struct DevCol {
@@ -579,23 +579,54 @@ __device__ __forceinline__ void utf8_check(const Rows& R, int n, int j, int64_t 
   if (bad) flags[row0 + j] = 1;
 }
 
+// One 16 KiB output tile of a ragged column. Chunk c = threadIdx.x + 256 k (k < kGatherChunks),
+// so the 64 lanes of a wave hold 64 consecutive chunks. A chunk inside one row (the common case)
+// loads its aligned source chunk and takes the next one from the neighbour lane (same row, so the
+// next 16 source bytes); lane 63 and chunks ending on a row end load it themselves. Chunks that
+// straddle rows are assembled row by row.
 template <bool kNT, class Rows>
 __device__ __forceinline__ void gather_tile(const DevArgs& a, const DevCol& col, const Rows& R,
                                             int n, uint64_t r0, int64_t T0, int64_t tot,
-                                            uint32_t* s_last) {
+                                            uint32_t* s_edge) {
   const bool utf8 = col.kind == MDSX_KIND_STR && col.flags;
   uint8_t* out = static_cast<uint8_t*>(col.data);
-  uint4 val[kGatherChunks];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t base = reinterpret_cast<uint64_t>(a.batch);
+  uint4 val[kGatherChunks], lo[kGatherChunks], hi[kGatherChunks];
   int jrow[kGatherChunks];
+  uint32_t shift[kGatherChunks];
+  bool single[kGatherChunks], need_hi[kGatherChunks];
+  // phase 1: locate rows, issue every load
 #pragma unroll
   for (int k = 0; k < kGatherChunks; ++k) {
-    const int c = threadIdx.x + kBlock * k;
-    const int64_t D = T0 + 16 * c;
-    val[k] = make_uint4(0, 0, 0, 0);
-    jrow[k] = 0;
-    if (D < tot) {
-      jrow[k] = find_row(R, n, D);
+    const int64_t D = T0 + 16 * (threadIdx.x + kBlock * k);
+    const bool valid = D < tot;
+    const int j = valid ? find_row(R, n, D) : 0;
+    const int64_t ro = R.o(j), re = R.o(j + 1);
+    const uint64_t s0 = base + R.s(j) + uint64_t(D - ro);
+    const uint4* al = reinterpret_cast<const uint4*>(s0 & ~uint64_t(15));
+    jrow[k] = j;
+    shift[k] = uint32_t(s0 & 15);
+    single[k] = valid && D + 16 <= re;
+    const bool next_same = single[k] && D + 16 < re && lane != 63;  // lane+1 starts in row j
+    need_hi[k] = single[k] && shift[k] != 0 && !next_same;
+    lo[k] = single[k] ? ld16<kNT>(al) : make_uint4(0, 0, 0, 0);
+    hi[k] = need_hi[k] ? ld16<kNT>(al + 1) : make_uint4(0, 0, 0, 0);
+  }
+  // phase 2: realign, assemble row-straddling chunks, store
+#pragma unroll
+  for (int k = 0; k < kGatherChunks; ++k) {
+    const int64_t D = T0 + 16 * (threadIdx.x + kBlock * k);
+    const uint4 nb = shfl_down1(lo[k]);
+    if (single[k]) {
+      const uint4 h = need_hi[k] ? hi[k] : nb;
+      val[k] = shift[k] ? funnel16_lane(lo[k], h, shift[k]) : lo[k];
+    } else if (D < tot) {
       val[k] = assemble<kNT>(R, n, jrow[k], D, a.batch);
+    } else {
+      val[k] = make_uint4(0, 0, 0, 0);
+    }
+    if (D < tot) {
       const uint64_t dst = reinterpret_cast<uint64_t>(out) + uint64_t(D);
       if (uint64_t(D) + 16 <= col.capacity) {
         st16<kNT>(dst, val[k]);
@@ -604,25 +635,26 @@ __device__ __forceinline__ void gather_tile(const DevArgs& a, const DevCol& col,
           out[D + b] = uint8_t(byte_of(val[k], b));
       }
     }
-    if (utf8) s_last[c] = val[k].w;
   }
   if (!utf8) return;
+  // UTF-8: the 4 bytes before each chunk come from the previous lane (lane 0: the previous
+  // wave's lane 63 through LDS; the tile's first chunk: assembled from its row).
+#pragma unroll
+  for (int k = 0; k < kGatherChunks; ++k)
+    if (lane == 63) s_edge[k * (kBlock / 64) + wave] = val[k].w;
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < kGatherChunks; ++k) {
     const int c = threadIdx.x + kBlock * k;
     const int64_t D = T0 + 16 * c;
-    if (D >= tot) continue;
-    uint32_t pw;
-    if (c > 0) {
-      pw = s_last[c - 1];
-    } else if (D > R.o(0)) {  // bytes before the tile inside the tile's first row
-      const uint4 prev = assemble<kNT>(R, 1, 0, D - 16, a.batch);
-      pw = prev.w;
-    } else {
-      pw = 0;
+    uint32_t pw = __shfl_up(val[k].w, 1);
+    if (lane == 0) {
+      if (c == 0)
+        pw = D > R.o(0) ? assemble<kNT>(R, 1, 0, D - 16, a.batch).w : 0u;
+      else
+        pw = s_edge[wave > 0 ? k * (kBlock / 64) + wave - 1 : (k - 1) * (kBlock / 64) + 3];
     }
-    utf8_check(R, n, jrow[k], D, tot, val[k], pw, col.flags, r0);
+    if (D < tot) utf8_check(R, n, jrow[k], D, tot, val[k], pw, col.flags, r0);
   }
 }
 
@@ -630,7 +662,7 @@ template <bool kNT>
 __global__ __launch_bounds__(kBlock) void gather_ragged_kernel(const DevArgs a) {
   __shared__ __attribute__((aligned(16))) int64_t s_off[kGatherRows + 1];
   __shared__ uint64_t s_src[kGatherRows];
-  __shared__ uint32_t s_last[kBlock * kGatherChunks];
+  __shared__ uint32_t s_edge[kGatherChunks * (kBlock / 64)];
   // which ragged column / tile (block-uniform)
   int vi = 0;
   while (vi + 1 < a.nvar && blockIdx.x >= a.gather_block0[vi + 1]) ++vi;
@@ -654,9 +686,9 @@ __global__ __launch_bounds__(kBlock) void gather_ragged_kernel(const DevArgs a) 
       if (i < n) s_src[i] = src[r0 + i];
     }
     __syncthreads();
-    gather_tile<kNT>(a, col, RowsLds{s_off, s_src}, n, r0, T0, tot, s_last);
+    gather_tile<kNT>(a, col, RowsLds{s_off, s_src}, n, r0, T0, tot, s_edge);
   } else {
-    gather_tile<kNT>(a, col, RowsGlobal{col.offsets + r0, src + r0}, n, r0, T0, tot, s_last);
+    gather_tile<kNT>(a, col, RowsGlobal{col.offsets + r0, src + r0}, n, r0, T0, tot, s_edge);
   }
 }
 
