@@ -610,7 +610,7 @@ __device__ __forceinline__ void gather_tile(const DevArgs& a, const DevCol& col,
     single[k] = valid && D + 16 <= re;
     const bool next_same = single[k] && D + 16 < re && lane != 63;  // lane+1 starts in row j
     need_hi[k] = single[k] && shift[k] != 0 && !next_same;
-    lo[k] = single[k] ? ld16<kNT>(al) : make_uint4(0, 0, 0, 0);
+    lo[k] = valid ? ld16<kNT>(al) : make_uint4(0, 0, 0, 0);  // also feeds lane-1's funnel
     hi[k] = need_hi[k] ? ld16<kNT>(al + 1) : make_uint4(0, 0, 0, 0);
   }
   // phase 2: realign, assemble row-straddling chunks, store
