@@ -38,6 +38,7 @@ struct mdsx_plan {
   int tile_rows = 256;
   int unroll = 4;       // 16-byte chunks per lane in flight in the row copy (2, 4 or 8)
   int nontemporal = 0;  // non-temporal loads/stores in the row copy
+  int gather_chunks = 2;  // 16-byte chunks per lane in the ragged gather (tile = 4 KiB x this)
   int64_t fixed_sum = 0;
   bool safe = true;
   mdsx::ColumnSpec cols[MDSX_MAX_COLUMNS];

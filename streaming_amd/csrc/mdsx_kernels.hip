@@ -38,8 +38,7 @@ namespace mdsx_kernels {
 
 constexpr int kBlock = 256;                     // 4 waves
 constexpr int kSmallMax = 16;                   // fixed columns <= 16 B: one row per lane
-constexpr int kGatherChunks = 4;                // 16-byte chunks per lane in gather_ragged_kernel
-constexpr uint64_t kGatherTile = uint64_t(kBlock) * 16 * kGatherChunks;  // 16 KiB per workgroup
+constexpr uint64_t kMapGrain = uint64_t(kBlock) * 16;  // 4 KiB: row-map granule of ragged outputs
 constexpr int kGatherRows = 1024;               // rows of a gather tile staged in LDS
 
 struct DevCol {
@@ -447,8 +446,8 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
       a.src_abs[uint64_t(vi) * a.rows + row] = v.d.offset + s_src[c * TR + t];
       if (len) {
         uint32_t* map = a.row_map + uint64_t(vi) * a.map_len;
-        for (uint64_t g = (uint64_t(off) + kGatherTile - 1) / kGatherTile;
-             g * kGatherTile < uint64_t(off) + len && g < a.map_len; ++g)
+        for (uint64_t g = (uint64_t(off) + kMapGrain - 1) / kMapGrain;
+             g * kMapGrain < uint64_t(off) + len && g < a.map_len; ++g)
           map[g] = uint32_t(row);
       }
     }
@@ -579,12 +578,12 @@ __device__ __forceinline__ void utf8_check(const Rows& R, int n, int j, int64_t 
   if (bad) flags[row0 + j] = 1;
 }
 
-// One 16 KiB output tile of a ragged column. Chunk c = threadIdx.x + 256 k (k < kGatherChunks),
+// One output tile (kChunks x 4 KiB) of a ragged column. Chunk c = threadIdx.x + 256 k (k < kChunks),
 // so the 64 lanes of a wave hold 64 consecutive chunks. A chunk inside one row (the common case)
 // loads its aligned source chunk and takes the next one from the neighbour lane (same row, so the
 // next 16 source bytes); lane 63 and chunks ending on a row end load it themselves. Chunks that
 // straddle rows are assembled row by row.
-template <bool kNT, class Rows>
+template <bool kNT, int kGatherChunks, class Rows>
 __device__ __forceinline__ void gather_tile(const DevArgs& a, const DevCol& col, const Rows& R,
                                             int n, uint64_t r0, int64_t T0, int64_t tot,
                                             uint32_t* s_edge) {
@@ -658,8 +657,9 @@ __device__ __forceinline__ void gather_tile(const DevArgs& a, const DevCol& col,
   }
 }
 
-template <bool kNT>
+template <bool kNT, int kGatherChunks>
 __global__ __launch_bounds__(kBlock) void gather_ragged_kernel(const DevArgs a) {
+  constexpr uint64_t kGatherTile = kMapGrain * kGatherChunks;
   __shared__ __attribute__((aligned(16))) int64_t s_off[kGatherRows + 1];
   __shared__ uint64_t s_src[kGatherRows];
   __shared__ uint32_t s_edge[kGatherChunks * (kBlock / 64)];
@@ -673,10 +673,11 @@ __global__ __launch_bounds__(kBlock) void gather_ragged_kernel(const DevArgs a) 
   const int64_t tot = col.offsets[a.rows];
   const int64_t T0 = int64_t(g * kGatherTile);
   if (T0 >= tot) return;
-  if (a.status->code != 0 || g + 1 >= a.map_len) return;  // decode failed: outputs are void
+  if (a.status->code != 0 || (g + 1) * kGatherChunks >= a.map_len) return;  // decode failed
   const uint32_t* map = a.row_map + uint64_t(vi) * a.map_len;
-  const uint64_t r0 = map[g];
-  const uint64_t r1 = (T0 + int64_t(kGatherTile) < tot) ? uint64_t(map[g + 1]) : a.rows - 1;
+  const uint64_t r0 = map[g * kGatherChunks];
+  const uint64_t r1 =
+      (T0 + int64_t(kGatherTile) < tot) ? uint64_t(map[(g + 1) * kGatherChunks]) : a.rows - 1;
   if (r0 >= a.rows || r1 >= a.rows || r1 < r0) return;  // never for a status-clean decode
   const int n = int(r1 - r0 + 1);
   const uint64_t* src = a.src_abs + uint64_t(vi) * a.rows;
@@ -686,9 +687,10 @@ __global__ __launch_bounds__(kBlock) void gather_ragged_kernel(const DevArgs a) 
       if (i < n) s_src[i] = src[r0 + i];
     }
     __syncthreads();
-    gather_tile<kNT>(a, col, RowsLds{s_off, s_src}, n, r0, T0, tot, s_edge);
+    gather_tile<kNT, kGatherChunks>(a, col, RowsLds{s_off, s_src}, n, r0, T0, tot, s_edge);
   } else {
-    gather_tile<kNT>(a, col, RowsGlobal{col.offsets + r0, src + r0}, n, r0, T0, tot, s_edge);
+    gather_tile<kNT, kGatherChunks>(a, col, RowsGlobal{col.offsets + r0, src + r0}, n, r0, T0,
+                                    tot, s_edge);
   }
 }
 
@@ -702,7 +704,7 @@ __host__ uint64_t round256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
 Layout workspace_layout(const mdsx_plan* plan, const mdsx_batch* b) {
   Layout L;
   const uint64_t nv = uint64_t(plan->nvar);
-  L.map_len = b->bytes / kGatherTile + 2;
+  L.map_len = b->bytes / kMapGrain + 8;
   L.tile_total = 256;
   L.tile_prefix = L.tile_total + round256(nv * b->ntiles * 8);
   L.src_abs = L.tile_prefix + round256(nv * b->ntiles * 8);
@@ -739,6 +741,7 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   a->nvar = plan->nvar;
   a->tile_rows = plan->tile_rows;
   uint32_t gblocks = 0;
+  const uint64_t tile = kMapGrain * uint64_t(plan->gather_chunks);
   for (int c = 0; c < plan->ncols; ++c) {
     const mdsx::ColumnSpec& s = plan->cols[c];
     DevCol& d = a->cols[c];
@@ -760,7 +763,7 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
     a->gather_block0[v] = gblocks;
     for (int c = 0; c < plan->ncols; ++c)
       if (plan->cols[c].var_index == v)
-        gblocks += uint32_t((outs[c].capacity + kGatherTile - 1) / kGatherTile);
+        gblocks += uint32_t((outs[c].capacity + tile - 1) / tile);
   }
   a->gather_block0[plan->nvar] = gblocks;
   return MDSX_OK;
@@ -843,10 +846,17 @@ int mdsx_decode_shards(const mdsx_plan* plan, const mdsx_batch* batch,
   if (rc != MDSX_OK || plan->nvar == 0) return rc;
   const uint32_t gblocks = a.gather_block0[plan->nvar];
   if (gblocks == 0) return MDSX_OK;
-  if (nt)
-    hipLaunchKernelGGL((gather_ragged_kernel<true>), dim3(gblocks), dim3(kBlock), 0, s, a);
-  else
-    hipLaunchKernelGGL((gather_ragged_kernel<false>), dim3(gblocks), dim3(kBlock), 0, s, a);
+  const int gk = plan->gather_chunks;
+#define MDSX_GATHER(NT, K) \
+  hipLaunchKernelGGL((gather_ragged_kernel<NT, K>), dim3(gblocks), dim3(kBlock), 0, s, a)
+  if (gk == 1) {
+    if (nt) MDSX_GATHER(true, 1); else MDSX_GATHER(false, 1);
+  } else if (gk == 4) {
+    if (nt) MDSX_GATHER(true, 4); else MDSX_GATHER(false, 4);
+  } else {
+    if (nt) MDSX_GATHER(true, 2); else MDSX_GATHER(false, 2);
+  }
+#undef MDSX_GATHER
   return hip_check(hipGetLastError(), "gather_ragged_kernel launch");
 }
 

@@ -182,6 +182,8 @@ void apply_tuning(mdsx_plan* p) {
       if (per_row * v <= 64 * 1024) p->tile_rows = int(v);
     } else if (key == "unroll" && (v == 2 || v == 4 || v == 8)) {
       p->unroll = int(v);
+    } else if (key == "gk" && (v == 1 || v == 2 || v == 4)) {
+      p->gather_chunks = int(v);
     } else if (key == "nt") {
       p->nontemporal = v ? 1 : 0;
     }
