@@ -36,9 +36,10 @@ struct mdsx_plan {
   int ncols = 0;
   int nvar = 0;
   int tile_rows = 256;
-  int unroll = 4;       // 16-byte chunks per lane in flight in the row copy (2, 4 or 8)
+  int unroll = 4;       // 16-byte chunks per lane in flight in the row copy (4 or 6)
   int nontemporal = 0;  // non-temporal loads/stores in the row copy
   int gather_chunks = 2;  // 16-byte chunks per lane in the ragged gather (tile = 4 KiB x this)
+  int gather_min = 256;   // ragged columns averaging fewer bytes per row use the gather kernel
   int64_t fixed_sum = 0;
   bool safe = true;
   mdsx::ColumnSpec cols[MDSX_MAX_COLUMNS];

@@ -47,8 +47,10 @@ struct DevCol {
   uint8_t* flags;
   uint64_t capacity;
   uint32_t row_bytes;
-  int16_t kind;
-  int16_t var_index;
+  int8_t kind;
+  int8_t var_index;
+  int8_t gather;  // ragged column copied by gather_ragged_kernel (short rows) instead of waves
+  int8_t pad_;
 };
 
 struct DevArgs {
@@ -292,15 +294,62 @@ __device__ __forceinline__ uint4 byte_mask(uint32_t a, uint32_t b) {
   return make_uint4(m[0], m[1], m[2], m[3]);
 }
 
+// Strict UTF-8 well-formedness (what bytes.decode('utf-8') accepts, encodings.py:80-81) of the
+// 16 bytes of `v` at segment positions pos0 .. pos0+15 of a segment of `len` bytes, given the 3
+// bytes before them in pw (bytes 1..3 of the previous chunk's last dword; zero before the
+// segment start).
+__device__ __forceinline__ bool utf8_chunk_bad(const uint4 v, uint32_t pw, int64_t pos0,
+                                               int64_t len) {
+  uint32_t p1 = (pw >> 24) & 0xffu, p2 = (pw >> 16) & 0xffu, p3 = (pw >> 8) & 0xffu;
+  const bool ascii = ((v.x | v.y | v.z | v.w) & 0x80808080u) == 0;
+  if (ascii && p1 < 0xC0u && p2 < 0xE0u && p3 < 0xF0u) return false;
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t b = byte_of(v, j);
+    const int64_t pos = pos0 + j;
+    if (pos >= 0 && pos < len) {
+      const bool cont = (b & 0xC0u) == 0x80u;
+      const bool need = p1 >= 0xC0u || p2 >= 0xE0u || p3 >= 0xF0u;
+      bad |= cont != need;
+      bad |= b == 0xC0u || b == 0xC1u || b >= 0xF5u;
+      bad |= (p1 == 0xE0u && b < 0xA0u) || (p1 == 0xEDu && b > 0x9Fu) ||
+             (p1 == 0xF0u && b < 0x90u) || (p1 == 0xF4u && b > 0x8Fu);
+      bad |= (b >= 0xC0u && pos + 1 >= len) || (b >= 0xE0u && pos + 2 >= len) ||
+             (b >= 0xF0u && pos + 3 >= len);
+    }
+    p3 = p2;
+    p2 = p1;
+    p1 = b;
+  }
+  return bad;
+}
+
+// Store the bytes of `chunk` (held by lane `le`, 16-byte aligned destination D) that fall in
+// [d0, dend): one byte per lane, lanes 0..15, in a single wave instruction.
+__device__ __forceinline__ void wave_edge_store(const uint4 chunk, int le, uint64_t D,
+                                                uint64_t d0, uint64_t dend, int lane) {
+  const uint32_t w0 = __builtin_amdgcn_readlane(chunk.x, le);
+  const uint32_t w1 = __builtin_amdgcn_readlane(chunk.y, le);
+  const uint32_t w2 = __builtin_amdgcn_readlane(chunk.z, le);
+  const uint32_t w3 = __builtin_amdgcn_readlane(chunk.w, le);
+  const uint64_t A = D + uint64_t(lane);
+  if (lane < 16 && A >= d0 && A < dend) {
+    const uint32_t w = lane < 4 ? w0 : lane < 8 ? w1 : lane < 12 ? w2 : w3;
+    *reinterpret_cast<uint8_t*>(A) = uint8_t(w >> (8 * (lane & 3)));
+  }
+}
+
 // One wave copies `len` bytes from src to dst (any alignment of either). Destination chunks are
 // 16-byte aligned; lane k of a step owns chunk k. Its source bytes straddle two aligned 16-byte
 // source chunks: it loads the first and takes the second from lane k+1 (lane 63 from lane 0 of
-// the next step, or one extra load at the end of a batch). Partial chunks at the two ends are
-// written byte by byte.
-template <int kUnroll, bool kNT>
-__device__ __forceinline__ void wave_copy(const uint8_t* src, uint8_t* dst, uint64_t len,
+// the next step, or one extra load at the end of a batch). The (at most two) partial chunks at
+// the ends are written one byte per lane. With kUtf8, returns whether the segment is not
+// well-formed UTF-8 (wave-uniform).
+template <bool kUtf8, int kUnroll, bool kNT, bool kEdges = true>
+__device__ __forceinline__ bool wave_copy(const uint8_t* src, uint8_t* dst, uint64_t len,
                                           int lane) {
-  if (len == 0) return;
+  if (len == 0) return false;
   const uint64_t d0 = reinterpret_cast<uint64_t>(dst);
   const uint64_t dend = d0 + len;
   const uint64_t dbeg = d0 & ~uint64_t(15);
@@ -309,6 +358,10 @@ __device__ __forceinline__ void wave_copy(const uint8_t* src, uint8_t* dst, uint
   const uint32_t sh = uint32_t(sfirst & 15);
   const uint4* sal = reinterpret_cast<const uint4*>(sfirst & ~uint64_t(15));
   const uint64_t nload = nchunks + (sh ? 1 : 0);
+  const bool head_partial = dbeg < d0 || dbeg + 16 > dend;
+  const bool tail_partial = nchunks > 1 && (dend & 15) != 0;
+  bool bad = false;
+  uint32_t carry = 0;  // last dword of the previous chunk (UTF-8 look-back)
   for (uint64_t base = 0; base < nchunks; base += 64 * kUnroll) {
     uint4 lo[kUnroll];
 #pragma unroll
@@ -323,8 +376,9 @@ __device__ __forceinline__ void wave_copy(const uint8_t* src, uint8_t* dst, uint
     }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
-      if (base + uint64_t(u) * 64 >= nchunks) break;  // wave-uniform
-      const uint64_t k = base + uint64_t(u) * 64 + lane;
+      const uint64_t k0 = base + uint64_t(u) * 64;
+      if (k0 >= nchunks) break;  // wave-uniform
+      const uint64_t k = k0 + lane;
       uint4 out = lo[u];
       if (sh != 0) {
         uint4 hi = shfl_down1(lo[u]);
@@ -332,20 +386,32 @@ __device__ __forceinline__ void wave_copy(const uint8_t* src, uint8_t* dst, uint
         if (lane == 63) hi = nxt;
         out = funnel16(lo[u], hi, sh);
       }
-      if (k < nchunks) {
-        const uint64_t D = dbeg + 16 * k;
-        if (D >= d0 && D + 16 <= dend) {
-          st16<kNT>(D, out);
-        } else {
-#pragma unroll
-          for (int j = 0; j < 16; ++j) {
-            const uint64_t A = D + j;
-            if (A >= d0 && A < dend) *reinterpret_cast<uint8_t*>(A) = uint8_t(byte_of(out, j));
-          }
+      const uint64_t D = dbeg + 16 * k;
+      if (kUtf8) {
+        uint4 vout = out;
+        if (k == 0 && D < d0) {  // zero the bytes before the segment start
+          const uint32_t head = uint32_t(d0 - D);
+          const uint32_t m0 = head >= 4 ? 0u : (0xffffffffu << (8 * head));
+          const uint32_t m1 = head >= 8 ? 0u : head <= 4 ? 0xffffffffu : (0xffffffffu << (8 * (head - 4)));
+          const uint32_t m2 = head >= 12 ? 0u : head <= 8 ? 0xffffffffu : (0xffffffffu << (8 * (head - 8)));
+          const uint32_t m3 = head <= 12 ? 0xffffffffu : (0xffffffffu << (8 * (head - 12)));
+          vout = make_uint4(vout.x & m0, vout.y & m1, vout.z & m2, vout.w & m3);
         }
+        uint32_t pw = __shfl_up(vout.w, 1);
+        if (lane == 0) pw = carry;
+        carry = __shfl(vout.w, 63);
+        if (k < nchunks) bad |= utf8_chunk_bad(vout, pw, int64_t(D) - int64_t(d0), int64_t(len));
+      }
+      if (k < nchunks && D >= d0 && D + 16 <= dend) st16<kNT>(D, out);
+      if (kEdges) {  // kEdges == false: the caller guarantees 16-byte aligned dst and length
+        if (k0 == 0 && head_partial) wave_edge_store(out, 0, dbeg, d0, dend, lane);
+        if (tail_partial && nchunks - 1 >= k0 && nchunks - 1 < k0 + 64)
+          wave_edge_store(out, int(nchunks - 1 - k0), dbeg + 16 * (nchunks - 1), d0, dend, lane);
       }
     }
   }
+  if (kUtf8) return __any(bad);
+  return false;
 }
 
 // Fixed column of 1..16 bytes: one row per lane. dst is aligned to the largest power of two
@@ -380,12 +446,14 @@ __device__ __forceinline__ void gather_small(const uint8_t* p, uint8_t* dst, uin
 
 // Pass 2: per-row column boundaries; fixed columns decoded; ragged columns prepared for the
 // destination-major gather (final offsets, per-row source addresses, gather-tile row map).
-template <int kUnroll, bool kNT>
+template <int kUnroll, bool kNT, bool kRagged, bool kEdges>
 __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int TR = a.tile_rows;
-  uint32_t* s_src = reinterpret_cast<uint32_t*>(smem);  // [ncols][TR] src offsets in the shard
-  uint8_t* s_ok = reinterpret_cast<uint8_t*>(s_src + a.ncols * TR);  // [TR]
+  uint64_t* s_vdst = reinterpret_cast<uint64_t*>(smem);                 // [nvar][TR]
+  uint32_t* s_src = reinterpret_cast<uint32_t*>(s_vdst + a.nvar * TR);  // [ncols][TR]
+  uint32_t* s_vlen = s_src + a.ncols * TR;                               // [nvar][TR]
+  uint8_t* s_ok = reinterpret_cast<uint8_t*>(s_vlen + a.nvar * TR);     // [TR]
 
   const TileView v = tile_view(a);
   const int t = threadIdx.x;
@@ -417,9 +485,11 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
     uint64_t pos = uint64_t(b) + 4ull * a.nvar;
     for (int c = 0; c < a.ncols; ++c) {
       const DevCol& col = a.cols[c];
-      const uint64_t len = col.var_index < 0 ? uint64_t(col.row_bytes)
-                           : ok ? load_u32_any(v.shard + b + 4u * uint32_t(col.var_index))
-                                : 0u;
+      uint64_t len = col.row_bytes;
+      if (col.var_index >= 0) {
+        len = ok ? load_u32_any(v.shard + b + 4u * uint32_t(col.var_index)) : 0u;
+        s_vlen[col.var_index * TR + t] = uint32_t(len);
+      }
       s_src[c * TR + t] = uint32_t(pos);
       pos += len;
     }
@@ -428,21 +498,24 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
       rc = MDSX_E_BOUNDS;
     }
     // Ragged columns: final offset = tile prefix + the local offset the scan pass left in
-    // offsets[row]; the row's source address; the gather tiles whose first byte it holds.
+    // offsets[row]; then either the destination for this kernel's wave copy, or (gather
+    // columns) the row's source address and the 4 KiB output grains whose first byte it holds.
     for (int c = 0; c < a.ncols; ++c) {
       const DevCol& col = a.cols[c];
       if (col.var_index < 0) continue;
       const int vi = col.var_index;
       const int64_t off = a.tile_prefix[uint64_t(vi) * a.ntiles + blockIdx.x] + col.offsets[row];
       col.offsets[row] = off;
+      s_vdst[vi * TR + t] = uint64_t(off);
       if (col.flags) col.flags[row] = 0;
       if (!ok) continue;
-      const uint64_t len = load_u32_any(v.shard + b + 4u * uint32_t(vi));
+      const uint64_t len = s_vlen[vi * TR + t];
       if (uint64_t(off) + len > col.capacity) {
         report(a.status, MDSX_E_CAPACITY, v.shard_idx, int(i), c);
         ok = false;
         continue;
       }
+      if (!col.gather) continue;
       a.src_abs[uint64_t(vi) * a.rows + row] = v.d.offset + s_src[c * TR + t];
       if (len) {
         uint32_t* map = a.row_map + uint64_t(vi) * a.map_len;
@@ -467,16 +540,28 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
     }
   }
 
-  // ---- large fixed columns: one row per wave
+  // ---- large fixed columns and long-row ragged columns: one row per wave
   for (int r = wave; r < int(v.nrows); r += kBlock / 64) {
     if (!s_ok[r]) continue;  // wave-uniform
     const uint64_t row = v.d.row0 + v.r0 + r;
     for (int c = 0; c < a.ncols; ++c) {
       const DevCol& col = a.cols[c];
-      if (col.var_index >= 0 || col.row_bytes <= uint32_t(kSmallMax)) continue;
-      wave_copy<kUnroll, kNT>(v.shard + s_src[c * TR + r],
-                              static_cast<uint8_t*>(col.data) + row * col.row_bytes,
-                              col.row_bytes, lane);
+      const uint8_t* src = v.shard + s_src[c * TR + r];
+      if (col.var_index < 0) {
+        if (col.row_bytes <= uint32_t(kSmallMax)) continue;
+        wave_copy<false, kUnroll, kNT, kEdges>(
+            src, static_cast<uint8_t*>(col.data) + row * col.row_bytes, col.row_bytes, lane);
+      } else if (kRagged && !col.gather) {
+        const int vi = col.var_index;
+        uint8_t* dst = static_cast<uint8_t*>(col.data) + s_vdst[vi * TR + r];
+        const uint64_t len = s_vlen[vi * TR + r];
+        if (col.kind == MDSX_KIND_STR) {
+          const bool bad = wave_copy<true, kUnroll, kNT>(src, dst, len, lane);
+          if (lane == 0 && col.flags && bad) col.flags[row] = 1;
+        } else {
+          wave_copy<false, kUnroll, kNT>(src, dst, len, lane);
+        }
+      }
     }
   }
 }
@@ -750,8 +835,11 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
     d.flags = outs[c].flags;
     d.capacity = outs[c].capacity;
     d.row_bytes = uint32_t(s.row_bytes);
-    d.kind = int16_t(s.kind);
-    d.var_index = int16_t(s.var_index);
+    d.kind = int8_t(s.kind);
+    d.var_index = int8_t(s.var_index);
+    // Short ragged rows keep a wave's lanes busy only when copied destination-major.
+    d.gather = s.kind != MDSX_KIND_FIXED && b->rows > 0 &&
+               outs[c].capacity < uint64_t(plan->gather_min) * b->rows;
     if (s.kind == MDSX_KIND_FIXED) {
       if (!d.data) return mdsx::fail(MDSX_E_ARG, "mdsx: null data pointer for a fixed column");
     } else {
@@ -762,7 +850,7 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   for (int v = 0; v < plan->nvar; ++v) {  // gather workgroups of each ragged column, in order
     a->gather_block0[v] = gblocks;
     for (int c = 0; c < plan->ncols; ++c)
-      if (plan->cols[c].var_index == v)
+      if (plan->cols[c].var_index == v && a->cols[c].gather)
         gblocks += uint32_t((outs[c].capacity + tile - 1) / tile);
   }
   a->gather_block0[plan->nvar] = gblocks;
@@ -828,20 +916,35 @@ int mdsx_decode_shards(const mdsx_plan* plan, const mdsx_batch* batch,
   if (rc != MDSX_OK) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (a.ntiles == 0) return MDSX_OK;
-  const size_t lds = size_t(plan->tile_rows) * (4 * size_t(plan->ncols) + 1) + 16;
-  const int u = plan->unroll, nt = plan->nontemporal;
-  if (u == 8 && nt)
-    hipLaunchKernelGGL((decode_kernel<8, true>), dim3(a.ntiles), dim3(kBlock), lds, s, a);
-  else if (u == 8)
-    hipLaunchKernelGGL((decode_kernel<8, false>), dim3(a.ntiles), dim3(kBlock), lds, s, a);
-  else if (u == 2 && nt)
-    hipLaunchKernelGGL((decode_kernel<2, true>), dim3(a.ntiles), dim3(kBlock), lds, s, a);
-  else if (u == 2)
-    hipLaunchKernelGGL((decode_kernel<2, false>), dim3(a.ntiles), dim3(kBlock), lds, s, a);
-  else if (nt)
-    hipLaunchKernelGGL((decode_kernel<4, true>), dim3(a.ntiles), dim3(kBlock), lds, s, a);
-  else
-    hipLaunchKernelGGL((decode_kernel<4, false>), dim3(a.ntiles), dim3(kBlock), lds, s, a);
+  const size_t lds =
+      size_t(plan->tile_rows) * (12 * size_t(plan->nvar) + 4 * size_t(plan->ncols) + 1) + 16;
+  const bool nt = plan->nontemporal != 0, ragged = plan->nvar > 0;
+  // Edge (partial 16-byte chunk) stores are only needed for ragged columns and for large fixed
+  // columns whose row size is not a multiple of 16 (outputs are 256-byte aligned).
+  bool edges = ragged;
+  for (int c = 0; c < plan->ncols; ++c)
+    if (plan->cols[c].kind == MDSX_KIND_FIXED && plan->cols[c].row_bytes > kSmallMax &&
+        plan->cols[c].row_bytes % 16 != 0)
+      edges = true;
+#define MDSX_DECODE(U, NT, RG, ED) \
+  hipLaunchKernelGGL((decode_kernel<U, NT, RG, ED>), dim3(a.ntiles), dim3(kBlock), lds, s, a)
+#define MDSX_DECODE_U(U)                                  \
+  do {                                                    \
+    if (ragged) {                                         \
+      if (nt) MDSX_DECODE(U, true, true, true);           \
+      else MDSX_DECODE(U, false, true, true);             \
+    } else if (edges) {                                   \
+      if (nt) MDSX_DECODE(U, true, false, true);          \
+      else MDSX_DECODE(U, false, false, true);            \
+    } else {                                              \
+      if (nt) MDSX_DECODE(U, true, false, false);         \
+      else MDSX_DECODE(U, false, false, false);           \
+    }                                                     \
+  } while (0)
+  if (plan->unroll == 6) MDSX_DECODE_U(6);
+  else MDSX_DECODE_U(4);
+#undef MDSX_DECODE_U
+#undef MDSX_DECODE
   rc = hip_check(hipGetLastError(), "decode_kernel launch");
   if (rc != MDSX_OK || plan->nvar == 0) return rc;
   const uint32_t gblocks = a.gather_block0[plan->nvar];

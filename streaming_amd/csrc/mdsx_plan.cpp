@@ -180,7 +180,9 @@ void apply_tuning(mdsx_plan* p) {
     if (key == "tile" && (v == 64 || v == 128 || v == 256)) {
       const int64_t per_row = 4 * int64_t(p->ncols) + 12 * int64_t(p->nvar);
       if (per_row * v <= 64 * 1024) p->tile_rows = int(v);
-    } else if (key == "unroll" && (v == 2 || v == 4 || v == 8)) {
+    } else if (key == "gmin" && v >= 0) {
+      p->gather_min = int(v);
+    } else if (key == "unroll" && (v == 4 || v == 6)) {
       p->unroll = int(v);
     } else if (key == "gk" && (v == 1 || v == 2 || v == 4)) {
       p->gather_chunks = int(v);
