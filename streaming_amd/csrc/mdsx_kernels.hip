@@ -294,35 +294,58 @@ __device__ __forceinline__ uint4 byte_mask(uint32_t a, uint32_t b) {
   return make_uint4(m[0], m[1], m[2], m[3]);
 }
 
-// Strict UTF-8 well-formedness (what bytes.decode('utf-8') accepts, encodings.py:80-81) of the
-// 16 bytes of `v` at segment positions pos0 .. pos0+15 of a segment of `len` bytes, given the 3
-// bytes before them in pw (bytes 1..3 of the previous chunk's last dword; zero before the
-// segment start).
-__device__ __forceinline__ bool utf8_chunk_bad(const uint4 v, uint32_t pw, int64_t pos0,
-                                               int64_t len) {
-  uint32_t p1 = (pw >> 24) & 0xffu, p2 = (pw >> 16) & 0xffu, p3 = (pw >> 8) & 0xffu;
+// ---- strict UTF-8 well-formedness, 4 bytes per dword op (SWAR) ------------------------------
+// What bytes.decode('utf-8') accepts (encodings.py:80-81; Unicode Table 3-7): every byte is
+// checked against its 3 predecessors. Per-byte predicates are bit 7 of each byte lane.
+__device__ __forceinline__ uint32_t hi_c0(uint32_t y) { return y & (y << 1) & 0x80808080u; }
+__device__ __forceinline__ uint32_t hi_e0(uint32_t y) {
+  return y & (y << 1) & (y << 2) & 0x80808080u;
+}
+__device__ __forceinline__ uint32_t hi_f0(uint32_t y) {
+  return y & (y << 1) & (y << 2) & (y << 3) & 0x80808080u;
+}
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t v) {  // bit 7 set where the byte is 0
+  return ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v) & 0x80808080u;
+}
+
+// Error bits of dword x given the dword before it (p): lone / missing continuation bytes,
+// C0, C1, F5..FF, overlong E0/F0 forms, surrogates (ED A0..BF), code points > U+10FFFF.
+__device__ __forceinline__ uint32_t utf8_dword_err(uint32_t x, uint32_t p) {
+  const uint32_t p1 = alignbyte(x, p, 3), p2 = alignbyte(x, p, 2), p3 = alignbyte(x, p, 1);
+  const uint32_t cont = x & ~(x << 1) & 0x80808080u;
+  const uint32_t need = hi_c0(p1) | hi_e0(p2) | hi_f0(p3);
+  uint32_t err = need ^ cont;
+  err |= zero_bytes((x & 0xFEFEFEFEu) ^ 0xC0C0C0C0u);              // C0, C1
+  err |= ((x & 0x7F7F7F7Fu) + 0x0B0B0B0Bu) & x & 0x80808080u;      // F5..FF
+  const uint32_t b5 = (x << 2) & 0x80808080u, b45 = ((x << 2) | (x << 3)) & 0x80808080u;
+  err |= zero_bytes(p1 ^ 0xE0E0E0E0u) & ~b5 & 0x80808080u;         // E0 followed by < A0
+  err |= zero_bytes(p1 ^ 0xEDEDEDEDu) & b5;                        // ED followed by > 9F
+  err |= zero_bytes(p1 ^ 0xF0F0F0F0u) & ~b45 & 0x80808080u;        // F0 followed by < 90
+  err |= zero_bytes(p1 ^ 0xF4F4F4F4u) & b45;                       // F4 followed by > 8F
+  return err;
+}
+
+// 16 segment bytes `v` (bytes outside the segment already zeroed) and the dword before them
+// (zero before the segment start). `last`: v holds the segment's last byte, so a sequence still
+// open at the end of v is truncated. Zero bytes never err except after an unfinished lead byte,
+// which is exactly the truncated-sequence case.
+__device__ __forceinline__ bool utf8_chunk_bad(const uint4 v, uint32_t pw, bool last) {
   const bool ascii = ((v.x | v.y | v.z | v.w) & 0x80808080u) == 0;
-  if (ascii && p1 < 0xC0u && p2 < 0xE0u && p3 < 0xF0u) return false;
-  bool bad = false;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const uint32_t b = byte_of(v, j);
-    const int64_t pos = pos0 + j;
-    if (pos >= 0 && pos < len) {
-      const bool cont = (b & 0xC0u) == 0x80u;
-      const bool need = p1 >= 0xC0u || p2 >= 0xE0u || p3 >= 0xF0u;
-      bad |= cont != need;
-      bad |= b == 0xC0u || b == 0xC1u || b >= 0xF5u;
-      bad |= (p1 == 0xE0u && b < 0xA0u) || (p1 == 0xEDu && b > 0x9Fu) ||
-             (p1 == 0xF0u && b < 0x90u) || (p1 == 0xF4u && b > 0x8Fu);
-      bad |= (b >= 0xC0u && pos + 1 >= len) || (b >= 0xE0u && pos + 2 >= len) ||
-             (b >= 0xF0u && pos + 3 >= len);
-    }
-    p3 = p2;
-    p2 = p1;
-    p1 = b;
-  }
-  return bad;
+  if (ascii && hi_c0(pw) == 0) return false;  // no open sequence enters, none starts
+  uint32_t err = utf8_dword_err(v.x, pw) | utf8_dword_err(v.y, v.x) | utf8_dword_err(v.z, v.y) |
+                 utf8_dword_err(v.w, v.z);
+  if (last) err |= utf8_dword_err(0u, v.w);  // positions 16..18 after the segment end
+  return err != 0;
+}
+
+// Bytes of a 16-byte chunk at address D that lie in [lo, hi), others zeroed.
+__device__ __forceinline__ uint4 keep_range(const uint4 v, uint64_t D, uint64_t lo, uint64_t hi) {
+  const int64_t a = max(int64_t(lo) - int64_t(D), int64_t(0));
+  const int64_t b = min(int64_t(hi) - int64_t(D), int64_t(16));
+  if (a == 0 && b == 16) return v;
+  if (b <= a) return make_uint4(0, 0, 0, 0);
+  const uint4 m = byte_mask(uint32_t(a), uint32_t(b));
+  return make_uint4(v.x & m.x, v.y & m.y, v.z & m.z, v.w & m.w);
 }
 
 // Store the bytes of `chunk` (held by lane `le`, 16-byte aligned destination D) that fall in
@@ -388,19 +411,11 @@ __device__ __forceinline__ bool wave_copy(const uint8_t* src, uint8_t* dst, uint
       }
       const uint64_t D = dbeg + 16 * k;
       if (kUtf8) {
-        uint4 vout = out;
-        if (k == 0 && D < d0) {  // zero the bytes before the segment start
-          const uint32_t head = uint32_t(d0 - D);
-          const uint32_t m0 = head >= 4 ? 0u : (0xffffffffu << (8 * head));
-          const uint32_t m1 = head >= 8 ? 0u : head <= 4 ? 0xffffffffu : (0xffffffffu << (8 * (head - 4)));
-          const uint32_t m2 = head >= 12 ? 0u : head <= 8 ? 0xffffffffu : (0xffffffffu << (8 * (head - 8)));
-          const uint32_t m3 = head <= 12 ? 0xffffffffu : (0xffffffffu << (8 * (head - 12)));
-          vout = make_uint4(vout.x & m0, vout.y & m1, vout.z & m2, vout.w & m3);
-        }
+        const uint4 vout = keep_range(out, D, d0, dend);
         uint32_t pw = __shfl_up(vout.w, 1);
         if (lane == 0) pw = carry;
         carry = __shfl(vout.w, 63);
-        if (k < nchunks) bad |= utf8_chunk_bad(vout, pw, int64_t(D) - int64_t(d0), int64_t(len));
+        if (k < nchunks) bad |= utf8_chunk_bad(vout, pw, k == nchunks - 1);
       }
       if (k < nchunks && D >= d0 && D + 16 <= dend) st16<kNT>(D, out);
       if (kEdges) {  // kEdges == false: the caller guarantees 16-byte aligned dst and length
