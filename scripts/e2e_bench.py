@@ -1,0 +1,156 @@
+"""End-to-end (host-inclusive) decode rates for DESIGN.md, on one GPU.
+
+Writes synthetic shard files (config B, C, or E = B-compressible written with zstd) to a temp
+directory (page cache), then measures, in one process:
+  * host read (or zstd decompress) into pinned staging, all shards, `--workers` threads;
+  * H2D of the staged batch; device-resident decode; D2H of the decoded columns;
+  * the pipelined ShardPipeline (read/decompress -> pinned -> H2D -> decode), with and without
+    the D2H hand-off.
+Prints one JSON object.
+"""
+
+import argparse
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from streaming_amd.compression import compress  # noqa: E402
+from streaming_amd.decoder import BatchDecoder, Plan, make_batch, output_bytes  # noqa: E402
+from streaming_amd.pipeline import ShardFile, ShardPipeline, _fill, to_host  # noqa: E402
+from streaming_amd.synth import var_c_shards  # noqa: E402
+from streaming_amd.writer import encode_fixed_shard, shard_config_bytes  # noqa: E402
+
+
+def make_files(cfg, samples, out, workers):
+    rng = np.random.default_rng(5)
+    files = []
+    if cfg in ('B', 'E'):
+        names, encs, sizes = ['id', 'x'], ['int32', 'ndarray:float32:1024'], [4, 4096]
+        comp = 'zstd' if cfg == 'E' else None
+        config = shard_config_bytes(names, encs, sizes, comp, [], 1 << 26)
+        per = ((1 << 26) - 8 - len(config)) // (4100 + 4)
+        shards = []
+        for s0 in range(0, samples, per):
+            n = min(per, samples - s0)
+            if cfg == 'B':
+                x = rng.integers(0, 2**32, (n, 1024), dtype=np.uint32)
+            else:  # compressible: small integers as float32
+                x = rng.integers(0, 256, (n, 1024)).astype(np.float32)
+            shards.append((encode_fixed_shard(config, [np.arange(s0, s0 + n, dtype=np.int32), x]),
+                           n))
+    else:
+        names, encs, sizes = ['b', 'n', 's'], ['bytes', 'int', 'str'], [None, 8, None]
+        comp = None
+        data, counts, _ = var_c_shards(samples, seed=6)
+        shards = list(zip(data, counts))
+    from concurrent.futures import ThreadPoolExecutor
+
+    def write(i_raw):
+        i, (raw, n) = i_raw
+        path = os.path.join(out, f'shard.{i:05}.mds' + ('.zstd' if comp else ''))
+        blob = compress('zstd', raw) if comp else raw
+        with open(path, 'wb') as f:
+            f.write(blob)
+        return ShardFile(path, len(raw), n, comp), len(blob)
+
+    with ThreadPoolExecutor(workers) as ex:
+        res = list(ex.map(write, enumerate(shards)))
+    return Plan(names, encs, sizes), [r[0] for r in res], sum(r[1] for r in res)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--config', default='B', choices=['B', 'C', 'E'])
+    ap.add_argument('--samples', type=int, default=1_000_000)
+    ap.add_argument('--workers', type=int, default=16)
+    ap.add_argument('--per-batch', type=int, default=8)
+    ap.add_argument('--dir', default=None)
+    args = ap.parse_args()
+    torch.cuda.set_device(0)
+    tmp = tempfile.mkdtemp(prefix='mdsx_e2e_', dir=args.dir)
+    try:
+        t0 = time.perf_counter()
+        plan, files, file_bytes = make_files(args.config, args.samples, tmp, args.workers)
+        gen_s = time.perf_counter() - t0
+        raw_bytes = sum(f.raw_bytes for f in files)
+        rows = sum(f.samples for f in files)
+        res = {'config': args.config, 'samples': rows, 'shards': len(files),
+               'raw_bytes': raw_bytes, 'file_bytes': file_bytes, 'workers': args.workers,
+               'host_cpus': len(os.sched_getaffinity(0)), 'generate_s': gen_s}
+        # 1. stage everything into one pinned buffer (page cache -> pinned), threads
+        batch = make_batch(plan, [f.raw_bytes for f in files], [f.samples for f in files])
+        pinned = torch.empty(batch.buffer.numel(), dtype=torch.uint8, pin_memory=True)
+        view = pinned.numpy()
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(args.workers) as ex:
+            for rep in range(2):  # first pass warms the page cache
+                t0 = time.perf_counter()
+                list(ex.map(lambda i: _fill(view[batch.offsets[i]:batch.offsets[i] +
+                                                 files[i].raw_bytes], files[i]),
+                            range(len(files))))
+                read_s = time.perf_counter() - t0
+        res['host_read_or_decompress_GBps'] = raw_bytes / read_s / 1e9
+        # 2. H2D
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        batch.buffer.copy_(pinned, non_blocking=True)
+        torch.cuda.synchronize()
+        res['h2d_GBps'] = pinned.numel() / (time.perf_counter() - t0) / 1e9
+        # 3. device-resident decode
+        dec = BatchDecoder(plan, batch)
+        out = dec.run()
+        dec.check()
+        for _ in range(3):
+            dec.run()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(10):
+            dec.run()
+        torch.cuda.synchronize()
+        dec_s = (time.perf_counter() - t0) / 10
+        res['decode_resident_ms'] = dec_s * 1e3
+        res['decode_resident_samples_per_s'] = rows / dec_s
+        res['decode_resident_GiBps'] = raw_bytes / dec_s / 2**30
+        W = output_bytes(plan, out)
+        # 4. D2H of the outputs
+        to_host(dec.result())
+        t0 = time.perf_counter()
+        to_host(dec.result())
+        res['d2h_GBps'] = W / (time.perf_counter() - t0) / 1e9
+        del dec, out, batch
+        torch.cuda.empty_cache()
+        # 5. pipelined end to end
+        for d2h in (False, True):
+            pipe = ShardPipeline(plan, files, shards_per_batch=args.per_batch, depth=2,
+                                 workers=args.workers)
+            for b in pipe:  # warm-up pass (allocations, page cache)
+                pass
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            n = 0
+            for b in pipe:
+                n += b.rows
+                if d2h:
+                    to_host(b)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            pipe.close()
+            assert n == rows
+            key = 'e2e_with_d2h' if d2h else 'e2e_device_handoff'
+            res[key] = {'samples_per_s': rows / dt, 'raw_GiBps': raw_bytes / dt / 2**30,
+                        'seconds': dt}
+        print(json.dumps(res, indent=1))
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+if __name__ == '__main__':
+    main()

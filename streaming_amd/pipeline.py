@@ -1,0 +1,213 @@
+"""End-to-end host path: shard files -> pinned staging -> HBM -> device decode (-> host).
+
+The reference reads every sample from the local cache file with ``open``/``seek``/``read``
+(``streaming/base/format/mds/reader.py:128-149``) after ``Stream.prepare_shard`` has downloaded
+and, for compressed shards, decompressed the file (``streaming/base/stream.py:319-412``,
+``compression.py:243-258``). :class:`ShardPipeline` is the device-side counterpart for a whole
+set of shards:
+
+1. host stage (thread pool): read each raw shard file -- or decompress its ``zip_data`` file
+   (zstd through libzstd) -- straight into a pinned staging buffer laid out as a device batch;
+2. H2D stage: one async copy per batch on a copy stream;
+3. decode stage: scan + decode kernels on the compute stream, waiting on the copy event;
+4. optional D2H of the decoded columns into pinned host memory (the host hand-off).
+
+Batches of shards flow through a ring of ``depth`` staging/device slots, so reading and
+decompressing batch i+1 overlaps the copy and decode of batch i.
+"""
+
+from __future__ import annotations
+
+import os
+import threading
+from concurrent.futures import ThreadPoolExecutor
+from dataclasses import dataclass
+from typing import Iterator, Optional, Sequence, Union
+
+import numpy as np
+import torch
+
+from streaming_amd.compression import decompress, decompress_into, get_compression_extension
+from streaming_amd.decoder import (BatchDecoder, DecodedBatch, DeviceBatch, Plan, RaggedColumn,
+                                   _layout, _tables)
+
+__all__ = ['ShardFile', 'ShardPipeline', 'shard_files_from_index', 'to_host']
+
+
+@dataclass
+class ShardFile:
+    """One shard as the pipeline reads it."""
+    path: str                      # raw file, or the compressed file if compression is set
+    raw_bytes: int                 # decompressed size (index.json raw_data.bytes)
+    samples: int
+    compression: Optional[str] = None
+
+
+def shard_files_from_index(dirname: str, index: dict, split: Optional[str] = None,
+                           prefer_raw: bool = True) -> list[ShardFile]:
+    """ShardFiles of an index.json: the raw file when present, else the compressed one."""
+    out = []
+    for info in index['shards']:
+        raw = os.path.join(dirname, split or '', info['raw_data']['basename'])
+        z = info.get('zip_data')
+        if (prefer_raw and os.path.exists(raw)) or not z:
+            out.append(ShardFile(raw, info['raw_data']['bytes'], info['samples']))
+        else:
+            out.append(
+                ShardFile(os.path.join(dirname, split or '', z['basename']),
+                          info['raw_data']['bytes'], info['samples'], info['compression']))
+    return out
+
+
+def _fill(view: np.ndarray, shard: ShardFile) -> None:
+    """Read or decompress one shard into its slice of the pinned staging buffer."""
+    if shard.compression:
+        with open(shard.path, 'rb') as f:
+            data = f.read()
+        ext = get_compression_extension(shard.compression)
+        if ext == 'zstd':
+            n = decompress_into(shard.compression, data, view)
+        else:
+            raw = decompress(shard.compression, data)
+            n = len(raw)
+            view[:n] = np.frombuffer(raw, np.uint8)
+    else:
+        with open(shard.path, 'rb', buffering=0) as f:
+            n = f.readinto(memoryview(view))
+    if n != shard.raw_bytes:
+        raise ValueError(f'{shard.path}: expected {shard.raw_bytes} raw bytes, got {n}')
+
+
+class _Slot:
+
+    def __init__(self, total: int, device: torch.device) -> None:
+        self.host = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+        self.dev = torch.empty(total, dtype=torch.uint8, device=device)
+        self.copied = torch.cuda.Event()
+        self.decoded = torch.cuda.Event()
+        self.decoder: Optional[BatchDecoder] = None
+        self.key: Optional[tuple] = None
+
+
+class ShardPipeline:
+    """Stream shard files through the device decoder in batches of ``shards_per_batch``.
+
+    Args:
+        plan: the shards' schema (all shards of a pipeline share it).
+        shards: shard files in order.
+        shards_per_batch: shards decoded per device batch.
+        depth: staging/device slots in flight (2 = double buffering).
+        workers: host threads reading / decompressing shards.
+        device: CUDA device.
+    """
+
+    def __init__(self,
+                 plan: Plan,
+                 shards: Sequence[ShardFile],
+                 shards_per_batch: int = 8,
+                 depth: int = 2,
+                 workers: int = 8,
+                 device: Union[str, torch.device, None] = None) -> None:
+        self.plan = plan
+        self.shards = list(shards)
+        self.per = max(1, shards_per_batch)
+        self.depth = max(1, depth)
+        dev = torch.device(device or 'cuda')
+        if dev.index is None:
+            dev = torch.device('cuda', torch.cuda.current_device())
+        self.device = dev
+        self.groups = [self.shards[i:i + self.per] for i in range(0, len(self.shards), self.per)]
+        biggest = max((_layout([s.raw_bytes for s in g])[1] for g in self.groups), default=0)
+        self.slots = [_Slot(biggest, dev) for _ in range(min(self.depth, len(self.groups)))]
+        self.pool = ThreadPoolExecutor(max_workers=max(1, workers))
+        self.copy_stream = torch.cuda.Stream(dev)
+        self._lock = threading.Lock()
+
+    def _stage(self, slot: _Slot, group: Sequence[ShardFile]):
+        sizes = [s.raw_bytes for s in group]
+        offsets, total = _layout(sizes)
+        view = slot.host.numpy()
+        futs = [
+            self.pool.submit(_fill, view[o:o + s.raw_bytes], s) for o, s in zip(offsets, group)
+        ]
+        return futs, sizes, offsets, total
+
+    def _batch(self, slot: _Slot, group, sizes, offsets, total) -> DeviceBatch:
+        raw, tile_shard, row0, rows, tiles = _tables(sizes, [s.samples for s in group], offsets,
+                                                     self.plan.tile_rows)
+        dev = self.device
+        return DeviceBatch(slot.dev[:total], torch.from_numpy(raw).to(dev, non_blocking=False),
+                           torch.from_numpy(tile_shard).to(dev) if tiles else torch.zeros(
+                               1, dtype=torch.int32, device=dev), offsets, sizes,
+                           [s.samples for s in group], row0, tiles, rows, self.plan.tile_rows)
+
+    def __iter__(self) -> Iterator[DecodedBatch]:
+        """Decoded batches in order (device tensors, valid until the slot is reused ``depth``
+        batches later; clone or :func:`to_host` them to keep them)."""
+        compute = torch.cuda.current_stream(self.device)
+        pending = []  # (slot, futures, sizes, offsets, total, group)
+        ngroups = len(self.groups)
+        for i in range(min(len(self.slots), ngroups)):
+            pending.append((self.slots[i], *self._stage(self.slots[i], self.groups[i]),
+                            self.groups[i]))
+        for gi in range(ngroups):
+            slot, futs, sizes, offsets, total, group = pending.pop(0)
+            for f in futs:
+                f.result()
+            with torch.cuda.stream(self.copy_stream):
+                self.copy_stream.wait_event(slot.decoded)  # device slot free again
+                slot.dev[:total].copy_(slot.host[:total], non_blocking=True)
+                slot.copied.record(self.copy_stream)
+            compute.wait_event(slot.copied)
+            batch = self._batch(slot, group, sizes, offsets, total)
+            key = (tuple(sizes), tuple(s.samples for s in group))
+            if slot.decoder is None or slot.key != key:
+                slot.decoder = BatchDecoder(self.plan, batch)
+                slot.key = key
+            else:
+                slot.decoder.batch = batch
+                slot.decoder._abi = batch.abi()
+                if self.plan.num_var:
+                    slot.decoder._sized = False  # ragged totals differ per batch: re-size
+            out = slot.decoder.run()
+            slot.decoded.record(compute)
+            nxt = gi + len(self.slots)
+            if nxt < ngroups:
+                # the host buffer may be refilled once its H2D copy has completed
+                slot.copied.synchronize()
+                pending.append((slot, *self._stage(slot, self.groups[nxt]), self.groups[nxt]))
+            yield out
+        # surface kernel-reported errors of the last batches
+        for slot in self.slots:
+            if slot.decoder is not None:
+                slot.decoder.check()
+
+    def close(self) -> None:
+        self.pool.shutdown(wait=True)
+
+
+def to_host(decoded: DecodedBatch, pin: bool = True) -> dict[str, Union[np.ndarray, tuple]]:
+    """D2H hand-off of a decoded batch: numpy arrays (ragged columns as (values, offsets[, flags]))."""
+    out = {}
+    for name, col in decoded.columns.items():
+        if isinstance(col, RaggedColumn):
+            parts = [col.values, col.offsets] + ([col.flags] if col.flags is not None else [])
+            host = []
+            for t in parts:
+                h = torch.empty(t.shape, dtype=t.dtype, pin_memory=pin)
+                h.copy_(t, non_blocking=True)
+                host.append(h)
+            out[name] = host
+        else:
+            h = torch.empty(col.shape, dtype=col.dtype, pin_memory=pin)
+            h.copy_(col, non_blocking=True)
+            out[name] = h
+    torch.cuda.current_stream().synchronize()
+    res = {}
+    for name, v in out.items():
+        if isinstance(v, list):
+            res[name] = tuple(x.numpy() for x in v)
+        else:
+            res[name] = v.view(torch.uint8).numpy() if v.dtype in (torch.uint16, torch.uint32,
+                                                                   torch.uint64) else v.numpy()
+    return res
