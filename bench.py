@@ -44,14 +44,16 @@ def parse_args():
     ap.add_argument('--samples', type=int, default=1_000_000, help='samples per GPU')
     ap.add_argument('--cpu-seconds', type=float, default=10.0,
                     help='CPU baseline time budget (0 disables)')
+    ap.add_argument('--cpu-procs', type=int, default=1,
+                    help='CPU baseline processes (disjoint shard copies, one per core)')
     ap.add_argument('--no-verify', action='store_true')
     return ap.parse_args()
 
 
 def init_dist(args):
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
+    from streaming_amd.distributed import rank_info
+    info = rank_info()
+    world, rank, local = info.world_size, info.rank, info.local_rank
     if world > 1:
         torch.cuda.set_device(local)
         torch.distributed.init_process_group('nccl', device_id=torch.device('cuda', local))
@@ -96,23 +98,29 @@ def verify(args, plan, out, sources):
         raise SystemExit('PARITY FAILURE: decoded columns differ from the encoded sources')
 
 
-def cpu_baseline(args):
-    """Oracle per-sample reader (reference algorithm) on 1 host core, bounded sample."""
-    from oracle.mds_oracle import OracleMDSReader
+def _cpu_shard(config, seed):
+    """One 64 MiB shard of the workload written to a temp dir (oracle reader input)."""
     from streaming_amd.synth import var_c_shards
     from streaming_amd.writer import encode_fixed_shard, shard_config_bytes
-    tmp = tempfile.mkdtemp(prefix='mdsx_cpu_')
-    if args.config == 'B':
+    if config == 'B':
         n = 16352
         names, encs, sizes = ['id', 'x'], ['int32', 'ndarray:float32:1024'], [4, 4096]
-        config = shard_config_bytes(names, encs, sizes, None, [], 1 << 26)
-        rng = np.random.default_rng(7)
-        raw = encode_fixed_shard(config, [np.arange(n, dtype=np.int32),
-                                          rng.integers(0, 2**32, (n, 1024), dtype=np.uint32)])
+        cfg = shard_config_bytes(names, encs, sizes, None, [], 1 << 26)
+        rng = np.random.default_rng(seed)
+        raw = encode_fixed_shard(cfg, [np.arange(n, dtype=np.int32),
+                                       rng.integers(0, 2**32, (n, 1024), dtype=np.uint32)])
     else:
-        shards, counts, _ = var_c_shards(16000, seed=7)
+        shards, counts, _ = var_c_shards(16000, seed=seed)
         raw, n = shards[0], counts[0]
         names, encs, sizes = ['b', 'n', 's'], ['bytes', 'int', 'str'], [None, 8, None]
+    return raw, n, names, encs, sizes
+
+
+def _cpu_worker(config, seed, seconds, q):
+    """Oracle per-sample reader loop over one shard for `seconds` (one process = one core)."""
+    from oracle.mds_oracle import OracleMDSReader
+    raw, n, names, encs, sizes = _cpu_shard(config, seed)
+    tmp = tempfile.mkdtemp(prefix='mdsx_cpu_')
     path = os.path.join(tmp, 'shard.00000.mds')
     with open(path, 'wb') as f:
         f.write(raw)
@@ -120,29 +128,64 @@ def cpu_baseline(args):
             'column_encodings': encs, 'column_sizes': sizes, 'samples': n}
     reader = OracleMDSReader(tmp, None, info)
     offs = np.frombuffer(raw[4:4 + 4 * (n + 1)], np.uint32).astype(np.int64)
-    sizes = np.diff(offs).tolist()
+    row_bytes = np.diff(offs).tolist()
+    for i in range(min(n, 256)):  # warm the page cache and the interpreter
+        reader.get_item(i)
     done, nbytes, i = 0, 0, 0
     t0 = time.perf_counter()
     while True:
         reader.get_item(i)
-        nbytes += sizes[i]
+        nbytes += row_bytes[i]
         done += 1
         i = i + 1 if i + 1 < n else 0
-        if (done & 255) == 0 and time.perf_counter() - t0 >= args.cpu_seconds:
+        if (done & 255) == 0 and time.perf_counter() - t0 >= seconds:
             break
     dt = time.perf_counter() - t0
     os.remove(path)
     os.rmdir(tmp)
+    q.put((done, nbytes, dt))
+
+
+def cpu_baseline(args):
+    """The reference algorithm (oracle port) timed on host cores: `--cpu-procs` processes, each
+    looping the per-sample reader over its own shard; aggregate samples/s."""
+    import multiprocessing as mp
+    procs = max(1, args.cpu_procs)
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_cpu_worker, args=(args.config, 7 + k, args.cpu_seconds, q))
+          for k in range(procs)]
+    for p in ps:
+        p.start()
+    res = [q.get() for _ in ps]
+    for p in ps:
+        p.join()
+    done = sum(r[0] for r in res)
+    nbytes = sum(r[1] for r in res)
+    dt = max(r[2] for r in res)
     return {
         'value': done / dt,
         'unit': 'samples/s',
         'gib_per_s': nbytes / dt / 2**30,
-        'cores': 1,
+        'cores': procs,
         'kind': 'port',
         'sample': (f'oracle per-sample MDSReader loop (open/seek/read + frombuffer per sample, '
-                   f'mds/reader.py:103-149) over one 64 MiB config-{args.config} shard from '
-                   f'page cache, {done} samples in {dt:.1f} s'),
+                   f'mds/reader.py:103-149; encodings.py:760-773) over a 64 MiB config-'
+                   f'{args.config} shard from page cache per process, {procs} process(es), '
+                   f'{done} samples in {dt:.1f} s'),
     }
+
+
+def committed_traffic(config):
+    """Per-launch HBM bytes of the decode kernel from the newest committed rocprofv3 PMC run of
+    this benchmark (FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM, + WRITE_SIZE)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(HERE, 'profiles', 'r*', f'pmc_bench_{config}_summary.json')))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        summ = json.load(f)
+    return summ.get('hbm_traffic_bytes_per_launch'), os.path.relpath(files[-1], HERE)
 
 
 def main():
@@ -171,11 +214,8 @@ def main():
     torch.cuda.synchronize(dev)
     barrier(world)
     t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
+    from streaming_amd.distributed import max_over_ranks
+    elapsed = max_over_ranks(t1 - t0, device=dev)
     dec.check()
     if not args.no_verify:
         verify(args, plan, dec.result(), sources)
@@ -193,6 +233,7 @@ def main():
 
     if rank == 0:
         cpu = cpu_baseline(args) if args.cpu_seconds > 0 else None
+        traffic, traffic_src = committed_traffic(args.config)
         line = {
             'metric': METRIC,
             'value': value,
@@ -223,7 +264,8 @@ def main():
                 'peak': HBM_PEAK_GBS,
                 'unit': 'GB/s',
                 'frac': achieved / HBM_PEAK_GBS,
-                'traffic': None,
+                'traffic': traffic,
+                'traffic_source': traffic_src,
                 'algorithmic_bytes_per_launch': R + W,
                 'kernel_ms': kern_s * 1e3,
                 'scan_ms': float(np.mean(scan_ms)),

@@ -20,6 +20,7 @@ from torch.utils.data import Dataset
 
 from streaming_amd.array import Array
 from streaming_amd.decoder import DecodedBatch, decode_batch, stage_shards
+from streaming_amd.distributed import owned_shards
 from streaming_amd.reader import MDSReader, get_plan, load_index, reader_from_json
 from streaming_amd.spanner import Spanner
 
@@ -28,9 +29,7 @@ __all__ = ['LocalDataset', 'shard_assignment']
 
 def shard_assignment(num_shards: int, rank: int, world_size: int) -> list[int]:
     """Shards owned by ``rank``: round-robin, imbalance <= 1 shard, no data exchange."""
-    if not (0 <= rank < world_size):
-        raise ValueError(f'rank {rank} outside world of {world_size}')
-    return list(range(rank, num_shards, world_size))
+    return owned_shards(num_shards, rank, world_size)
 
 
 class LocalDataset(Array, Dataset):
