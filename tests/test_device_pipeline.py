@@ -1,0 +1,97 @@
+"""GPU: the host pipeline (files / zstd -> pinned -> H2D -> decode) and the Stream plugin give
+the reference's outputs."""
+
+import hashlib
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from streaming_amd.decoder import Plan, RaggedColumn
+from streaming_amd.pipeline import ShardPipeline, shard_files_from_index, to_host
+from streaming_amd.plugin import make_device_stream
+from tests import golden_util as gu
+from tests.test_plugin import FakeStream, _ref_like_reader
+
+pytestmark = pytest.mark.gpu
+
+
+def _merge(parts):
+    """Concatenate per-batch device outputs into reference-format column arrays."""
+    merged = {}
+    for name in parts[0]:
+        vals = [p[name] for p in parts]
+        if isinstance(vals[0], RaggedColumn):
+            values = np.concatenate([v.values.cpu().numpy() for v in vals])
+            offs, base = [np.zeros(1, np.int64)], 0
+            for v in vals:
+                o = v.offsets.cpu().numpy()
+                offs.append(o[1:] + base)
+                base += int(o[-1])
+            merged[name] = (values, np.concatenate(offs))
+        else:
+            merged[name] = np.concatenate(
+                [v.reshape(v.shape[0], -1).view(torch.uint8).cpu().numpy() for v in vals])
+    return merged
+
+
+@pytest.mark.parametrize('name,per', [('zstd', 1), ('config_c_small', 1), ('config_a', 5),
+                                      ('config_a', 64), ('wide', 3)])
+def test_pipeline_matches_reference(name, per):
+    d = os.path.join(gu.GOLDEN, name)
+    idx = gu.index(name)
+    info = idx['shards'][0]
+    plan = Plan(info['column_names'], info['column_encodings'], info['column_sizes'])
+    files = shard_files_from_index(d, idx)
+    pipe = ShardPipeline(plan, files, shards_per_batch=per, depth=2, workers=4)
+    parts = []
+    for b in pipe:
+        parts.append({k: (RaggedColumn(v.values.clone(), v.offsets.clone()) if isinstance(
+            v, RaggedColumn) else v.clone()) for k, v in b.columns.items()})
+    pipe.close()
+    m = gu.manifest()[name]['columns']
+    for cname, v in _merge(parts).items():
+        if isinstance(v, tuple):
+            assert hashlib.sha256(v[0].tobytes()).hexdigest() == m[cname]['values']
+            assert hashlib.sha256(v[1].tobytes()).hexdigest() == m[cname]['offsets']
+        else:
+            assert hashlib.sha256(v.tobytes()).hexdigest() == m[cname]['rows']
+
+
+def test_to_host_handoff():
+    d = os.path.join(gu.GOLDEN, 'kat')
+    idx = gu.index('kat')
+    info = idx['shards'][0]
+    plan = Plan(info['column_names'], info['column_encodings'], info['column_sizes'])
+    pipe = ShardPipeline(plan, shard_files_from_index(d, idx), workers=1)
+    host = to_host(next(iter(pipe)))
+    pipe.close()
+    assert host['a'].tolist() == [-2, 7]
+    vals, offs, flags = host['s']
+    assert bytes(vals[offs[0]:offs[1]]).decode() == 'hé' and flags.tolist() == [0, 0]
+
+
+@pytest.mark.parametrize('name', ['kat', 'scalars', 'bad_utf8'])
+def test_plugin_stream_get_item(name):
+    d = os.path.join(gu.GOLDEN, name)
+
+    class Base(FakeStream):
+
+        def get_shards(self, world, allow_unsafe_types):
+            return [_ref_like_reader(info, self.local) for info in gu.index(name)['shards']]
+
+    shards = make_device_stream(Base)(d).get_shards(None, False)
+    expected = gu.items(name)
+    k = 0
+    for r in shards:
+        for i in range(len(r)):
+            rec = expected[k]
+            if any(w['t'] == 'error' for w in rec.values()):
+                with pytest.raises(UnicodeDecodeError):
+                    r[i]
+            else:
+                s = r[i]
+                assert {c: gu.value_record(v) for c, v in s.items()} == rec
+            k += 1
+    assert k == len(expected)
