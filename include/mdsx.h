@@ -164,6 +164,28 @@ int mdsx_decode_shards(const mdsx_plan* plan, const mdsx_batch* batch,
                        const mdsx_column_out* outs, void* d_workspace, uint64_t workspace_bytes,
                        void* stream);
 
+/* ---- batch gather by sample id ---------------------------------------------
+ * out[k] = column[idx[k]] over already-decoded columns: the device side of the reference's
+ * per-sample iteration over a worker's sample ids (StreamingDataset.__iter__ ->
+ * _each_sample_id -> get_item, dataset.py:1430-1473,1237-1293). idx: device int64[m] of rows of
+ * the decoded batch (no -1 padding: the reference skips those ids). The caller zeroes the
+ * 16-byte status record at the start of the workspace before a gather sequence; out-of-range
+ * ids report MDSX_E_BOUNDS there. Ragged columns: mdsx_gather_ragged_scan writes dst_offsets
+ * (int64[m + 1]) and the total (d_total, device int64, may be NULL), then
+ * mdsx_gather_ragged_copy (same idx, workspace and stream) copies the values (and str flags). */
+uint64_t mdsx_gather_workspace_bytes(uint64_t m);
+int mdsx_gather_fixed(const void* src, uint64_t src_rows, uint64_t row_bytes, const int64_t* idx,
+                      uint64_t m, void* dst, void* d_workspace, uint64_t workspace_bytes,
+                      void* stream);
+int mdsx_gather_ragged_scan(const int64_t* src_offsets, uint64_t src_rows, const int64_t* idx,
+                            uint64_t m, int64_t* dst_offsets, void* d_workspace,
+                            uint64_t workspace_bytes, int64_t* d_total, void* stream);
+int mdsx_gather_ragged_copy(const uint8_t* src_values, const int64_t* src_offsets,
+                            const uint8_t* src_flags, uint64_t src_rows, const int64_t* idx,
+                            uint64_t m, uint8_t* dst_values, uint64_t dst_capacity,
+                            int64_t* dst_offsets, uint8_t* dst_flags, void* d_workspace,
+                            uint64_t workspace_bytes, void* stream);
+
 /* ---- diagnostics ---------------------------------------------------------------------------
  * HBM roofline probe: a streaming 16-byte-per-lane device-to-device copy of `bytes` (multiple of
  * 16, 16-byte aligned pointers) on `stream`. Not part of the decode path: it measures what a

@@ -55,6 +55,10 @@ EXPORTED_SYMBOLS = (
     'mdsx_scan_shards',
     'mdsx_decode_shards',
     'mdsx_copy_probe',
+    'mdsx_gather_workspace_bytes',
+    'mdsx_gather_fixed',
+    'mdsx_gather_ragged_scan',
+    'mdsx_gather_ragged_copy',
 )
 
 
@@ -133,6 +137,16 @@ def _declare(handle: ctypes.CDLL) -> None:
     handle.mdsx_decode_shards.argtypes = [vp, pb, ctypes.POINTER(ColumnOut), vp, c_u64, vp]
     handle.mdsx_copy_probe.restype = c_int
     handle.mdsx_copy_probe.argtypes = [vp, vp, c_u64, vp]
+    handle.mdsx_gather_workspace_bytes.restype = c_u64
+    handle.mdsx_gather_workspace_bytes.argtypes = [c_u64]
+    handle.mdsx_gather_fixed.restype = c_int
+    handle.mdsx_gather_fixed.argtypes = [vp, c_u64, c_u64, vp, c_u64, vp, vp, c_u64, vp]
+    handle.mdsx_gather_ragged_scan.restype = c_int
+    handle.mdsx_gather_ragged_scan.argtypes = [vp, c_u64, vp, c_u64, vp, vp, c_u64, vp, vp]
+    handle.mdsx_gather_ragged_copy.restype = c_int
+    handle.mdsx_gather_ragged_copy.argtypes = [
+        vp, vp, vp, c_u64, vp, c_u64, vp, c_u64, vp, vp, vp, c_u64, vp
+    ]
 
 
 def lib() -> ctypes.CDLL:

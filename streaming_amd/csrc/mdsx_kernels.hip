@@ -894,6 +894,143 @@ __global__ __launch_bounds__(kBlock) void copy_probe_kernel(const uint4* __restr
   for (; i < n; i += stride) st16<true>(reinterpret_cast<uint64_t>(dst + i), ld16<true>(src + i));
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Batch gather by sample id: out[k] = column[idx[k]] for decoded columns, the
+// device side of StreamingDataset.__iter__'s per-sample get_item over a worker's sample ids
+// (dataset.py:1430-1473). One launch sequence per column.
+
+constexpr int kGatherRowTile = 256;  // rows of the output per workgroup
+
+// Fixed column: one output row per wave (rows > 16 bytes) or per lane (<= 16 bytes).
+template <bool kNT>
+__global__ __launch_bounds__(kBlock) void gather_fixed_kernel(const uint8_t* src, uint64_t nsrc,
+                                                              uint32_t row_bytes,
+                                                              const int64_t* idx, uint64_t m,
+                                                              uint8_t* dst, mdsx_status* st) {
+  const uint64_t k0 = uint64_t(blockIdx.x) * kGatherRowTile;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (row_bytes <= uint32_t(kSmallMax)) {
+    const uint64_t k = k0 + threadIdx.x;
+    if (k < m) {
+      const int64_t r = idx[k];
+      if (r < 0 || uint64_t(r) >= nsrc) {
+        report(st, MDSX_E_BOUNDS, -1, int(k), -1);
+      } else {
+        const uint8_t* p = src + uint64_t(r) * row_bytes;  // both rows aligned to row_bytes'
+        uint8_t* q = dst + k * row_bytes;                    // power-of-two factor
+        switch (row_bytes) {
+          case 1: *q = *p; break;
+          case 2: *reinterpret_cast<uint16_t*>(q) = *reinterpret_cast<const uint16_t*>(p); break;
+          case 4: *reinterpret_cast<uint32_t*>(q) = *reinterpret_cast<const uint32_t*>(p); break;
+          case 8: *reinterpret_cast<uint2*>(q) = *reinterpret_cast<const uint2*>(p); break;
+          case 16: *reinterpret_cast<uint4*>(q) = *reinterpret_cast<const uint4*>(p); break;
+          default:
+            for (uint32_t j = 0; j < row_bytes; ++j) q[j] = p[j];
+        }
+      }
+    }
+    return;
+  }
+  const bool aligned = (row_bytes & 15) == 0;
+  for (int i = wave; i < kGatherRowTile; i += kBlock / 64) {
+    const uint64_t k = k0 + i;
+    if (k >= m) break;  // wave-uniform
+    const int64_t r = idx[k];
+    if (r < 0 || uint64_t(r) >= nsrc) {
+      if (lane == 0) report(st, MDSX_E_BOUNDS, -1, int(k), -1);
+      continue;
+    }
+    if (aligned)
+      wave_copy<false, 4, kNT, false>(src + uint64_t(r) * row_bytes, dst + k * row_bytes,
+                                      row_bytes, lane);
+    else
+      wave_copy<false, 4, kNT, true>(src + uint64_t(r) * row_bytes, dst + k * row_bytes,
+                                     row_bytes, lane);
+  }
+}
+
+// Ragged column, pass 1: selected lengths -> local exclusive offsets + per-tile totals.
+__global__ __launch_bounds__(kBlock) void gather_len_kernel(const int64_t* src_off, uint64_t nsrc,
+                                                            const int64_t* idx, uint64_t m,
+                                                            int64_t* dst_off, int64_t* tile_total,
+                                                            mdsx_status* st) {
+  __shared__ int64_t s_wsum[kBlock / 64];
+  const uint64_t k = uint64_t(blockIdx.x) * kGatherRowTile + threadIdx.x;
+  int64_t len = 0;
+  if (k < m) {
+    const int64_t r = idx[k];
+    if (r < 0 || uint64_t(r) >= nsrc)
+      report(st, MDSX_E_BOUNDS, -1, int(k), -1);
+    else
+      len = src_off[r + 1] - src_off[r];
+  }
+  int64_t total;
+  const int64_t excl = block_exclusive_scan(len, s_wsum, &total);
+  if (k < m) dst_off[k] = excl;
+  if (threadIdx.x == 0) tile_total[blockIdx.x] = total;
+}
+
+// Exclusive scan of n tile totals (one workgroup); total -> *out_total and dst_off[m].
+__global__ __launch_bounds__(kBlock) void scan_tile_totals_kernel(const int64_t* in, int64_t* out,
+                                                                  uint32_t n, int64_t* dst_off,
+                                                                  uint64_t m, int64_t* out_total) {
+  __shared__ int64_t s_wsum[kBlock / 64];
+  int64_t carry = 0;
+  for (uint32_t base = 0; base < n; base += kBlock) {
+    const uint32_t k = base + threadIdx.x;
+    const int64_t x = k < n ? in[k] : 0;
+    int64_t total;
+    const int64_t excl = block_exclusive_scan(x, s_wsum, &total);
+    if (k < n) out[k] = carry + excl;
+    carry += total;
+  }
+  if (threadIdx.x == 0) {
+    dst_off[m] = carry;
+    if (out_total) *out_total = carry;
+  }
+}
+
+// Ragged column, pass 2: final offsets, flags, and one row per wave copied.
+template <bool kNT>
+__global__ __launch_bounds__(kBlock) void gather_copy_kernel(
+    const uint8_t* src_vals, const int64_t* src_off, const uint8_t* src_flags, uint64_t nsrc,
+    const int64_t* idx, uint64_t m, uint8_t* dst_vals, uint64_t capacity, int64_t* dst_off,
+    uint8_t* dst_flags, const int64_t* tile_prefix, mdsx_status* st) {
+  __shared__ int64_t s_dst[kGatherRowTile];
+  __shared__ int64_t s_src[kGatherRowTile];
+  __shared__ int64_t s_len[kGatherRowTile];
+  const uint64_t k0 = uint64_t(blockIdx.x) * kGatherRowTile;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  {
+    const uint64_t k = k0 + threadIdx.x;
+    int64_t len = -1;
+    if (k < m) {
+      const int64_t off = tile_prefix[blockIdx.x] + dst_off[k];
+      dst_off[k] = off;
+      s_dst[threadIdx.x] = off;
+      const int64_t r = idx[k];
+      if (r >= 0 && uint64_t(r) < nsrc) {
+        s_src[threadIdx.x] = src_off[r];
+        len = src_off[r + 1] - src_off[r];
+        if (uint64_t(off + len) > capacity) {
+          report(st, MDSX_E_CAPACITY, -1, int(k), -1);
+          len = -1;
+        }
+        if (dst_flags) dst_flags[k] = src_flags ? src_flags[r] : 0;
+      }
+    }
+    s_len[threadIdx.x] = len;
+  }
+  __syncthreads();
+  for (int i = wave; i < kGatherRowTile; i += kBlock / 64) {
+    if (k0 + i >= m) break;
+    const int64_t len = s_len[i];
+    if (len <= 0) continue;  // wave-uniform
+    wave_copy<false, 4, kNT, true>(src_vals + s_src[i], dst_vals + s_dst[i], uint64_t(len), lane);
+  }
+}
+
 }  // namespace mdsx_kernels
 
 using namespace mdsx_kernels;
@@ -976,6 +1113,82 @@ int mdsx_decode_shards(const mdsx_plan* plan, const mdsx_batch* batch,
   }
 #undef MDSX_GATHER
   return hip_check(hipGetLastError(), "gather_ragged_kernel launch");
+}
+
+
+uint64_t mdsx_gather_workspace_bytes(uint64_t m) {
+  const uint64_t tiles = (m + kGatherRowTile - 1) / kGatherRowTile;
+  return 256 + 2 * ((tiles * 8 + 255) & ~uint64_t(255));
+}
+
+static int gather_ws(void* ws, uint64_t ws_bytes, uint64_t m, mdsx_status** st, int64_t** tt,
+                     int64_t** tp) {
+  if (!ws || ws_bytes < mdsx_gather_workspace_bytes(m))
+    return mdsx::fail(MDSX_E_ARG, "mdsx_gather: workspace smaller than mdsx_gather_workspace_bytes");
+  const uint64_t tiles = (m + kGatherRowTile - 1) / kGatherRowTile;
+  uint8_t* b = static_cast<uint8_t*>(ws);
+  *st = reinterpret_cast<mdsx_status*>(b);
+  *tt = reinterpret_cast<int64_t*>(b + 256);
+  *tp = reinterpret_cast<int64_t*>(b + 256 + ((tiles * 8 + 255) & ~uint64_t(255)));
+  return MDSX_OK;
+}
+
+int mdsx_gather_fixed(const void* src, uint64_t src_rows, uint64_t row_bytes, const int64_t* idx,
+                      uint64_t m, void* dst, void* d_workspace, uint64_t workspace_bytes,
+                      void* stream) {
+  mdsx_status* st;
+  int64_t *tt, *tp;
+  int rc = gather_ws(d_workspace, workspace_bytes, m, &st, &tt, &tp);
+  if (rc != MDSX_OK) return rc;
+  if (!src || !idx || !dst || row_bytes == 0 || row_bytes >= (uint64_t(1) << 32))
+    return mdsx::fail(MDSX_E_ARG, "mdsx_gather_fixed: bad argument");
+  if (m == 0) return MDSX_OK;
+  const unsigned grid = unsigned((m + kGatherRowTile - 1) / kGatherRowTile);
+  hipLaunchKernelGGL((gather_fixed_kernel<true>), dim3(grid), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), static_cast<const uint8_t*>(src), src_rows,
+                     uint32_t(row_bytes), idx, m, static_cast<uint8_t*>(dst), st);
+  return hip_check(hipGetLastError(), "gather_fixed_kernel launch");
+}
+
+int mdsx_gather_ragged_scan(const int64_t* src_offsets, uint64_t src_rows, const int64_t* idx,
+                            uint64_t m, int64_t* dst_offsets, void* d_workspace,
+                            uint64_t workspace_bytes, int64_t* d_total, void* stream) {
+  mdsx_status* st;
+  int64_t *tt, *tp;
+  int rc = gather_ws(d_workspace, workspace_bytes, m, &st, &tt, &tp);
+  if (rc != MDSX_OK) return rc;
+  if (!src_offsets || !dst_offsets || (m && !idx))
+    return mdsx::fail(MDSX_E_ARG, "mdsx_gather_ragged_scan: bad argument");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const unsigned tiles = unsigned((m + kGatherRowTile - 1) / kGatherRowTile);
+  if (tiles) {
+    hipLaunchKernelGGL(gather_len_kernel, dim3(tiles), dim3(kBlock), 0, s, src_offsets, src_rows,
+                       idx, m, dst_offsets, tt, st);
+    rc = hip_check(hipGetLastError(), "gather_len_kernel launch");
+    if (rc != MDSX_OK) return rc;
+  }
+  hipLaunchKernelGGL(scan_tile_totals_kernel, dim3(1), dim3(kBlock), 0, s, tt, tp, tiles,
+                     dst_offsets, m, d_total);
+  return hip_check(hipGetLastError(), "scan_tile_totals_kernel launch");
+}
+
+int mdsx_gather_ragged_copy(const uint8_t* src_values, const int64_t* src_offsets,
+                            const uint8_t* src_flags, uint64_t src_rows, const int64_t* idx,
+                            uint64_t m, uint8_t* dst_values, uint64_t dst_capacity,
+                            int64_t* dst_offsets, uint8_t* dst_flags, void* d_workspace,
+                            uint64_t workspace_bytes, void* stream) {
+  mdsx_status* st;
+  int64_t *tt, *tp;
+  int rc = gather_ws(d_workspace, workspace_bytes, m, &st, &tt, &tp);
+  if (rc != MDSX_OK) return rc;
+  if (!src_offsets || !dst_offsets || (m && !idx) || (dst_capacity && (!dst_values || !src_values)))
+    return mdsx::fail(MDSX_E_ARG, "mdsx_gather_ragged_copy: bad argument");
+  if (m == 0) return MDSX_OK;
+  const unsigned tiles = unsigned((m + kGatherRowTile - 1) / kGatherRowTile);
+  hipLaunchKernelGGL((gather_copy_kernel<true>), dim3(tiles), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), src_values, src_offsets, src_flags,
+                     src_rows, idx, m, dst_values, dst_capacity, dst_offsets, dst_flags, tp, st);
+  return hip_check(hipGetLastError(), "gather_copy_kernel launch");
 }
 
 int mdsx_copy_probe(const void* d_src, void* d_dst, uint64_t bytes, void* stream) {

@@ -301,6 +301,59 @@ class DecodedBatch:
     def __getitem__(self, name: str) -> Union[torch.Tensor, RaggedColumn]:
         return self.columns[name]
 
+    def gather(self, ids: Union[torch.Tensor, Sequence[int], np.ndarray],
+               check: bool = True) -> 'DecodedBatch':
+        """Rows ``ids`` of every column, in that order (the device batch gather of the
+        reference's per-sample iteration over sample ids, ``dataset.py:1430-1473``; ids of -1,
+        the reference's padding, are skipped). Runs the ``mdsx_gather_*`` kernels."""
+        lib = _native.lib()
+        first = next(iter(self.columns.values()))
+        dev = first.values.device if isinstance(first, RaggedColumn) else first.device
+        idx = torch.as_tensor(ids, dtype=torch.int64).to(dev).reshape(-1)
+        idx = idx[idx != -1].contiguous()
+        m = int(idx.numel())
+        ws = torch.zeros(int(lib.mdsx_gather_workspace_bytes(m)), dtype=torch.uint8, device=dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        out: dict[str, Union[torch.Tensor, RaggedColumn]] = {}
+        for name, col in self.columns.items():
+            if isinstance(col, RaggedColumn):
+                offs = torch.empty(m + 1, dtype=torch.int64, device=dev)
+                total = torch.zeros(1, dtype=torch.int64, device=dev)
+                _check(
+                    lib.mdsx_gather_ragged_scan(col.offsets.data_ptr(), self.rows,
+                                                idx.data_ptr() if m else None, m, offs.data_ptr(),
+                                                ws.data_ptr(), ws.numel(), total.data_ptr(),
+                                                stream), 'mdsx_gather_ragged_scan')
+                cap = int(total.item())  # sizes the values buffer (host sync)
+                vals = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
+                flags = torch.zeros(m, dtype=torch.uint8, device=dev) if col.flags is not None \
+                    else None
+                _check(
+                    lib.mdsx_gather_ragged_copy(
+                        col.values.data_ptr() if col.values.numel() else None,
+                        col.offsets.data_ptr(), col.flags.data_ptr() if flags is not None else None,
+                        self.rows, idx.data_ptr() if m else None, m,
+                        vals.data_ptr() if cap else None, cap, offs.data_ptr(),
+                        flags.data_ptr() if flags is not None else None, ws.data_ptr(),
+                        ws.numel(), stream), 'mdsx_gather_ragged_copy')
+                out[name] = RaggedColumn(vals[:cap], offs, flags)
+            else:
+                row_shape = tuple(col.shape[1:])
+                dst = torch.empty((m, ) + row_shape, dtype=col.dtype, device=dev)
+                row_bytes = col[0].numel() * col.element_size() if col.shape[0] else \
+                    int(np.prod(row_shape, dtype=np.int64)) * col.element_size()
+                if m:
+                    _check(
+                        lib.mdsx_gather_fixed(col.data_ptr(), self.rows, row_bytes, idx.data_ptr(),
+                                              m, dst.data_ptr(), ws.data_ptr(), ws.numel(),
+                                              stream), 'mdsx_gather_fixed')
+                out[name] = dst
+        if check:
+            st = _native.Status.from_buffer_copy(ws[:16].cpu().numpy().tobytes())
+            if st.code != 0:
+                raise IndexError(f'sample id out of range at position {st.row} of the gather')
+        return DecodedBatch(out, m)
+
 
 def _status_error(status: _native.Status, plan: Plan) -> Exception:
     code = status.code

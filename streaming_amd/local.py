@@ -12,7 +12,7 @@ Same interface as the reference ``LocalDataset`` (``streaming/base/local.py:20-7
 
 from __future__ import annotations
 
-from typing import Any, Optional, Sequence, Union
+from typing import Any, Iterator, Optional, Sequence, Union
 
 import numpy as np
 import torch
@@ -53,6 +53,7 @@ class LocalDataset(Array, Dataset):
         ]
         self.num_samples = sum(shard.samples for shard in self.shards)
         self.spanner = Spanner(np.array([s.samples for s in self.shards], np.int64))
+        self._all: Optional[DecodedBatch] = None
 
     def __len__(self) -> int:
         return self.num_samples
@@ -64,6 +65,17 @@ class LocalDataset(Array, Dataset):
     def get_item(self, sample_id: int) -> dict[str, Any]:
         shard_id, index_in_shard = self.spanner[sample_id]
         return self.shards[shard_id][index_in_shard]
+
+    def iter_batches(self, sample_ids: Union[Sequence[int], np.ndarray, torch.Tensor],
+                     batch_size: int) -> Iterator[DecodedBatch]:
+        """Device batches of ``batch_size`` samples in the order of ``sample_ids`` (global ids,
+        ``-1`` padding skipped as the reference's ``_each_sample_id`` does,
+        ``dataset.py:1430-1473``): every shard decoded once, each batch gathered on device."""
+        if self._all is None:
+            self._all = self.decode_all()
+        ids = torch.as_tensor(np.asarray(sample_ids, np.int64)).reshape(-1)
+        for lo in range(0, ids.numel(), batch_size):
+            yield self._all.gather(ids[lo:lo + batch_size])
 
     def decode_all(self, shard_ids: Optional[Sequence[int]] = None,
                    check: bool = True) -> DecodedBatch:

@@ -1,0 +1,80 @@
+"""GPU: batch gather by sample id against the oracle's per-sample decode."""
+
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import mds_oracle
+from streaming_amd import LocalDataset
+from streaming_amd.decoder import RaggedColumn
+from streaming_amd.synth import fixed_b_batch_on_device
+from tests import golden_util as gu
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_rows(name):
+    """Per-sample column bytes of a golden set through the oracle, in global order."""
+    d = os.path.join(gu.GOLDEN, name)
+    rows = []
+    for info in gu.index(name)['shards']:
+        r = mds_oracle.OracleMDSReader(d, None, info)
+        for i in range(len(r)):
+            rows.append(dict(zip(r.column_names, r.split_sample(r.get_sample_data(i)))))
+    return rows
+
+
+@pytest.mark.parametrize('name', ['config_b_small', 'config_c_small', 'scalars', 'bad_utf8',
+                                  'wide', 'config_a'])
+def test_gather_matches_oracle(name):
+    rows = _oracle_rows(name)
+    n = len(rows)
+    rng = np.random.default_rng(len(name))
+    ids = rng.integers(0, n, 3 * n + 5)
+    ids[::7] = -1  # reference padding, skipped
+    ds = LocalDataset(os.path.join(gu.GOLDEN, name))
+    got = ds.decode_all().gather(ids)
+    keep = ids[ids != -1]
+    assert got.rows == len(keep)
+    for cname, col in got.columns.items():
+        if isinstance(col, RaggedColumn):
+            vals, offs = col.values.cpu().numpy(), col.offsets.cpu().numpy()
+            flags = col.flags.cpu().numpy() if col.flags is not None else None
+            for k, r in enumerate(keep):
+                assert vals[offs[k]:offs[k + 1]].tobytes() == rows[r][cname], (cname, k)
+                if flags is not None:
+                    assert flags[k] == (0 if mds_oracle.utf8_is_valid(rows[r][cname]) else 1)
+        else:
+            raw = col.reshape(col.shape[0], -1).view(torch.uint8).cpu().numpy()
+            for k, r in enumerate(keep):
+                assert raw[k].tobytes() == rows[r][cname], (cname, k)
+
+
+def test_iter_batches_order():
+    ds = LocalDataset(os.path.join(gu.GOLDEN, 'config_a'))
+    ids = np.random.default_rng(0).permutation(len(ds))
+    seen = []
+    for b in ds.iter_batches(ids, 256):
+        assert b.rows <= 256
+        seen.extend(b['number'].cpu().tolist())
+    want = [ds[int(i)]['number'] for i in ids[:500]]
+    assert seen[:500] == want
+    assert len(seen) == len(ds)
+
+
+def test_gather_out_of_range_raises():
+    ds = LocalDataset(os.path.join(gu.GOLDEN, 'kat'))
+    with pytest.raises(IndexError):
+        ds.decode_all().gather([0, 5])
+
+
+def test_gather_config_b_full_size_permutation():
+    synth = fixed_b_batch_on_device(1_000_000, seed=21)
+    from streaming_amd.decoder import decode_batch
+    dec = decode_batch(synth.plan, synth.batch)
+    perm = torch.randperm(1_000_000, device=dec['x'].device)
+    g = dec.gather(perm)
+    assert torch.equal(g['id'], synth.sources['id'][perm])
+    assert torch.equal(g['x'].view(torch.int32), synth.sources['x'].view(torch.int32)[perm])
