@@ -877,21 +877,27 @@ int hip_check(hipError_t e, const char* what) {
   return mdsx::fail(MDSX_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-// HBM roofline probe: a grid-stride 16-byte-per-lane copy (what a pure stream of the same bytes
-// achieves on this device), used to report the measured copy ceiling next to the decode rate.
+// HBM roofline probe: the fastest plain stream measured on MI355X (scripts/microbench/
+// copy_ceiling.hip): each workgroup copies a contiguous 256 KiB, 8 x 16 B per lane in flight,
+// non-temporal. Reported next to the decode rate as the measured copy ceiling.
+constexpr uint64_t kProbeBlock = 256 * 1024 / 16;  // 16-byte units per workgroup
 __global__ __launch_bounds__(kBlock) void copy_probe_kernel(const uint4* __restrict__ src,
                                                             uint4* __restrict__ dst, uint64_t n) {
-  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
-  uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
-  for (; i + 3 * stride < n; i += 4 * stride) {
-    const uint4 a = ld16<true>(src + i), b = ld16<true>(src + i + stride),
-                c = ld16<true>(src + i + 2 * stride), d = ld16<true>(src + i + 3 * stride);
-    st16<true>(reinterpret_cast<uint64_t>(dst + i), a);
-    st16<true>(reinterpret_cast<uint64_t>(dst + i + stride), b);
-    st16<true>(reinterpret_cast<uint64_t>(dst + i + 2 * stride), c);
-    st16<true>(reinterpret_cast<uint64_t>(dst + i + 3 * stride), d);
+  const uint64_t b0 = uint64_t(blockIdx.x) * kProbeBlock;
+  const uint64_t b1 = b0 + kProbeBlock < n ? b0 + kProbeBlock : n;
+  for (uint64_t base = b0; base < b1; base += kBlock * 8) {
+    uint4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint64_t i = base + u * kBlock + threadIdx.x;
+      if (i < b1) v[u] = ld16<true>(src + i);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint64_t i = base + u * kBlock + threadIdx.x;
+      if (i < b1) st16<true>(reinterpret_cast<uint64_t>(dst + i), v[u]);
+    }
   }
-  for (; i < n; i += stride) st16<true>(reinterpret_cast<uint64_t>(dst + i), ld16<true>(src + i));
 }
 
 
@@ -1197,8 +1203,7 @@ int mdsx_copy_probe(const void* d_src, void* d_dst, uint64_t bytes, void* stream
     return mdsx::fail(MDSX_E_ARG, "mdsx_copy_probe: 16-byte aligned pointers and size required");
   const uint64_t n = bytes / 16;
   if (n == 0) return MDSX_OK;
-  const uint64_t want = (n + kBlock - 1) / kBlock;
-  const unsigned grid = unsigned(want < 256 * 8 ? want : 256 * 8);
+  const unsigned grid = unsigned((n + kProbeBlock - 1) / kProbeBlock);
   hipLaunchKernelGGL(copy_probe_kernel, dim3(grid), dim3(kBlock), 0,
                      static_cast<hipStream_t>(stream), static_cast<const uint4*>(d_src),
                      static_cast<uint4*>(d_dst), n);
