@@ -47,6 +47,8 @@ def parse_args():
     ap.add_argument('--cpu-procs', type=int, default=1,
                     help='CPU baseline processes (disjoint shard copies, one per core)')
     ap.add_argument('--no-verify', action='store_true')
+    ap.add_argument('--no-copy-probe', dest='copy_probe', action='store_false',
+                    help='skip the same-run copy-ceiling measurement')
     return ap.parse_args()
 
 
@@ -188,6 +190,29 @@ def committed_traffic(config):
     return summ.get('hbm_traffic_bytes_per_launch'), os.path.relpath(files[-1], HERE)
 
 
+def copy_ceiling(batch, dev, iters=10):
+    """Median rate of a read+write streaming copy of the batch's shard bytes (GB/s)."""
+    from streaming_amd import _native
+    lib = _native.lib()
+    src = batch.buffer
+    dst = torch.empty_like(src)
+    stream = torch.cuda.current_stream(dev)
+    start = [torch.cuda.Event(enable_timing=True) for _ in range(iters + 1)]
+    end = [torch.cuda.Event(enable_timing=True) for _ in range(iters + 1)]
+    for i in range(iters + 1):
+        start[i].record(stream)
+        rc = lib.mdsx_copy_probe(src.data_ptr(), dst.data_ptr(), src.numel(), stream.cuda_stream)
+        end[i].record(stream)
+        if rc != 0:
+            raise RuntimeError(f'mdsx_copy_probe failed: {lib.mdsx_last_error().decode()}')
+    torch.cuda.synchronize(dev)
+    if not torch.equal(src[-4096:], dst[-4096:]):
+        raise RuntimeError('mdsx_copy_probe: copy mismatch')
+    ms = float(np.median([start[i].elapsed_time(end[i]) for i in range(1, iters + 1)]))
+    del dst
+    return {'GBps': 2 * src.numel() / ms / 1e6, 'ms': ms, 'bytes_per_launch': 2 * src.numel()}
+
+
 def main():
     args = parse_args()
     world, rank, local = init_dist(args)
@@ -231,6 +256,8 @@ def main():
     gibs = R * world * K / elapsed / 2**30
     achieved = (R + W) / kern_s / 1e9
 
+    copy = copy_ceiling(batch, dev) if args.copy_probe else None
+
     if rank == 0:
         cpu = cpu_baseline(args) if args.cpu_seconds > 0 else None
         traffic, traffic_src = committed_traffic(args.config)
@@ -269,6 +296,10 @@ def main():
                 'algorithmic_bytes_per_launch': R + W,
                 'kernel_ms': kern_s * 1e3,
                 'scan_ms': float(np.mean(scan_ms)),
+                # same-run streaming copy of the shard bytes (mdsx_copy_probe, the fastest copy
+                # shape measured on this part): the practical HBM ceiling next to the 8 TB/s peak
+                'copy_ceiling': copy,
+                'frac_of_copy_ceiling': achieved / copy['GBps'] if copy else None,
             },
             'cpu_baseline': cpu,
         }

@@ -186,6 +186,20 @@ int mdsx_gather_ragged_copy(const uint8_t* src_values, const int64_t* src_offset
                             int64_t* dst_offsets, uint8_t* dst_flags, void* d_workspace,
                             uint64_t workspace_bytes, void* stream);
 
+/* ---- dynamic ndarray columns ------------------------------------------------------------------
+ * Header parse of NDArray.decode (encodings.py:270-305) over a decoded MDSX_KIND_NDARRAY column
+ * (values with headers + offsets): per row the value dtype id (encodings.py:131-143; dtype_id
+ * is the static one of 'ndarray:<dtype>' or 0 for 'ndarray'), ndim, byte offset of the values
+ * inside `values`, element count, and out_bad = 1 where the reference's decode raises (unknown
+ * dtype, header past the row, value bytes != numel x itemsize). d_max_ndim (device int32, may
+ * be NULL) receives the largest ndim by atomicMax (caller zeroes it). mdsx_ndarray_shapes
+ * writes the shapes as int64[rows, shape_cols], padded with 1. */
+int mdsx_ndarray_meta(const uint8_t* values, const int64_t* offsets, uint64_t rows, int dtype_id,
+                      uint8_t* out_dtype, uint8_t* out_ndim, int64_t* out_data_offset,
+                      int64_t* out_numel, uint8_t* out_bad, int32_t* d_max_ndim, void* stream);
+int mdsx_ndarray_shapes(const uint8_t* values, const int64_t* offsets, uint64_t rows,
+                        int dtype_id, int32_t shape_cols, int64_t* out_shape, void* stream);
+
 /* ---- diagnostics ---------------------------------------------------------------------------
  * HBM roofline probe: a streaming 16-byte-per-lane device-to-device copy of `bytes` (multiple of
  * 16, 16-byte aligned pointers) on `stream`. Not part of the decode path: it measures what a

@@ -59,6 +59,8 @@ EXPORTED_SYMBOLS = (
     'mdsx_gather_fixed',
     'mdsx_gather_ragged_scan',
     'mdsx_gather_ragged_copy',
+    'mdsx_ndarray_meta',
+    'mdsx_ndarray_shapes',
 )
 
 
@@ -137,6 +139,10 @@ def _declare(handle: ctypes.CDLL) -> None:
     handle.mdsx_decode_shards.argtypes = [vp, pb, ctypes.POINTER(ColumnOut), vp, c_u64, vp]
     handle.mdsx_copy_probe.restype = c_int
     handle.mdsx_copy_probe.argtypes = [vp, vp, c_u64, vp]
+    handle.mdsx_ndarray_meta.restype = c_int
+    handle.mdsx_ndarray_meta.argtypes = [vp, vp, c_u64, c_int, vp, vp, vp, vp, vp, vp, vp]
+    handle.mdsx_ndarray_shapes.restype = c_int
+    handle.mdsx_ndarray_shapes.argtypes = [vp, vp, c_u64, c_int, ctypes.c_int32, vp, vp]
     handle.mdsx_gather_workspace_bytes.restype = c_u64
     handle.mdsx_gather_workspace_bytes.argtypes = [c_u64]
     handle.mdsx_gather_fixed.restype = c_int

@@ -1037,6 +1037,88 @@ __global__ __launch_bounds__(kBlock) void gather_copy_kernel(
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Dynamic ndarray columns ('ndarray', 'ndarray:<dtype>'): per-row header parse over the decoded
+// ragged values -- NDArray.decode (encodings.py:270-305): [dtype id: u8 if dynamic]
+// [ndim << 2 | shape dtype: u8][shape: ndim x u8/u16/u32/u64][values]. One row per lane.
+__device__ __forceinline__ bool value_dtype_ok(uint32_t id) {
+  return id == 8 || id == 9 || id == 16 || id == 17 || id == 18 || id == 32 || id == 33 ||
+         id == 34 || id == 64 || id == 65 || id == 66;
+}
+
+__device__ __forceinline__ uint64_t read_uint(const uint8_t* p, int nbytes) {
+  uint64_t v = 0;
+  for (int b = 0; b < nbytes; ++b) v |= uint64_t(p[b]) << (8 * b);
+  return v;
+}
+
+template <bool kShapes>
+__global__ __launch_bounds__(kBlock) void ndarray_meta_kernel(
+    const uint8_t* values, const int64_t* offsets, uint64_t rows, int dtype_id, uint8_t* out_dtype,
+    uint8_t* out_ndim, int64_t* out_data_offset, int64_t* out_numel, uint8_t* out_bad,
+    int32_t* max_ndim, int32_t shape_cols, int64_t* out_shape) {
+  const uint64_t r = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (r >= rows) return;
+  const int64_t b = offsets[r], e = offsets[r + 1];
+  const uint8_t* p = values + b;
+  const int64_t len = e - b;
+  int64_t pos = 0;
+  bool bad = false;
+  uint32_t id = uint32_t(dtype_id);
+  if (id == 0) {
+    if (len < 1) bad = true;
+    else id = p[pos++];
+    if (!bad && !value_dtype_ok(id)) bad = true;
+  }
+  uint32_t ndim = 0, code = 0;
+  if (!bad) {
+    if (pos + 1 > len) bad = true;
+    else {
+      const uint32_t byte = p[pos++];
+      ndim = byte >> 2;
+      code = byte & 3;
+    }
+  }
+  // shape = frombuffer(data[index:index + ndim * sbytes], shape dtype): a truncated header
+  // yields fewer dims (or raises when the tail is not whole dims); the values then start past
+  // the end and are empty.
+  const int sbytes = 1 << code;
+  const int64_t want = int64_t(ndim) * sbytes;
+  if (!bad && want > len - pos) {
+    if ((len - pos) % sbytes) bad = true;
+    else ndim = uint32_t((len - pos) / sbytes);
+  }
+  // numpy's size rule (PyArray_NewFromDescr): zero dims make the array empty, the product of
+  // the non-zero dims times the item size must fit in intp; dims above intp max raise.
+  const int64_t item = int64_t(id >> 3);
+  int64_t prod = item;
+  bool zero = false;
+  if (!bad) {
+    for (uint32_t k = 0; k < ndim; ++k) {
+      const uint64_t dim = read_uint(p + pos + k * sbytes, sbytes);
+      if (kShapes && int32_t(k) < shape_cols) out_shape[r * shape_cols + k] = int64_t(dim);
+      if (dim > uint64_t(INT64_MAX)) { bad = true; break; }
+      if (dim == 0) { zero = true; continue; }
+      if (__builtin_mul_overflow(prod, int64_t(dim), &prod)) { bad = true; break; }
+    }
+    pos = pos + want < len ? pos + want : len;
+  }
+  const int64_t numel = (bad || zero) ? 0 : prod / item;
+  // frombuffer(data[index:], dtype).reshape(shape): the value bytes must be exactly numel items
+  if (!bad && (len - pos) != numel * item) bad = true;
+  if (kShapes) {
+    for (int32_t k = int32_t(ndim); k < shape_cols; ++k) out_shape[r * shape_cols + k] = 1;
+    return;
+  }
+  out_dtype[r] = uint8_t(bad ? 0 : id);
+  out_ndim[r] = uint8_t(bad ? 0 : ndim);
+  out_data_offset[r] = b + pos;
+  out_numel[r] = bad ? 0 : numel;
+  out_bad[r] = bad ? 1 : 0;
+  if (!bad && max_ndim) atomicMax(max_ndim, int32_t(ndim));
+}
+
 }  // namespace mdsx_kernels
 
 using namespace mdsx_kernels;
@@ -1195,6 +1277,37 @@ int mdsx_gather_ragged_copy(const uint8_t* src_values, const int64_t* src_offset
                      static_cast<hipStream_t>(stream), src_values, src_offsets, src_flags,
                      src_rows, idx, m, dst_values, dst_capacity, dst_offsets, dst_flags, tp, st);
   return hip_check(hipGetLastError(), "gather_copy_kernel launch");
+}
+
+
+int mdsx_ndarray_meta(const uint8_t* values, const int64_t* offsets, uint64_t rows, int dtype_id,
+                      uint8_t* out_dtype, uint8_t* out_ndim, int64_t* out_data_offset,
+                      int64_t* out_numel, uint8_t* out_bad, int32_t* d_max_ndim, void* stream) {
+  if (!offsets || (rows && (!values || !out_dtype || !out_ndim || !out_data_offset ||
+                            !out_numel || !out_bad)))
+    return mdsx::fail(MDSX_E_ARG, "mdsx_ndarray_meta: bad argument");
+  if (dtype_id != 0 && !(dtype_id == 8 || dtype_id == 9 || dtype_id == 16 || dtype_id == 17 ||
+                         dtype_id == 18 || dtype_id == 32 || dtype_id == 33 || dtype_id == 34 ||
+                         dtype_id == 64 || dtype_id == 65 || dtype_id == 66))
+    return mdsx::fail(MDSX_E_ENCODING, "mdsx_ndarray_meta: unknown dtype id");
+  if (rows == 0) return MDSX_OK;
+  const unsigned grid = unsigned((rows + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL((ndarray_meta_kernel<false>), dim3(grid), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), values, offsets, rows, dtype_id, out_dtype,
+                     out_ndim, out_data_offset, out_numel, out_bad, d_max_ndim, 0, nullptr);
+  return hip_check(hipGetLastError(), "ndarray_meta_kernel launch");
+}
+
+int mdsx_ndarray_shapes(const uint8_t* values, const int64_t* offsets, uint64_t rows,
+                        int dtype_id, int32_t shape_cols, int64_t* out_shape, void* stream) {
+  if (!offsets || shape_cols < 0 || (rows && shape_cols && (!values || !out_shape)))
+    return mdsx::fail(MDSX_E_ARG, "mdsx_ndarray_shapes: bad argument");
+  if (rows == 0 || shape_cols == 0) return MDSX_OK;
+  const unsigned grid = unsigned((rows + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL((ndarray_meta_kernel<true>), dim3(grid), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), values, offsets, rows, dtype_id, nullptr,
+                     nullptr, nullptr, nullptr, nullptr, nullptr, shape_cols, out_shape);
+  return hip_check(hipGetLastError(), "ndarray_meta_kernel launch");
 }
 
 int mdsx_copy_probe(const void* d_src, void* d_dst, uint64_t bytes, void* stream) {

@@ -34,7 +34,7 @@ from streaming_amd.encodings import EncodingInfo, parse_encoding
 
 __all__ = [
     'Plan', 'DeviceBatch', 'RaggedColumn', 'DecodedBatch', 'BatchDecoder', 'decode_batch',
-    'make_batch', 'stage_shards', 'torch_dtype', 'output_bytes'
+    'make_batch', 'stage_shards', 'torch_dtype', 'output_bytes', 'NdarrayMeta', 'ndarray_meta'
 ]
 
 _TORCH_DTYPES = {
@@ -289,6 +289,61 @@ class RaggedColumn:
 
     def __len__(self) -> int:
         return int(self.offsets.numel()) - 1
+
+
+@dataclass
+class NdarrayMeta:
+    """Per-row header facts of a dynamic ndarray column, parsed on the device
+    (``mdsx_ndarray_meta`` / ``mdsx_ndarray_shapes``; NDArray.decode, encodings.py:270-305).
+
+    Row i's values are ``values[data_offset[i] : data_offset[i] + numel[i] * itemsize]`` of
+    dtype id ``dtype[i]`` (encodings.py:131-143) and shape ``shape[i, :ndim[i]]``; ``bad[i]`` is 1
+    where the reference's decode raises.
+    """
+    dtype: torch.Tensor          # uint8[rows]
+    ndim: torch.Tensor           # uint8[rows]
+    data_offset: torch.Tensor    # int64[rows]
+    numel: torch.Tensor          # int64[rows]
+    bad: torch.Tensor            # uint8[rows]
+    shape: torch.Tensor          # int64[rows, max_ndim] (padded with 1)
+
+    def row(self, col: 'RaggedColumn', i: int) -> torch.Tensor:
+        """Row i as a device tensor of its dtype and shape (a copy; values may be unaligned)."""
+        if int(self.bad[i]):
+            raise ValueError(f'row {i}: malformed ndarray')
+        from streaming_amd.encodings import VALUE_DTYPES
+        dt = torch_dtype(VALUE_DTYPES[int(self.dtype[i])])
+        n = int(self.numel[i])
+        item = torch.empty(0, dtype=dt).element_size()
+        o = int(self.data_offset[i])
+        shape = [int(d) for d in self.shape[i, :int(self.ndim[i])]]
+        return col.values[o:o + n * item].clone().view(dt).reshape(shape)
+
+
+def ndarray_meta(col: 'RaggedColumn', dtype_id: int = 0) -> NdarrayMeta:
+    """Parse the headers of a decoded dynamic ndarray column on the device. ``dtype_id`` is the
+    static value dtype id of ``ndarray:<dtype>`` columns, 0 for ``ndarray``."""
+    lib = _native.lib()
+    rows = len(col)
+    dev = col.offsets.device
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    u8 = dict(dtype=torch.uint8, device=dev)
+    i64 = dict(dtype=torch.int64, device=dev)
+    dtype, ndim, bad = (torch.empty(rows, **u8) for _ in range(3))
+    data_offset, numel = torch.empty(rows, **i64), torch.empty(rows, **i64)
+    max_ndim = torch.zeros(1, dtype=torch.int32, device=dev)
+    vals = col.values.data_ptr() if col.values.numel() else None
+    _check(
+        lib.mdsx_ndarray_meta(vals, col.offsets.data_ptr(), rows, dtype_id, dtype.data_ptr(),
+                              ndim.data_ptr(), data_offset.data_ptr(), numel.data_ptr(),
+                              bad.data_ptr(), max_ndim.data_ptr(), stream), 'mdsx_ndarray_meta')
+    width = int(max_ndim.item())  # sizes the shape table (host sync)
+    shape = torch.ones((rows, width), **i64)
+    _check(
+        lib.mdsx_ndarray_shapes(vals, col.offsets.data_ptr(), rows, dtype_id, width,
+                                shape.data_ptr() if shape.numel() else None, stream),
+        'mdsx_ndarray_shapes')
+    return NdarrayMeta(dtype, ndim, data_offset, numel, bad, shape)
 
 
 @dataclass
