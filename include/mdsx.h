@@ -200,6 +200,36 @@ int mdsx_ndarray_meta(const uint8_t* values, const int64_t* offsets, uint64_t ro
 int mdsx_ndarray_shapes(const uint8_t* values, const int64_t* offsets, uint64_t rows,
                         int dtype_id, int32_t shape_cols, int64_t* out_shape, void* stream);
 
+/* ---- shard encode (MDSWriter on the device) ----------------------------------------------------
+ * The reverse of the decode: columns in the decoder's output layout -> MDS shard files,
+ * byte-identical to the reference writer's. Replaces MDSWriter.encode_sample +
+ * encode_joint_shard (streaming/base/format/mds/writer.py:92-144) for whole batches; the shard
+ * split of Writer.write (streaming/base/format/base/writer.py:248-269) is decided by the caller
+ * from the cumulative sample sizes (a greedy prefix rule, O(shards) binary searches). */
+typedef struct mdsx_column_in {
+  const void* data;        /* fixed: rows x row_bytes (row-major); variable: packed values */
+  const int64_t* offsets;  /* variable: rows + 1 offsets into data (offsets[0] may be > 0);
+                              fixed: NULL */
+  uint64_t bytes;          /* size of data: bounds the variable offsets / fixed rows */
+  uint64_t reserved;
+} mdsx_column_in;
+
+/* Workspace of the encode calls (status record at offset 0). */
+uint64_t mdsx_encode_workspace_bytes(void);
+/* d_cum (device int64[rows + 1]): cum[i] = bytes of samples 0..i-1 (heads included, the 4-byte
+ * offsets-table entry not). Checks every variable column (monotone offsets inside [0, bytes],
+ * lengths < 2^32: the u32 head) into the status record, which this call resets. */
+int mdsx_encode_sizes(const mdsx_plan* plan, const mdsx_column_in* cols, uint64_t rows,
+                      int64_t* d_cum, void* d_workspace, uint64_t workspace_bytes, void* stream);
+/* Write every shard of `batch` (laid out as for decoding: shard s holds rows
+ * [row0, row0 + samples) and must be exactly 4 + 4 (samples + 1) + config_bytes +
+ * cum[row0 + samples] - cum[row0] bytes) into batch->data, which this call writes. d_config:
+ * the shard config JSON (device). Does nothing if the status record already holds an error;
+ * inconsistent descriptors are reported as MDSX_E_HEADER, never written through. */
+int mdsx_encode_shards(const mdsx_plan* plan, const mdsx_batch* batch, const mdsx_column_in* cols,
+                       const int64_t* d_cum, const uint8_t* d_config, uint32_t config_bytes,
+                       void* d_workspace, uint64_t workspace_bytes, void* stream);
+
 /* ---- diagnostics ---------------------------------------------------------------------------
  * HBM roofline probe: a streaming 16-byte-per-lane device-to-device copy of `bytes` (multiple of
  * 16, 16-byte aligned pointers) on `stream`. Not part of the decode path: it measures what a

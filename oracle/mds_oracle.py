@@ -13,6 +13,11 @@ Restated from (paths relative to the mosaicml/streaming repository):
   (u32 size head of the variable columns, then one slice per column)
 * ``mds_decode``                       <- ``streaming/base/format/mds/encodings.py:760-773``
   with the per-encoding decoders of ``encodings.py:62-397`` (Bytes, Str, Int, NDArray, scalars)
+* ``writer_split``                     <- ``Writer.write`` (``streaming/base/format/base/
+  writer.py:248-269``): flush when ``size_limit < shard_size + sample + 4``, per sample
+* ``encode_sample_from_columns`` / ``encode_joint_shard`` <- ``MDSWriter.encode_sample`` /
+  ``encode_joint_shard`` (``streaming/base/format/mds/writer.py:92-117,133-144``) over columns in
+  the device format (the checker of the device encoder)
 * ``decode_shard_columns``             <- the reader applied to every sample of a shard, written
   in the device decoder's output format (fixed columns as row bytes, ragged columns as packed
   values + int64 offsets + a UTF-8 validity flag per row for ``str``)
@@ -33,7 +38,8 @@ import numpy as np
 
 __all__ = [
     'OracleMDSReader', 'mds_decode', 'decode_shard_columns', 'decode_fixed_shard_vectorized',
-    'column_digests', 'utf8_is_valid', 'load_index'
+    'column_digests', 'utf8_is_valid', 'load_index', 'writer_split', 'encode_sample_from_columns',
+    'encode_joint_shard'
 ]
 
 _VALUE_DTYPES = {
@@ -218,3 +224,43 @@ def column_digests(columns: dict[str, Any]) -> dict[str, dict[str, str]]:
                 d['flags'] = hashlib.sha256(np.ascontiguousarray(col[3]).tobytes()).hexdigest()
             out[name] = d
     return out
+
+
+def writer_split(sample_sizes, size_limit: Optional[int], extra_per_shard: int,
+                 extra_per_sample: int = 4) -> list[int]:
+    """Samples per shard, one sample at a time as ``Writer.write`` does
+    (base/writer.py:248-269, ``_reset_cache`` :147-152, ``finish`` :289-314)."""
+    shards, count, cur = [], 0, extra_per_shard
+    for size in sample_sizes:
+        new = int(size) + extra_per_sample
+        if size_limit and size_limit < cur + new:
+            shards.append(count)  # flush_shard, even with nothing cached
+            count, cur = 0, extra_per_shard
+        count += 1
+        cur += new
+    if count:
+        shards.append(count)
+    return shards
+
+
+def encode_sample_from_columns(columns: list, row: int) -> bytes:
+    """``encode_sample`` (mds/writer.py:92-117) of row ``row``: ``columns`` in column order,
+    each ``('fixed', uint8[rows, size])`` or ``('var', values uint8, offsets int64)``."""
+    heads, body = [], []
+    for col in columns:
+        if col[0] == 'fixed':
+            body.append(col[1][row].tobytes())
+        else:
+            v = col[1][int(col[2][row]):int(col[2][row + 1])].tobytes()
+            heads.append(len(v))
+            body.append(v)
+    return np.array(heads, np.uint32).tobytes() + b''.join(body)
+
+
+def encode_joint_shard(config: bytes, samples: list) -> bytes:
+    """``encode_joint_shard`` (mds/writer.py:133-144)."""
+    n = np.uint32(len(samples))
+    sizes = list(map(len, samples))
+    offsets = np.array([0] + sizes).cumsum().astype(np.uint32)
+    offsets += len(n.tobytes()) + len(offsets.tobytes()) + len(config)
+    return n.tobytes() + offsets.tobytes() + config + b''.join(samples)

@@ -61,6 +61,9 @@ EXPORTED_SYMBOLS = (
     'mdsx_gather_ragged_copy',
     'mdsx_ndarray_meta',
     'mdsx_ndarray_shapes',
+    'mdsx_encode_workspace_bytes',
+    'mdsx_encode_sizes',
+    'mdsx_encode_shards',
 )
 
 
@@ -78,6 +81,12 @@ class ColumnOut(ctypes.Structure):
     """``mdsx_column_out``."""
     _fields_ = [('data', ctypes.c_void_p), ('offsets', ctypes.c_void_p), ('flags', ctypes.c_void_p),
                 ('capacity', ctypes.c_uint64)]
+
+
+class ColumnIn(ctypes.Structure):
+    """``mdsx_column_in``."""
+    _fields_ = [('data', ctypes.c_void_p), ('offsets', ctypes.c_void_p), ('bytes', ctypes.c_uint64),
+                ('reserved', ctypes.c_uint64)]
 
 
 class Batch(ctypes.Structure):
@@ -143,6 +152,14 @@ def _declare(handle: ctypes.CDLL) -> None:
     handle.mdsx_ndarray_meta.argtypes = [vp, vp, c_u64, c_int, vp, vp, vp, vp, vp, vp, vp]
     handle.mdsx_ndarray_shapes.restype = c_int
     handle.mdsx_ndarray_shapes.argtypes = [vp, vp, c_u64, c_int, ctypes.c_int32, vp, vp]
+    handle.mdsx_encode_workspace_bytes.restype = c_u64
+    handle.mdsx_encode_workspace_bytes.argtypes = []
+    handle.mdsx_encode_sizes.restype = c_int
+    handle.mdsx_encode_sizes.argtypes = [vp, ctypes.POINTER(ColumnIn), c_u64, vp, vp, c_u64, vp]
+    handle.mdsx_encode_shards.restype = c_int
+    handle.mdsx_encode_shards.argtypes = [
+        vp, ctypes.POINTER(Batch), ctypes.POINTER(ColumnIn), vp, vp, ctypes.c_uint32, vp, c_u64, vp
+    ]
     handle.mdsx_gather_workspace_bytes.restype = c_u64
     handle.mdsx_gather_workspace_bytes.argtypes = [c_u64]
     handle.mdsx_gather_fixed.restype = c_int

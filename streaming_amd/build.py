@@ -12,7 +12,11 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SOURCES = [os.path.join(HERE, 'csrc', 'mdsx_kernels.hip'), os.path.join(HERE, 'csrc', 'mdsx_plan.cpp')]
+SOURCES = [
+    os.path.join(HERE, 'csrc', name)
+    for name in ('mdsx_kernels.hip', 'mdsx_encode.hip', 'mdsx_plan.cpp')
+]
+HEADERS = [os.path.join(HERE, 'csrc', name) for name in ('mdsx_internal.h', 'mdsx_device.h')]
 OUTPUT = os.path.join(HERE, 'lib', 'libmdsx.so')
 ARCH = os.environ.get('MDSX_OFFLOAD_ARCH', 'gfx950')
 
@@ -34,8 +38,8 @@ def command(output: str = OUTPUT, extra: tuple = ()) -> list[str]:
 def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(os.path.dirname(OUTPUT), exist_ok=True)
     if not force and os.path.exists(OUTPUT):
-        newest = max(os.path.getmtime(p) for p in SOURCES + [
-            os.path.join(HERE, 'csrc', 'mdsx_internal.h'), os.path.join(ROOT, 'include', 'mdsx.h')
+        newest = max(os.path.getmtime(p) for p in SOURCES + HEADERS + [
+            os.path.join(ROOT, 'include', 'mdsx.h')
         ])
         if os.path.getmtime(OUTPUT) >= newest:
             return OUTPUT

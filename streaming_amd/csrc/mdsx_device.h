@@ -1,0 +1,292 @@
+// Device helpers shared by the decode, gather and encode kernels of libmdsx.so (gfx950, wave64):
+// 16-byte (non-temporal) loads/stores, byte realignment (v_alignbyte funnels over neighbour-lane
+// chunks), the strict UTF-8 SWAR check, and the wave-wide realigning row copy.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "mdsx_internal.h"
+
+namespace mdsx_kernels {
+
+int hip_check(hipError_t e, const char* what);
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// 16-byte global load / store, optionally non-temporal (streamed once: no reuse in L2/MALL).
+template <bool kNT>
+__device__ __forceinline__ uint4 ld16(const uint4* p) {
+  if constexpr (kNT) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  } else {
+    return *p;
+  }
+}
+
+template <bool kNT>
+__device__ __forceinline__ void st16(uint64_t addr, const uint4 v) {
+  if constexpr (kNT) {
+    const u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(addr));
+  } else {
+    *reinterpret_cast<uint4*>(addr) = v;
+  }
+}
+
+__device__ __forceinline__ uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t r) {
+  return __builtin_amdgcn_alignbyte(hi, lo, r);
+}
+
+__device__ __forceinline__ void report(mdsx_status* st, int code, int shard, int row, int col) {
+  if (atomicCAS(&st->code, 0, code) == 0) {
+    st->shard = shard;
+    st->row = row;
+    st->column = col;
+  }
+}
+
+// u32 at any byte address (reads the two aligned dwords that cover it).
+__device__ __forceinline__ uint32_t load_u32_any(const uint8_t* p) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uint64_t(3));
+  return alignbyte(q[1], q[0], uint32_t(a & 3));
+}
+
+// ---------------------------------------------------------------------------------------------
+// Realignment: bytes [sh, sh + 16) of the 32-byte pair (lo, hi). sh is wave-uniform.
+__device__ __forceinline__ uint4 funnel16(const uint4 lo, const uint4 hi, uint32_t sh) {
+  const uint32_t r = sh & 3;
+  switch (sh >> 2) {
+    case 0:
+      return make_uint4(alignbyte(lo.y, lo.x, r), alignbyte(lo.z, lo.y, r),
+                        alignbyte(lo.w, lo.z, r), alignbyte(hi.x, lo.w, r));
+    case 1:
+      return make_uint4(alignbyte(lo.z, lo.y, r), alignbyte(lo.w, lo.z, r),
+                        alignbyte(hi.x, lo.w, r), alignbyte(hi.y, hi.x, r));
+    case 2:
+      return make_uint4(alignbyte(lo.w, lo.z, r), alignbyte(hi.x, lo.w, r),
+                        alignbyte(hi.y, hi.x, r), alignbyte(hi.z, hi.y, r));
+    default:
+      return make_uint4(alignbyte(hi.x, lo.w, r), alignbyte(hi.y, hi.x, r),
+                        alignbyte(hi.z, hi.y, r), alignbyte(hi.w, hi.z, r));
+  }
+}
+
+// The same with a per-lane shift (selects instead of a uniform branch).
+__device__ __forceinline__ uint4 funnel16_lane(const uint4 lo, const uint4 hi, uint32_t sh) {
+  const uint32_t q = sh >> 2, r = sh & 3;
+  const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  uint32_t s[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k)
+    s[k] = q == 0 ? w[k] : q == 1 ? w[k + 1] : q == 2 ? w[k + 2] : w[k + 3];
+  return make_uint4(alignbyte(s[1], s[0], r), alignbyte(s[2], s[1], r), alignbyte(s[3], s[2], r),
+                    alignbyte(s[4], s[3], r));
+}
+
+__device__ __forceinline__ uint32_t byte_of(const uint4& v, int j) {
+  const uint32_t w = (j < 4) ? v.x : (j < 8) ? v.y : (j < 12) ? v.z : v.w;
+  return (w >> (8 * (j & 3))) & 0xffu;
+}
+
+__device__ __forceinline__ uint4 shfl_down1(const uint4 v) {
+  return make_uint4(__shfl_down(v.x, 1), __shfl_down(v.y, 1), __shfl_down(v.z, 1),
+                    __shfl_down(v.w, 1));
+}
+
+__device__ __forceinline__ uint4 readlane0(const uint4 v) {
+  return make_uint4(__builtin_amdgcn_readlane(v.x, 0), __builtin_amdgcn_readlane(v.y, 0),
+                    __builtin_amdgcn_readlane(v.z, 0), __builtin_amdgcn_readlane(v.w, 0));
+}
+
+// Byte mask of bytes [a, b) of a 16-byte chunk (0 <= a <= b <= 16).
+__device__ __forceinline__ uint4 byte_mask(uint32_t a, uint32_t b) {
+  uint32_t m[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int lo = min(max(int(a) - 4 * j, 0), 4), hi = min(max(int(b) - 4 * j, 0), 4);
+    const uint64_t mh = (uint64_t(1) << (8 * hi)) - 1, ml = (uint64_t(1) << (8 * lo)) - 1;
+    m[j] = uint32_t(mh & ~ml);
+  }
+  return make_uint4(m[0], m[1], m[2], m[3]);
+}
+
+// ---- strict UTF-8 well-formedness, 4 bytes per dword op (SWAR) ------------------------------
+// What bytes.decode('utf-8') accepts (encodings.py:80-81; Unicode Table 3-7): every byte is
+// checked against its 3 predecessors. Per-byte predicates are bit 7 of each byte lane.
+__device__ __forceinline__ uint32_t hi_c0(uint32_t y) { return y & (y << 1) & 0x80808080u; }
+__device__ __forceinline__ uint32_t hi_e0(uint32_t y) {
+  return y & (y << 1) & (y << 2) & 0x80808080u;
+}
+__device__ __forceinline__ uint32_t hi_f0(uint32_t y) {
+  return y & (y << 1) & (y << 2) & (y << 3) & 0x80808080u;
+}
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t v) {  // bit 7 set where the byte is 0
+  return ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v) & 0x80808080u;
+}
+
+// Error bits of dword x given the dword before it (p): lone / missing continuation bytes,
+// C0, C1, F5..FF, overlong E0/F0 forms, surrogates (ED A0..BF), code points > U+10FFFF.
+__device__ __forceinline__ uint32_t utf8_dword_err(uint32_t x, uint32_t p) {
+  const uint32_t p1 = alignbyte(x, p, 3), p2 = alignbyte(x, p, 2), p3 = alignbyte(x, p, 1);
+  const uint32_t cont = x & ~(x << 1) & 0x80808080u;
+  const uint32_t need = hi_c0(p1) | hi_e0(p2) | hi_f0(p3);
+  uint32_t err = need ^ cont;
+  err |= zero_bytes((x & 0xFEFEFEFEu) ^ 0xC0C0C0C0u);              // C0, C1
+  err |= ((x & 0x7F7F7F7Fu) + 0x0B0B0B0Bu) & x & 0x80808080u;      // F5..FF
+  const uint32_t b5 = (x << 2) & 0x80808080u, b45 = ((x << 2) | (x << 3)) & 0x80808080u;
+  err |= zero_bytes(p1 ^ 0xE0E0E0E0u) & ~b5 & 0x80808080u;         // E0 followed by < A0
+  err |= zero_bytes(p1 ^ 0xEDEDEDEDu) & b5;                        // ED followed by > 9F
+  err |= zero_bytes(p1 ^ 0xF0F0F0F0u) & ~b45 & 0x80808080u;        // F0 followed by < 90
+  err |= zero_bytes(p1 ^ 0xF4F4F4F4u) & b45;                       // F4 followed by > 8F
+  return err;
+}
+
+// 16 segment bytes `v` (bytes outside the segment already zeroed) and the dword before them
+// (zero before the segment start). `last`: v holds the segment's last byte, so a sequence still
+// open at the end of v is truncated. Zero bytes never err except after an unfinished lead byte,
+// which is exactly the truncated-sequence case.
+__device__ __forceinline__ bool utf8_chunk_bad(const uint4 v, uint32_t pw, bool last) {
+  const bool ascii = ((v.x | v.y | v.z | v.w) & 0x80808080u) == 0;
+  if (ascii && hi_c0(pw) == 0) return false;  // no open sequence enters, none starts
+  uint32_t err = utf8_dword_err(v.x, pw) | utf8_dword_err(v.y, v.x) | utf8_dword_err(v.z, v.y) |
+                 utf8_dword_err(v.w, v.z);
+  if (last) err |= utf8_dword_err(0u, v.w);  // positions 16..18 after the segment end
+  return err != 0;
+}
+
+// Bytes of a 16-byte chunk at address D that lie in [lo, hi), others zeroed.
+__device__ __forceinline__ uint4 keep_range(const uint4 v, uint64_t D, uint64_t lo, uint64_t hi) {
+  const int64_t a = max(int64_t(lo) - int64_t(D), int64_t(0));
+  const int64_t b = min(int64_t(hi) - int64_t(D), int64_t(16));
+  if (a == 0 && b == 16) return v;
+  if (b <= a) return make_uint4(0, 0, 0, 0);
+  const uint4 m = byte_mask(uint32_t(a), uint32_t(b));
+  return make_uint4(v.x & m.x, v.y & m.y, v.z & m.z, v.w & m.w);
+}
+
+// Store the bytes of `chunk` (held by lane `le`, 16-byte aligned destination D) that fall in
+// [d0, dend): one byte per lane, lanes 0..15, in a single wave instruction.
+__device__ __forceinline__ void wave_edge_store(const uint4 chunk, int le, uint64_t D,
+                                                uint64_t d0, uint64_t dend, int lane) {
+  const uint32_t w0 = __builtin_amdgcn_readlane(chunk.x, le);
+  const uint32_t w1 = __builtin_amdgcn_readlane(chunk.y, le);
+  const uint32_t w2 = __builtin_amdgcn_readlane(chunk.z, le);
+  const uint32_t w3 = __builtin_amdgcn_readlane(chunk.w, le);
+  const uint64_t A = D + uint64_t(lane);
+  if (lane < 16 && A >= d0 && A < dend) {
+    const uint32_t w = lane < 4 ? w0 : lane < 8 ? w1 : lane < 12 ? w2 : w3;
+    *reinterpret_cast<uint8_t*>(A) = uint8_t(w >> (8 * (lane & 3)));
+  }
+}
+
+__device__ __forceinline__ bool chunk_touches(const uint4* c, const uint8_t* src, uint64_t len) {
+  const uint64_t a = reinterpret_cast<uint64_t>(c), s0 = reinterpret_cast<uint64_t>(src);
+  return a + 16 > s0 && a < s0 + len;
+}
+
+// One wave copies `len` bytes from src to dst (any alignment of either). Destination chunks are
+// 16-byte aligned; lane k of a step owns chunk k. Its source bytes straddle two aligned 16-byte
+// source chunks: it loads the first and takes the second from lane k+1 (lane 63 from lane 0 of
+// the next step, or one extra load at the end of a batch). The (at most two) partial chunks at
+// the ends are written one byte per lane. With kUtf8, returns whether the segment is not
+// well-formed UTF-8 (wave-uniform).
+//
+// kClamp: the source is not padded (a caller's tensor): aligned chunks that do not touch
+// [src, src + len) are not loaded (they could lie on an unmapped page), only zero-filled.
+template <bool kUtf8, int kUnroll, bool kNT, bool kEdges = true, bool kClamp = false>
+__device__ __forceinline__ bool wave_copy(const uint8_t* src, uint8_t* dst, uint64_t len,
+                                          int lane) {
+  if (len == 0) return false;
+  const uint64_t d0 = reinterpret_cast<uint64_t>(dst);
+  const uint64_t dend = d0 + len;
+  const uint64_t dbeg = d0 & ~uint64_t(15);
+  const uint64_t nchunks = (((dend + 15) & ~uint64_t(15)) - dbeg) >> 4;
+  const uint64_t sfirst = reinterpret_cast<uint64_t>(src) - (d0 - dbeg);
+  const uint32_t sh = uint32_t(sfirst & 15);
+  const uint4* sal = reinterpret_cast<const uint4*>(sfirst & ~uint64_t(15));
+  const uint64_t nload = nchunks + (sh ? 1 : 0);
+  const bool head_partial = dbeg < d0 || dbeg + 16 > dend;
+  const bool tail_partial = nchunks > 1 && (dend & 15) != 0;
+  bool bad = false;
+  uint32_t carry = 0;  // last dword of the previous chunk (UTF-8 look-back)
+  for (uint64_t base = 0; base < nchunks; base += 64 * kUnroll) {
+    uint4 lo[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const uint64_t k = base + uint64_t(u) * 64 + lane;
+      bool live = k < nload;
+      if (kClamp) live = live && chunk_touches(sal + k, src, len);
+      lo[u] = live ? ld16<kNT>(sal + k) : make_uint4(0, 0, 0, 0);
+    }
+    uint4 tail = make_uint4(0, 0, 0, 0);
+    if (sh != 0 && lane == 63) {
+      const uint64_t k = base + 64 * kUnroll;
+      if (k < nload && (!kClamp || chunk_touches(sal + k, src, len))) tail = ld16<kNT>(sal + k);
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const uint64_t k0 = base + uint64_t(u) * 64;
+      if (k0 >= nchunks) break;  // wave-uniform
+      const uint64_t k = k0 + lane;
+      uint4 out = lo[u];
+      if (sh != 0) {
+        uint4 hi = shfl_down1(lo[u]);
+        const uint4 nxt = (u + 1 < kUnroll) ? readlane0(lo[u + 1 < kUnroll ? u + 1 : u]) : tail;
+        if (lane == 63) hi = nxt;
+        out = funnel16(lo[u], hi, sh);
+      }
+      const uint64_t D = dbeg + 16 * k;
+      if (kUtf8) {
+        const uint4 vout = keep_range(out, D, d0, dend);
+        uint32_t pw = __shfl_up(vout.w, 1);
+        if (lane == 0) pw = carry;
+        carry = __shfl(vout.w, 63);
+        if (k < nchunks) bad |= utf8_chunk_bad(vout, pw, k == nchunks - 1);
+      }
+      if (k < nchunks && D >= d0 && D + 16 <= dend) st16<kNT>(D, out);
+      if (kEdges) {  // kEdges == false: the caller guarantees 16-byte aligned dst and length
+        if (k0 == 0 && head_partial) wave_edge_store(out, 0, dbeg, d0, dend, lane);
+        if (tail_partial && nchunks - 1 >= k0 && nchunks - 1 < k0 + 64)
+          wave_edge_store(out, int(nchunks - 1 - k0), dbeg + 16 * (nchunks - 1), d0, dend, lane);
+      }
+    }
+  }
+  if (kUtf8) return __any(bad);
+  return false;
+}
+
+// Fixed column of 1..16 bytes: one row per lane. dst is aligned to the largest power of two
+// dividing the row size (outputs are 256-byte aligned tensors).
+__device__ __forceinline__ void gather_small(const uint8_t* p, uint8_t* dst, uint32_t size) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uint64_t(3));
+  const uint32_t r = uint32_t(a & 3);
+  const uint32_t nd = (size + 6) >> 2;  // dwords covering r + size bytes for any r <= 3
+  const uint32_t w0 = q[0];
+  const uint32_t w1 = nd > 1 ? q[1] : 0u;
+  const uint32_t w2 = nd > 2 ? q[2] : 0u;
+  const uint32_t w3 = nd > 3 ? q[3] : 0u;
+  const uint32_t w4 = nd > 4 ? q[4] : 0u;
+  const uint4 o = make_uint4(alignbyte(w1, w0, r), alignbyte(w2, w1, r), alignbyte(w3, w2, r),
+                             alignbyte(w4, w3, r));
+  switch (size) {
+    case 1: *dst = uint8_t(o.x); break;
+    case 2: *reinterpret_cast<uint16_t*>(dst) = uint16_t(o.x); break;
+    case 4: *reinterpret_cast<uint32_t*>(dst) = o.x; break;
+    case 8: *reinterpret_cast<uint2*>(dst) = make_uint2(o.x, o.y); break;
+    case 12:
+      reinterpret_cast<uint32_t*>(dst)[0] = o.x;
+      reinterpret_cast<uint32_t*>(dst)[1] = o.y;
+      reinterpret_cast<uint32_t*>(dst)[2] = o.z;
+      break;
+    case 16: *reinterpret_cast<uint4*>(dst) = o; break;
+    default:
+      for (uint32_t j = 0; j < size; ++j) dst[j] = uint8_t(byte_of(o, int(j)));
+  }
+}
+
+}  // namespace mdsx_kernels

@@ -177,7 +177,7 @@ void apply_tuning(mdsx_plan* p) {
     std::string key = strip(kv.substr(0, eq));
     int64_t v = 0;
     if (!parse_py_int(kv.substr(eq + 1), &v)) continue;
-    if (key == "tile" && (v == 64 || v == 128 || v == 256)) {
+    if (key == "tile" && (v == 16 || v == 32 || v == 64 || v == 128 || v == 256)) {
       const int64_t per_row = 4 * int64_t(p->ncols) + 12 * int64_t(p->nvar);
       if (per_row * v <= 64 * 1024) p->tile_rows = int(v);
     } else if (key == "gmin" && v >= 0) {

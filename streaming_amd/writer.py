@@ -228,6 +228,7 @@ class MDSWriter:
     def _reset_cache(self) -> None:
         self.new_samples: list[bytes] = []
         self.new_shard_size = self.extra_bytes_per_shard
+        self._dev_pending: list = []  # open shard's rows from write_columns (device columns)
 
     def get_config(self) -> dict[str, Any]:
         return json.loads(self.config_data)
@@ -257,6 +258,8 @@ class MDSWriter:
     def write(self, sample: dict[str, Any]) -> None:
         """Cache a sample, flushing a shard first if it would pass size_limit
         (base/writer.py:248-269)."""
+        if self._dev_pending:
+            raise ValueError('write: rows from write_columns are pending in the open shard')
         new_sample = self.encode_sample(sample)
         new_size = len(new_sample) + self.extra_bytes_per_sample
         if self.size_limit and self.size_limit < self.new_shard_size + new_size:
@@ -264,6 +267,44 @@ class MDSWriter:
             self._reset_cache()
         self.new_samples.append(new_sample)
         self.new_shard_size += new_size
+
+    def write_columns(self, columns: dict[str, Any]) -> None:
+        """Write a batch of rows given as device columns, encoded on the GPU.
+
+        ``columns``: name -> fixed tensor ``[rows, ...]`` (the column's encoded bytes per row,
+        e.g. ``int32[rows]`` or ``float32[rows, 1024]``) or ``RaggedColumn`` (each row's encoded
+        bytes, ``mds_encode`` output). Produces the same shards as :meth:`write` called per row
+        (the split of ``Writer.write``, base/writer.py:248-269); the open shard's rows stay on
+        the device until more rows arrive or :meth:`finish`. See ``streaming_amd.encoder``.
+        """
+        from streaming_amd.encoder import concat_columns, encode_batch, slice_columns
+        from streaming_amd.reader import get_plan
+        if self.new_samples:
+            raise ValueError('write_columns: rows cached by write() are pending in the open shard')
+        plan = get_plan(self.column_names, self.column_encodings, self.column_sizes)
+        fresh = not self.shards and not self._dev_pending
+        cols = concat_columns(self._dev_pending + [columns])
+        enc, consumed = encode_batch(plan, cols, self.config_data, self.size_limit, fresh=fresh,
+                                     final=False)
+        self._write_encoded(enc)
+        first = next(iter(cols.values()))
+        rows = len(first) if not hasattr(first, 'shape') else int(first.shape[0])
+        self._dev_pending = [slice_columns(cols, consumed, rows)] if consumed < rows else []
+
+    def _flush_device(self) -> None:
+        from streaming_amd.encoder import concat_columns, encode_batch
+        from streaming_amd.reader import get_plan
+        plan = get_plan(self.column_names, self.column_encodings, self.column_sizes)
+        enc, _ = encode_batch(plan, concat_columns(self._dev_pending), self.config_data,
+                              self.size_limit, fresh=not self.shards, final=True)
+        self._dev_pending = []
+        self._write_encoded(enc)
+
+    def _write_encoded(self, enc: Any) -> None:
+        if enc is None:
+            return
+        for s, (b, e) in enumerate(enc.bounds):
+            self._write_shard_file(enc.shard_bytes(s), e - b)
 
     def write_encoded_shard(self, raw: bytes, samples: int) -> None:
         """Write an already-encoded shard file (e.g. from :func:`encode_fixed_shard`)."""
@@ -308,6 +349,8 @@ class MDSWriter:
 
     def finish(self) -> None:
         """Flush the last shard and write ``index.json`` (base/writer.py:289-314)."""
+        if self._dev_pending:
+            self._flush_device()
         if self.new_samples:
             self.flush_shard()
             self._reset_cache()
