@@ -107,6 +107,9 @@ int mdsx_plan_num_var(const mdsx_plan* plan);
 /* Rows per tile for this schema (64 by default). Tile t of shard s covers rows
  * [(t - tile0) * tile_rows, ...) of that shard; a shard has ceil(samples / tile_rows) tiles. */
 int mdsx_plan_tile_rows(const mdsx_plan* plan);
+/* Rows per tile of the encoder's batches (mdsx_encode_shards): its tile table is built with
+ * this, not with mdsx_plan_tile_rows. */
+int mdsx_plan_encode_tile_rows(const mdsx_plan* plan);
 /* kind (MDSX_KIND_*), bytes per row for FIXED (0 for var), element size in bytes (dtype size;
  * 1 for byte-like kinds). */
 int mdsx_plan_column(const mdsx_plan* plan, int col, int* kind, int64_t* row_bytes,

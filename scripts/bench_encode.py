@@ -18,7 +18,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from streaming_amd.decoder import Plan, decode_batch, stage_shards  # noqa: E402
+from streaming_amd.decoder import Plan, RaggedColumn, decode_batch, stage_shards  # noqa: E402
 from streaming_amd.encoder import BatchEncoder  # noqa: E402
 from streaming_amd.synth import fixed_b_batch_on_device, var_c_shards  # noqa: E402
 from streaming_amd.writer import shard_config_bytes  # noqa: E402
@@ -32,12 +32,15 @@ def main():
     ap.add_argument('--samples', type=int, default=1_000_000)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--tune', default=None, help='MDSX_TUNE knobs for the encode plan')
     args = ap.parse_args()
+    if args.tune:
+        os.environ['MDSX_TUNE'] = args.tune
     dev = torch.device('cuda', 0)
     if args.config == 'B':
         synth = fixed_b_batch_on_device(args.samples, seed=11)
-        plan = synth.plan
         names, encs, sizes = ['id', 'x'], ['int32', 'ndarray:float32:1024'], [4, 4096]
+        plan = Plan(names, encs, sizes)
         columns = {'id': synth.sources['id'], 'x': synth.sources['x']}
         ref = synth.batch
     else:
@@ -69,14 +72,15 @@ def main():
     if enc.status().code != 0:
         raise SystemExit('encode reported an error')
     ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
-    col_bytes = sum(
-        (v.values.numel() + v.offsets.numel() * 8) if hasattr(v, 'values') else
-        v.numel() * v.element_size() for v in columns.values())
+    col_bytes = sum((v.values.numel() + v.offsets.numel() * 8) if isinstance(v, RaggedColumn)
+                    else v.numel() * v.element_size() for v in columns.values())
     shard_bytes = sum(out.batch.sizes)
     gbs = (col_bytes + shard_bytes) / ms / 1e6
     print(json.dumps({
         'metric': 'device MDS encode (columns -> shard files), HBM-resident',
         'config': args.config,
+        'tune': args.tune,
+        'tile_rows': plan.tile_rows,
         'samples': args.samples,
         'shards': len(out),
         'ms': ms,

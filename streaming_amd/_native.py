@@ -61,6 +61,7 @@ EXPORTED_SYMBOLS = (
     'mdsx_gather_ragged_copy',
     'mdsx_ndarray_meta',
     'mdsx_ndarray_shapes',
+    'mdsx_plan_encode_tile_rows',
     'mdsx_encode_workspace_bytes',
     'mdsx_encode_sizes',
     'mdsx_encode_shards',
@@ -152,6 +153,8 @@ def _declare(handle: ctypes.CDLL) -> None:
     handle.mdsx_ndarray_meta.argtypes = [vp, vp, c_u64, c_int, vp, vp, vp, vp, vp, vp, vp]
     handle.mdsx_ndarray_shapes.restype = c_int
     handle.mdsx_ndarray_shapes.argtypes = [vp, vp, c_u64, c_int, ctypes.c_int32, vp, vp]
+    handle.mdsx_plan_encode_tile_rows.restype = c_int
+    handle.mdsx_plan_encode_tile_rows.argtypes = [vp]
     handle.mdsx_encode_workspace_bytes.restype = c_u64
     handle.mdsx_encode_workspace_bytes.argtypes = []
     handle.mdsx_encode_sizes.restype = c_int

@@ -234,7 +234,7 @@ bool fill_args(const mdsx_plan* plan, const mdsx_column_in* cols, uint64_t rows,
   a->rows = rows;
   a->ncols = plan->ncols;
   a->nvar = plan->nvar;
-  a->tile_rows = plan->tile_rows;
+  a->tile_rows = plan->encode_tile_rows;
   int64_t fixed = 0;
   for (int c = 0; c < plan->ncols; ++c) {
     const mdsx::ColumnSpec& spec = plan->cols[c];
@@ -311,7 +311,7 @@ int mdsx_encode_shards(const mdsx_plan* plan, const mdsx_batch* batch, const mds
                      s, a);
   int rc = hip_check(hipGetLastError(), "encode_headers_kernel launch");
   if (rc || batch->ntiles == 0) return rc;
-  const size_t lds = size_t(plan->ncols) * plan->tile_rows * sizeof(uint32_t);
+  const size_t lds = size_t(plan->ncols) * plan->encode_tile_rows * sizeof(uint32_t);
   if (plan->nontemporal)
     hipLaunchKernelGGL((encode_kernel<4, true>), dim3(batch->ntiles), dim3(kEncBlock), lds, s, a);
   else

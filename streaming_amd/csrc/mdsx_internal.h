@@ -36,6 +36,7 @@ struct mdsx_plan {
   int ncols = 0;
   int nvar = 0;
   int tile_rows = 256;
+  int encode_tile_rows = 16;  // rows per workgroup of the encode kernel
   int unroll = 4;       // 16-byte chunks per lane in flight in the row copy (4 or 6)
   int nontemporal = 0;  // non-temporal loads/stores in the row copy
   int gather_chunks = 2;  // 16-byte chunks per lane in the ragged gather (tile = 4 KiB x this)

@@ -177,9 +177,12 @@ void apply_tuning(mdsx_plan* p) {
     std::string key = strip(kv.substr(0, eq));
     int64_t v = 0;
     if (!parse_py_int(kv.substr(eq + 1), &v)) continue;
-    if (key == "tile" && (v == 16 || v == 32 || v == 64 || v == 128 || v == 256)) {
+    if (key == "tile" && (v == 4 || v == 8 || v == 16 || v == 32 || v == 64 || v == 128 || v == 256)) {
       const int64_t per_row = 4 * int64_t(p->ncols) + 12 * int64_t(p->nvar);
       if (per_row * v <= 64 * 1024) p->tile_rows = int(v);
+    } else if (key == "etile" && (v == 4 || v == 8 || v == 16 || v == 32 || v == 64 ||
+                                  v == 128 || v == 256)) {
+      if (4 * int64_t(p->ncols) * v <= 64 * 1024) p->encode_tile_rows = int(v);
     } else if (key == "gmin" && v >= 0) {
       p->gather_min = int(v);
     } else if (key == "unroll" && (v == 4 || v == 6)) {
@@ -254,11 +257,24 @@ int mdsx_plan_create(const char* const* encodings, const int64_t* column_sizes, 
         c.kind = MDSX_KIND_BYTES;
     }
   }
-  // 64-row tiles (one workgroup each): 16 rows per wave, a fine enough grain that the last
-  // wave of workgroups leaves little of the chip idle (measured: scripts/tune_decode.py). LDS per
+  // Tile = rows of one workgroup. All-fixed plans: about 32 KiB of rows per tile (>= 4 rows),
+  // so the resident workgroups stream through a narrow window of the shard buffer -- measured
+  // on config B (4 KiB rows): 4-8-row tiles 5.87 TB/s, 16: 5.66, 64: 5.52, and the plain copy
+  // probe 5.42 on the same box (scripts/tune_decode.py). Ragged plans: 64-row tiles, which keep
+  // the per-tile scan totals few (config C: 16 rows 3.69, 32: 3.86, 64: 3.84 TB/s). LDS per
   // tile: a u32 source offset per (row, column), and per ragged column a u32 length and a u64
-  // destination offset per row (<= 16.4 KiB at 64 columns).
-  p->tile_rows = 64;
+  // destination offset per row (<= 16.4 KiB at 64 columns and 64 rows).
+  if (p->nvar == 0) {
+    const int64_t per_row = p->fixed_sum > 0 ? p->fixed_sum : 1;
+    int tr = 4;
+    while (tr < 256 && int64_t(tr) * 2 * per_row <= 32 * 1024) tr *= 2;
+    p->tile_rows = tr;
+  } else {
+    p->tile_rows = 64;
+  }
+  // Encoder tiles: 16 rows (config B encode 5.06 TB/s vs 4.94 at 8 and 4.76 at 64; config C
+  // 4.12 vs 3.74 at 64).
+  p->encode_tile_rows = 16;
   p->nontemporal = 1;  // shard bytes are read once and outputs written once: stream them
   apply_tuning(p);
   *out = p;
@@ -272,6 +288,10 @@ int mdsx_plan_num_columns(const mdsx_plan* plan) { return plan ? plan->ncols : M
 int mdsx_plan_num_var(const mdsx_plan* plan) { return plan ? plan->nvar : MDSX_E_ARG; }
 
 int mdsx_plan_tile_rows(const mdsx_plan* plan) { return plan ? plan->tile_rows : MDSX_E_ARG; }
+
+int mdsx_plan_encode_tile_rows(const mdsx_plan* plan) {
+  return plan ? plan->encode_tile_rows : MDSX_E_ARG;
+}
 
 int mdsx_plan_column(const mdsx_plan* plan, int col, int* kind, int64_t* row_bytes,
                      int* elem_bytes) {

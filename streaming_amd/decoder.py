@@ -122,6 +122,7 @@ class Plan:
                 ColumnPlan(i, name, enc, info, kind.value, row_bytes.value, elem.value))
         self.num_var = self._lib.mdsx_plan_num_var(handle)
         self.tile_rows = self._lib.mdsx_plan_tile_rows(handle)
+        self.encode_tile_rows = self._lib.mdsx_plan_encode_tile_rows(handle)
         self.is_safe = bool(self._lib.mdsx_plan_is_safe(handle))
 
     @property

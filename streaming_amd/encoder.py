@@ -90,6 +90,20 @@ class EncodedBatch:
     def shard_bytes(self, s: int) -> bytes:
         return self.shard(s).cpu().numpy().tobytes()
 
+    def decode_batch(self, plan: Plan) -> DeviceBatch:
+        """The encoded shards as a decode batch of ``plan`` (same buffer, the tile table rebuilt
+        for the decoder's tile size)."""
+        b = self.batch
+        if b.tile_rows == plan.tile_rows:
+            return b
+        raw, tile_shard, row0, rows, tiles = _tables(b.sizes, b.samples, b.offsets,
+                                                     plan.tile_rows)
+        dev = b.device
+        return DeviceBatch(b.buffer, torch.from_numpy(raw).to(dev),
+                           torch.from_numpy(tile_shard).to(dev) if tiles else torch.zeros(
+                               1, dtype=torch.int32, device=dev), b.offsets, b.sizes, b.samples,
+                           row0, tiles, rows, plan.tile_rows)
+
 
 def _row_count(plan: Plan, columns: dict[str, Column]) -> int:
     counts = {len(v) if isinstance(v, RaggedColumn) else int(v.shape[0]) for v in columns.values()}
@@ -182,13 +196,14 @@ class BatchEncoder:
             raise ValueError('encode: a shard of 4 GiB or more cannot hold u32 offsets')
         samples = [e - b for b, e in bounds]
         offsets, total = _layout(sizes)
-        raw, tile_shard, row0, nrows, tiles = _tables(sizes, samples, offsets, plan.tile_rows)
+        raw, tile_shard, row0, nrows, tiles = _tables(sizes, samples, offsets,
+                                                      plan.encode_tile_rows)
         descs = torch.from_numpy(raw).to(dev)
         tiles_t = torch.from_numpy(tile_shard).to(dev) if tiles else torch.zeros(
             1, dtype=torch.int32, device=dev)
         self.batch = DeviceBatch(torch.empty(total, dtype=torch.uint8, device=dev), descs,
                                  tiles_t, offsets, sizes, samples, row0, tiles, nrows,
-                                 plan.tile_rows)
+                                 plan.encode_tile_rows)
         self._abi = self.batch.abi()
         self.config = config
         self.cfg = torch.frombuffer(bytearray(config), dtype=torch.uint8).to(dev) \

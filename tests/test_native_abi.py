@@ -49,7 +49,19 @@ def test_plan_for_every_golden_schema(name):
         if size:
             assert col.row_bytes == size
     assert plan.num_var == sum(1 for s in info['column_sizes'] if not s)
-    assert plan.tile_rows in (64, 128, 256)
+    if plan.num_var:
+        assert plan.tile_rows == 64
+    else:  # about 32 KiB of rows per decode tile, 4..256 rows
+        per_row = sum(info['column_sizes'])
+        assert plan.tile_rows in (4, 8, 16, 32, 64, 128, 256)
+        assert plan.tile_rows == 4 or plan.tile_rows * per_row <= 32 * 1024
+        assert plan.tile_rows == 256 or 2 * plan.tile_rows * per_row > 32 * 1024
+    assert plan.encode_tile_rows == 16
+
+
+def test_config_b_tiles():
+    plan = Plan(['id', 'x'], ['int32', 'ndarray:float32:1024'], [4, 4096])
+    assert plan.tile_rows == 4 and plan.encode_tile_rows == 16
 
 
 def test_plan_kinds():
