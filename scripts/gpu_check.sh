@@ -7,7 +7,7 @@ OUT=gpurun_out/${TAG:-run}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 python -c "import torch;print(torch.__version__, torch.cuda.get_device_name(0))" > "$OUT/env.txt" 2>&1 || exit 1
-timeout -k 10 900 python -m pytest tests -m gpu -x -q ${PYTEST_K:+-k "$PYTEST_K"} > "$OUT/pytest_gpu.log" 2>&1 || { tail -40 "$OUT/pytest_gpu.log"; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > "$OUT/pytest_gpu.log" 2>&1 || { tail -40 "$OUT/pytest_gpu.log"; exit 1; }
 tail -3 "$OUT/pytest_gpu.log"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { tail -30 "$OUT/smoke.log"; exit 1; }
 cat "$OUT/smoke.log"
