@@ -233,6 +233,36 @@ int mdsx_encode_shards(const mdsx_plan* plan, const mdsx_batch* batch, const mds
                        const int64_t* d_cum, const uint8_t* d_config, uint32_t config_bytes,
                        void* d_workspace, uint64_t workspace_bytes, void* stream);
 
+/* ---- shard-file hashing on the device ------------------------------------------
+ * The xxHash digests the reference records per shard file in index.json (Writer._write_file,
+ * streaming/base/format/base/writer.py:197-200, via get_hash, streaming/base/hashing.py:55-68)
+ * and recomputes over the whole file to validate it (Stream._decompress_shard_part /
+ * _prepare_shard_part, streaming/base/stream.py:333-340,403-411), computed over byte ranges
+ * already resident in device memory. Algorithm ids name python-xxhash 3.x functions (xxHash
+ * 0.8.2); `seed` is their `seed=` argument (the reference uses 0). hashlib algorithms stay on
+ * the host. */
+#define MDSX_HASH_XXH32 1
+#define MDSX_HASH_XXH64 2
+#define MDSX_HASH_XXH3_64 3
+#define MDSX_HASH_XXH3_128 4 /* also xxhash.xxh128 */
+
+typedef struct mdsx_segment {
+  uint64_t offset; /* byte offset inside `data` (multiple of 16)                                 */
+  uint64_t bytes;  /* length                                                                     */
+} mdsx_segment;
+
+/* Workspace for hashing `nseg` segments totalling `total_segment_bytes` (status record at 0). */
+uint64_t mdsx_hash_workspace_bytes(int nseg, uint64_t total_segment_bytes);
+/* Digest of every segment of `data` (device, 16-byte aligned) into d_digests (device
+ * uint64[2 * nseg]: the hash value's low 64 bits, then its high 64 bits -- 0 except for
+ * xxh3_128; xxh32 values are in the low 32 bits). d_segs: device table of nseg segments.
+ * A segment outside [0, data_bytes) or not 16-byte aligned is reported as MDSX_E_BOUNDS in the
+ * status record (and no digest is written); a workspace too small for the segments' 1 KiB
+ * blocks as MDSX_E_CAPACITY. */
+int mdsx_hash_segments(int algo, uint64_t seed, const uint8_t* data, uint64_t data_bytes,
+                       const mdsx_segment* d_segs, int nseg, uint64_t* d_digests,
+                       void* d_workspace, uint64_t workspace_bytes, void* stream);
+
 /* ---- diagnostics ---------------------------------------------------------------------------
  * HBM roofline probe: a streaming 16-byte-per-lane device-to-device copy of `bytes` (multiple of
  * 16, 16-byte aligned pointers) on `stream`. Not part of the decode path: it measures what a

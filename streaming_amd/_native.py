@@ -20,7 +20,8 @@ __all__ = [
     'NativeLibraryError', 'MDSX_OK', 'MDSX_E_ARG', 'MDSX_E_ENCODING', 'MDSX_E_HEADER',
     'MDSX_E_BOUNDS', 'MDSX_E_HIP', 'MDSX_E_CAPACITY', 'MDSX_E_EMPTY', 'KIND_FIXED', 'KIND_BYTES',
     'KIND_STR', 'KIND_NDARRAY', 'ShardDesc', 'ColumnOut', 'Batch', 'Status', 'lib', 'lib_path',
-    'EXPORTED_SYMBOLS', 'raise_for_code'
+    'EXPORTED_SYMBOLS', 'raise_for_code', 'Segment', 'HASH_XXH32', 'HASH_XXH64', 'HASH_XXH3_64',
+    'HASH_XXH3_128'
 ]
 
 MDSX_OK = 0
@@ -65,7 +66,14 @@ EXPORTED_SYMBOLS = (
     'mdsx_encode_workspace_bytes',
     'mdsx_encode_sizes',
     'mdsx_encode_shards',
+    'mdsx_hash_workspace_bytes',
+    'mdsx_hash_segments',
 )
+
+HASH_XXH32 = 1
+HASH_XXH64 = 2
+HASH_XXH3_64 = 3
+HASH_XXH3_128 = 4
 
 
 class NativeLibraryError(RuntimeError):
@@ -101,6 +109,11 @@ class Status(ctypes.Structure):
     """``mdsx_status``."""
     _fields_ = [('code', ctypes.c_int32), ('shard', ctypes.c_int32), ('row', ctypes.c_int32),
                 ('column', ctypes.c_int32)]
+
+
+class Segment(ctypes.Structure):
+    """``mdsx_segment``."""
+    _fields_ = [('offset', ctypes.c_uint64), ('bytes', ctypes.c_uint64)]
 
 
 assert ctypes.sizeof(ShardDesc) == 32
@@ -163,6 +176,10 @@ def _declare(handle: ctypes.CDLL) -> None:
     handle.mdsx_encode_shards.argtypes = [
         vp, ctypes.POINTER(Batch), ctypes.POINTER(ColumnIn), vp, vp, ctypes.c_uint32, vp, c_u64, vp
     ]
+    handle.mdsx_hash_workspace_bytes.restype = c_u64
+    handle.mdsx_hash_workspace_bytes.argtypes = [c_int, c_u64]
+    handle.mdsx_hash_segments.restype = c_int
+    handle.mdsx_hash_segments.argtypes = [c_int, c_u64, vp, c_u64, vp, c_int, vp, vp, c_u64, vp]
     handle.mdsx_gather_workspace_bytes.restype = c_u64
     handle.mdsx_gather_workspace_bytes.argtypes = [c_u64]
     handle.mdsx_gather_fixed.restype = c_int

@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SOURCES = [
     os.path.join(HERE, 'csrc', name)
-    for name in ('mdsx_kernels.hip', 'mdsx_encode.hip', 'mdsx_plan.cpp')
+    for name in ('mdsx_kernels.hip', 'mdsx_encode.hip', 'mdsx_hash.hip', 'mdsx_plan.cpp')
 ]
 HEADERS = [os.path.join(HERE, 'csrc', name) for name in ('mdsx_internal.h', 'mdsx_device.h')]
 OUTPUT = os.path.join(HERE, 'lib', 'libmdsx.so')
