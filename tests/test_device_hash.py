@@ -138,3 +138,18 @@ def test_bad_segments_raise():
     assert hashing.hash_device('xxh3_64', buf, []) == []
     # the hasher is reusable after an error
     assert hashing.hash_device('xxh3_64', buf, [(0, 4096)]) == [_xx('xxh3_64', bytes(4096))]
+
+
+@pytest.mark.parametrize('algo', ['xxh3_64', 'xxh128'])
+def test_uneven_large_segments_repeated(algo):
+    """Segments of very different lengths (uneven chain lengths and chunk counts), hashed
+    several times in a row on the same workspace: every call must see only its own block sums."""
+    rng = np.random.default_rng(9)
+    lens = [int(x) for x in rng.integers(1 << 10, 24 << 20, 24)] + [40 << 20, 300, 5000]
+    chunks = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in lens]
+    buf, segs = _pack(chunks)
+    want = [_xx(algo, c) for c in chunks]
+    for rep in range(3):
+        order = rng.permutation(len(segs))
+        got = hashing.hash_device(algo, buf, [segs[i] for i in order])
+        assert got == [want[i] for i in order], rep
