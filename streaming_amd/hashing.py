@@ -22,7 +22,7 @@ import torch
 from streaming_amd import _native
 
 __all__ = ['get_hashes', 'is_hash', 'get_hash', 'DEVICE_HASHES', 'is_device_hash', 'hash_device',
-           'hash_batch', 'validate_batch']
+           'hash_batch', 'validate_batch', 'DeviceHasher', 'hex_digests']
 
 
 def _collect() -> dict[str, Callable[[bytes], Any]]:
@@ -128,10 +128,13 @@ def _status_check(status: torch.Tensor) -> None:
         raise ValueError(f'mdsx_hash_segments reported error {st.code}')
 
 
-def _hex(algo: str, digests: np.ndarray) -> list[str]:
+def hex_digests(algo: str, digests: Any) -> list[str]:
+    """``get_hash``-format hex strings of device digests (int64 [n, 2] tensor or array)."""
+    if isinstance(digests, torch.Tensor):
+        digests = digests.cpu().numpy()
     width = DEVICE_HASHES[algo][1]
     out = []
-    for lo, hi in digests.view(np.uint64).reshape(-1, 2):
+    for lo, hi in np.ascontiguousarray(digests).view(np.uint64).reshape(-1, 2):
         value = (int(hi) << 64) | int(lo)
         out.append(f'{value:0{width}x}')
     return out
@@ -143,7 +146,7 @@ def hash_device(algo: str, data: torch.Tensor, segments: Sequence[tuple[int, int
     computed on the device. ``data``: contiguous uint8 device tensor; offsets multiples of 16."""
     digests, status = _hasher(data.device).launch(algo, data, segments, seed)
     _status_check(status)
-    return _hex(algo, digests.cpu().numpy())
+    return hex_digests(algo, digests)
 
 
 def hash_batch(batch: Any, algo: str, seed: int = 0) -> list[str]:

@@ -30,6 +30,8 @@ import torch
 from streaming_amd.compression import decompress, decompress_into, get_compression_extension
 from streaming_amd.decoder import (BatchDecoder, DecodedBatch, DeviceBatch, Plan, RaggedColumn,
                                    _layout, _tables)
+from streaming_amd.hashing import (DeviceHasher, _status_check, get_hash, hex_digests,
+                                   is_device_hash, is_hash)
 
 __all__ = ['ShardFile', 'ShardPipeline', 'shard_files_from_index', 'to_host']
 
@@ -41,6 +43,7 @@ class ShardFile:
     raw_bytes: int                 # decompressed size (index.json raw_data.bytes)
     samples: int
     compression: Optional[str] = None
+    hashes: Optional[dict] = None  # index.json raw_data.hashes (digests of the raw shard file)
 
 
 def shard_files_from_index(dirname: str, index: dict, split: Optional[str] = None,
@@ -50,17 +53,19 @@ def shard_files_from_index(dirname: str, index: dict, split: Optional[str] = Non
     for info in index['shards']:
         raw = os.path.join(dirname, split or '', info['raw_data']['basename'])
         z = info.get('zip_data')
+        hashes = info['raw_data'].get('hashes') or {}
         if (prefer_raw and os.path.exists(raw)) or not z:
-            out.append(ShardFile(raw, info['raw_data']['bytes'], info['samples']))
+            out.append(ShardFile(raw, info['raw_data']['bytes'], info['samples'], None, hashes))
         else:
             out.append(
                 ShardFile(os.path.join(dirname, split or '', z['basename']),
-                          info['raw_data']['bytes'], info['samples'], info['compression']))
+                          info['raw_data']['bytes'], info['samples'], info['compression'], hashes))
     return out
 
 
-def _fill(view: np.ndarray, shard: ShardFile) -> None:
-    """Read or decompress one shard into its slice of the pinned staging buffer."""
+def _fill(view: np.ndarray, shard: ShardFile, host_hash: Optional[str] = None) -> None:
+    """Read or decompress one shard into its slice of the pinned staging buffer (and check a
+    hashlib digest of the raw bytes on the host when asked)."""
     if shard.compression:
         with open(shard.path, 'rb') as f:
             data = f.read()
@@ -76,6 +81,8 @@ def _fill(view: np.ndarray, shard: ShardFile) -> None:
             n = f.readinto(memoryview(view))
     if n != shard.raw_bytes:
         raise ValueError(f'{shard.path}: expected {shard.raw_bytes} raw bytes, got {n}')
+    if host_hash and get_hash(host_hash, view[:n].tobytes()) != shard.hashes[host_hash]:
+        raise ValueError(f'Checksum failure: {shard.path}')
 
 
 class _Slot:
@@ -85,6 +92,7 @@ class _Slot:
         self.dev = torch.empty(total, dtype=torch.uint8, device=device)
         self.copied = torch.cuda.Event()
         self.decoded = torch.cuda.Event()
+        self.hasher = DeviceHasher(device)
         self.decoder: Optional[BatchDecoder] = None
         self.key: Optional[tuple] = None
 
@@ -99,6 +107,11 @@ class ShardPipeline:
         depth: staging/device slots in flight (2 = double buffering).
         workers: host threads reading / decompressing shards.
         device: CUDA device.
+        validate_hash: check every shard against its index.json ``raw_data.hashes[algo]``
+            before its batch is handed out, raising ``ValueError('Checksum failure: ...')`` like
+            ``Stream._prepare_shard_part`` (``stream.py:401-411``). xxHash algorithms run on the
+            device over the resident batch (``streaming_amd.hashing``); hashlib ones on the
+            host threads as the shards are read.
     """
 
     def __init__(self,
@@ -107,9 +120,21 @@ class ShardPipeline:
                  shards_per_batch: int = 8,
                  depth: int = 2,
                  workers: int = 8,
-                 device: Union[str, torch.device, None] = None) -> None:
+                 device: Union[str, torch.device, None] = None,
+                 validate_hash: Optional[str] = None) -> None:
         self.plan = plan
         self.shards = list(shards)
+        self.validate_hash = validate_hash
+        if validate_hash:
+            if not is_hash(validate_hash):
+                raise ValueError(f'{validate_hash} is not a supported hash algorithm.')
+            for s in self.shards:
+                if validate_hash not in (s.hashes or {}):
+                    raise ValueError(
+                        f'Hash algorithm `{validate_hash}` chosen for data ' +
+                        f'validation does not match with those provided during dataset ' +
+                        f'creation `{sorted((s.hashes or {}).keys())}`. Provide one of those.')
+        self._device_hash = bool(validate_hash) and is_device_hash(validate_hash)
         self.per = max(1, shards_per_batch)
         self.depth = max(1, depth)
         dev = torch.device(device or 'cuda')
@@ -127,8 +152,10 @@ class ShardPipeline:
         sizes = [s.raw_bytes for s in group]
         offsets, total = _layout(sizes)
         view = slot.host.numpy()
+        host_hash = self.validate_hash if self.validate_hash and not self._device_hash else None
         futs = [
-            self.pool.submit(_fill, view[o:o + s.raw_bytes], s) for o, s in zip(offsets, group)
+            self.pool.submit(_fill, view[o:o + s.raw_bytes], s, host_hash)
+            for o, s in zip(offsets, group)
         ]
         return futs, sizes, offsets, total
 
@@ -160,6 +187,10 @@ class ShardPipeline:
                 slot.copied.record(self.copy_stream)
             compute.wait_event(slot.copied)
             batch = self._batch(slot, group, sizes, offsets, total)
+            digests = None
+            if self._device_hash:
+                digests, hstatus = slot.hasher.launch(self.validate_hash, slot.dev[:total],
+                                                      list(zip(offsets, sizes)))
             key = (tuple(sizes), tuple(s.samples for s in group))
             if slot.decoder is None or slot.key != key:
                 slot.decoder = BatchDecoder(self.plan, batch)
@@ -171,6 +202,11 @@ class ShardPipeline:
                     slot.decoder._sized = False  # ragged totals differ per batch: re-size
             out = slot.decoder.run()
             slot.decoded.record(compute)
+            if digests is not None:
+                _status_check(hstatus)
+                for got, shard in zip(hex_digests(self.validate_hash, digests), group):
+                    if got != shard.hashes[self.validate_hash]:
+                        raise ValueError(f'Checksum failure: {shard.path}')
             nxt = gi + len(self.slots)
             if nxt < ngroups:
                 # the host buffer may be refilled once its H2D copy has completed

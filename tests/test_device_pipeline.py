@@ -95,3 +95,24 @@ def test_plugin_stream_get_item(name):
                 assert {c: gu.value_record(v) for c, v in s.items()} == rec
             k += 1
     assert k == len(expected)
+
+
+@pytest.mark.parametrize('algo', ['xxh64', 'sha1'])
+def test_pipeline_validate_hash(algo):
+    """validate_hash as Stream._prepare_shard_part (stream.py:401-411): xxh64 on the device over
+    the resident batch, sha1 on the host threads; the reference writer's digests pass, a wrong
+    one raises 'Checksum failure'."""
+    d = os.path.join(gu.GOLDEN, 'zstd')
+    idx = gu.index('zstd')
+    info = idx['shards'][0]
+    plan = Plan(info['column_names'], info['column_encodings'], info['column_sizes'])
+    files = shard_files_from_index(d, idx)
+    pipe = ShardPipeline(plan, files, shards_per_batch=1, workers=2, validate_hash=algo)
+    assert sum(b.rows for b in pipe) == sum(s['samples'] for s in idx['shards'])
+    pipe.close()
+    files[-1].hashes = dict(files[-1].hashes, **{algo: '00' * 8})
+    pipe = ShardPipeline(plan, files, shards_per_batch=1, workers=2, validate_hash=algo)
+    with pytest.raises(ValueError, match='Checksum failure'):
+        for _ in pipe:
+            pass
+    pipe.close()

@@ -2,6 +2,8 @@
 (a stub Stream base stands in for the reference's; no GPU calls)."""
 
 import os
+
+import pytest
 from types import SimpleNamespace
 
 from streaming_amd.plugin import make_device_stream, to_device_reader
@@ -53,3 +55,19 @@ def test_to_device_reader_idempotent():
     info = gu.index('kat')['shards'][0]
     r = to_device_reader(_ref_like_reader(info, os.path.join(gu.GOLDEN, 'kat')))
     assert to_device_reader(r) is r
+
+
+def test_pipeline_validate_hash_algorithm_checks():
+    """Unknown / unrecorded validate_hash algorithms raise the reference's ValueErrors before any
+    device work (stream.py:401-408, hashing.py:65-66)."""
+    from streaming_amd.decoder import Plan
+    from streaming_amd.pipeline import ShardPipeline, shard_files_from_index
+    d = os.path.join(gu.GOLDEN, 'zstd')
+    idx = gu.index('zstd')
+    info = idx['shards'][0]
+    plan = Plan(info['column_names'], info['column_encodings'], info['column_sizes'])
+    files = shard_files_from_index(d, idx)
+    with pytest.raises(ValueError, match='not a supported hash algorithm'):
+        ShardPipeline(plan, files, validate_hash='fake')
+    with pytest.raises(ValueError, match='does not match with those provided'):
+        ShardPipeline(plan, files, validate_hash='xxh3_64')
