@@ -38,6 +38,8 @@ def main():
     ap.add_argument('--rounds', type=int, default=5)
     ap.add_argument('--iters', type=int, default=10)
     ap.add_argument('--variants', nargs='+', default=['tile=256'])
+    ap.add_argument('--blob', default='3072,5120', help="config C 'b' byte-length range")
+    ap.add_argument('--chars', default='16,256', help="config C 's' code-point range")
     args = ap.parse_args()
     torch.cuda.set_device(0)
     if args.config == 'B':
@@ -47,7 +49,9 @@ def main():
         src = synth.sources
     else:
         from streaming_amd.decoder import stage_shards
-        shards, counts, src = var_c_shards(args.samples, seed=4)
+        blob = tuple(int(x) for x in args.blob.split(','))
+        chars = tuple(int(x) for x in args.chars.split(','))
+        shards, counts, src = var_c_shards(args.samples, seed=4, str_chars=chars, blob_bytes=blob)
         names = (['b', 'n', 's'], ['bytes', 'int', 'str'], [None, 8, None])
         base_batch = stage_shards(shards, counts, Plan(*names))
     decs = {}

@@ -259,6 +259,118 @@ __device__ __forceinline__ bool wave_copy(const uint8_t* src, uint8_t* dst, uint
   return false;
 }
 
+// Four rows per wave, one per 16-lane group (g = lane / 16, gl = lane % 16): the same copy as
+// wave_copy -- aligned 16-byte destination chunks, the source realigned from the chunk a lane
+// loads and its group neighbour's (gl + 1; gl 15 takes the next step's gl 0 or one extra load)
+// -- for medium rows (a few hundred bytes) that would leave most of a wave's 64 lanes idle. Each group has its own
+// src / dst / len (len 0: the group idles); the loop runs to the longest row of the wave.
+// Partial chunks at a row's ends are stored one byte per lane of the group. (str rows are
+// validated afterwards by group_utf8_bad: fused here the check costs the decode kernel a wave per
+// SIMD, 118 vs 89 VGPRs.)
+template <int kUnroll, bool kNT>
+__device__ __forceinline__ void group_copy(const uint8_t* src, uint8_t* dst, uint64_t len,
+                                           int lane) {
+  const int gl = lane & 15;
+  const uint64_t d0 = reinterpret_cast<uint64_t>(dst);
+  const uint64_t dend = d0 + len;
+  const uint64_t dbeg = d0 & ~uint64_t(15);
+  const uint64_t nchunks = len ? (((dend + 15) & ~uint64_t(15)) - dbeg) >> 4 : 0;
+  const uint64_t sfirst = reinterpret_cast<uint64_t>(src) - (d0 - dbeg);
+  const uint32_t sh = uint32_t(sfirst & 15);
+  const uint4* sal = reinterpret_cast<const uint4*>(sfirst & ~uint64_t(15));
+  const uint64_t nload = nchunks ? nchunks + (sh ? 1 : 0) : 0;  // an empty row loads nothing
+  const bool head_partial = nchunks > 0 && (dbeg < d0 || dbeg + 16 > dend);
+  const bool tail_partial = nchunks > 1 && (dend & 15) != 0;
+  uint64_t maxc = nchunks;  // wave-uniform trip count
+  maxc = max(maxc, uint64_t(__shfl_xor(static_cast<unsigned long long>(maxc), 16)));
+  maxc = max(maxc, uint64_t(__shfl_xor(static_cast<unsigned long long>(maxc), 32)));
+  for (uint64_t base = 0; base < maxc; base += 16 * kUnroll) {
+    uint4 lo[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const uint64_t k = base + uint64_t(u) * 16 + gl;
+      lo[u] = k < nload ? ld16<kNT>(sal + k) : make_uint4(0, 0, 0, 0);
+    }
+    uint4 tail = make_uint4(0, 0, 0, 0);
+    if (sh != 0 && gl == 15 && base + 16 * kUnroll < nload) tail = ld16<kNT>(sal + base + 16 * kUnroll);
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const uint64_t k0 = base + uint64_t(u) * 16;
+      if (k0 >= maxc) break;  // wave-uniform
+      const uint64_t k = k0 + gl;
+      uint4 hi = make_uint4(__shfl_down(lo[u].x, 1, 16), __shfl_down(lo[u].y, 1, 16),
+                            __shfl_down(lo[u].z, 1, 16), __shfl_down(lo[u].w, 1, 16));
+      const uint4 nx = u + 1 < kUnroll ? lo[u + 1 < kUnroll ? u + 1 : u] : tail;
+      const uint4 nxt = u + 1 < kUnroll
+                            ? make_uint4(__shfl(nx.x, 0, 16), __shfl(nx.y, 0, 16),
+                                         __shfl(nx.z, 0, 16), __shfl(nx.w, 0, 16))
+                            : tail;
+      if (gl == 15) hi = nxt;
+      const uint4 out = sh ? funnel16_lane(lo[u], hi, sh) : lo[u];
+      const uint64_t D = dbeg + 16 * k;
+      if (k < nchunks && D >= d0 && D + 16 <= dend) st16<kNT>(D, out);
+      // partial chunks at the row ends: the group's 16 lanes store one byte each
+      const bool head = head_partial && k0 == 0;
+      const bool tl = tail_partial && nchunks - 1 >= k0 && nchunks - 1 < k0 + 16;
+      if (__any(head || tl)) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const bool on = e == 0 ? head : tl;
+          const int le = e == 0 ? 0 : int((nchunks - 1 - k0) & 15);
+          const uint32_t w0 = __shfl(out.x, le, 16), w1 = __shfl(out.y, le, 16);
+          const uint32_t w2 = __shfl(out.z, le, 16), w3 = __shfl(out.w, le, 16);
+          const uint64_t E = e == 0 ? dbeg : dbeg + 16 * (nchunks - 1);
+          const uint64_t A = E + uint64_t(gl);
+          if (on && A >= d0 && A < dend) {
+            const uint32_t w = gl < 4 ? w0 : gl < 8 ? w1 : gl < 12 ? w2 : w3;
+            *reinterpret_cast<uint8_t*>(A) = uint8_t(w >> (8 * (gl & 3)));
+          }
+        }
+      }
+    }
+  }
+}
+
+// Strict UTF-8 check of four rows per wave already packed in `values` (one row per 16-lane
+// group): each lane reads aligned 16-byte chunks of its group's row [off, off + len), bytes
+// outside the row zeroed, the look-back dword passed along the group (zero before the row
+// start). Returns, per lane, whether its group's row is not well-formed UTF-8.
+template <int kUnroll>
+__device__ __forceinline__ bool group_utf8_bad(const uint8_t* values, uint64_t off, uint64_t len,
+                                               int lane) {
+  const int gl = lane & 15;
+  const uint64_t d0 = reinterpret_cast<uint64_t>(values) + off;
+  const uint64_t dend = d0 + len;
+  const uint64_t dbeg = d0 & ~uint64_t(15);
+  const uint64_t nchunks = len ? (((dend + 15) & ~uint64_t(15)) - dbeg) >> 4 : 0;
+  uint64_t maxc = nchunks;
+  maxc = max(maxc, uint64_t(__shfl_xor(static_cast<unsigned long long>(maxc), 16)));
+  maxc = max(maxc, uint64_t(__shfl_xor(static_cast<unsigned long long>(maxc), 32)));
+  bool bad = false;
+  uint32_t carry = 0;
+  for (uint64_t base = 0; base < maxc; base += 16 * kUnroll) {
+    uint4 v[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const uint64_t k = base + uint64_t(u) * 16 + gl;
+      v[u] = k < nchunks ? *reinterpret_cast<const uint4*>(dbeg + 16 * k) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const uint64_t k0 = base + uint64_t(u) * 16;
+      if (k0 >= maxc) break;  // wave-uniform
+      const uint64_t k = k0 + gl;
+      const uint4 vout = keep_range(v[u], dbeg + 16 * k, d0, dend);
+      uint32_t pw = __shfl_up(vout.w, 1, 16);
+      if (gl == 0) pw = carry;
+      carry = __shfl(vout.w, 15, 16);
+      if (k < nchunks) bad |= utf8_chunk_bad(vout, pw, k == nchunks - 1);
+    }
+  }
+  const uint64_t m = __ballot(bad);
+  return ((m >> (lane & 48)) & 0xffffull) != 0;
+}
+
 // Fixed column of 1..16 bytes: one row per lane. dst is aligned to the largest power of two
 // dividing the row size (outputs are 256-byte aligned tensors).
 __device__ __forceinline__ void gather_small(const uint8_t* p, uint8_t* dst, uint32_t size) {

@@ -41,6 +41,7 @@ struct mdsx_plan {
   int nontemporal = 0;  // non-temporal loads/stores in the row copy
   int gather_chunks = 2;  // 16-byte chunks per lane in the ragged gather (tile = 4 KiB x this)
   int gather_min = 256;   // ragged columns averaging fewer bytes per row use the gather kernel
+  int group_max = 1024;   // ... fewer than this (and >= gather_min): four rows per wave
   int64_t fixed_sum = 0;
   bool safe = true;
   mdsx::ColumnSpec cols[MDSX_MAX_COLUMNS];

@@ -12,11 +12,14 @@
 //                        shuffles + LDS), per-tile totals.                      (ragged plans only)
 //   scan_totals_kernel   one workgroup per ragged column: exclusive scan of the tile totals.
 //   decode_kernel        one workgroup per tile: per-row column boundaries into LDS; fixed columns
-//                        of <= 16 bytes gathered one row per lane; larger fixed columns copied one
-//                        row per wave with 16-byte aligned loads and stores, the source realigned in
-//                        registers (v_alignbyte funnel over the neighbour lane's chunk); for ragged
-//                        columns: final offsets, each row's source address and the row that starts
-//                        every 16 KiB output tile.
+//                        of <= 16 bytes gathered one row per lane; larger fixed columns and long
+//                        ragged rows copied one row per wave with 16-byte aligned loads and stores,
+//                        the source realigned in registers (v_alignbyte funnel over the neighbour
+//                        lane's chunk); medium ragged rows (a few hundred bytes) four per wave, one
+//                        per 16-lane group; then the tile's str rows are UTF-8 checked from the
+//                        L2-resident output, four rows per wave; for short-row ragged columns:
+//                        final offsets, each row's source address and the row that starts every
+//                        4 KiB output grain (for the gather kernel).
 //   gather_ragged_kernel one workgroup per 16 KiB tile of a ragged column's packed output
 //                        (destination-major): every lane writes whole aligned 16-byte chunks,
 //                        assembled from the row(s) that cover them (binary search over the tile's
@@ -41,6 +44,7 @@ constexpr int kBlock = 256;                     // 4 waves
 constexpr int kSmallMax = 16;                   // fixed columns <= 16 B: one row per lane
 constexpr uint64_t kMapGrain = uint64_t(kBlock) * 16;  // 4 KiB: row-map granule of ragged outputs
 constexpr int kGatherRows = 1024;               // rows of a gather tile staged in LDS
+constexpr int kGroupUnroll = 2;                 // chunks per lane in flight in group_copy
 
 struct DevCol {
   void* data;
@@ -51,7 +55,7 @@ struct DevCol {
   int8_t kind;
   int8_t var_index;
   int8_t gather;  // ragged column copied by gather_ragged_kernel (short rows) instead of waves
-  int8_t pad_;
+  int8_t group;   // ragged column of medium rows: four rows per wave (group_copy)
 };
 
 struct DevArgs {
@@ -71,7 +75,8 @@ struct DevArgs {
   int32_t ncols;
   int32_t nvar;
   int32_t tile_rows;
-  int32_t pad_;
+  int16_t any_group;     // some ragged column uses group_copy
+  int16_t any_wave_str;  // some str column is copied by decode_kernel (validated there)
   uint32_t gather_block0[MDSX_MAX_COLUMNS + 1];  // first gather workgroup of each ragged column
   DevCol cols[MDSX_MAX_COLUMNS];
 };
@@ -267,9 +272,9 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
         ok = false;
         continue;
       }
-      if (!col.gather) continue;
+      if (!col.gather && !col.group) continue;
       a.src_abs[uint64_t(vi) * a.rows + row] = v.d.offset + s_src[c * TR + t];
-      if (len) {
+      if (col.gather && len) {
         uint32_t* map = a.row_map + uint64_t(vi) * a.map_len;
         for (uint64_t g = (uint64_t(off) + kMapGrain - 1) / kMapGrain;
              g * kMapGrain < uint64_t(off) + len && g < a.map_len; ++g)
@@ -303,19 +308,59 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
         if (col.row_bytes <= uint32_t(kSmallMax)) continue;
         wave_copy<false, kUnroll, kNT, kEdges>(
             src, static_cast<uint8_t*>(col.data) + row * col.row_bytes, col.row_bytes, lane);
-      } else if (kRagged && !col.gather) {
+      } else if (kRagged && !col.gather && !col.group) {
         const int vi = col.var_index;
         uint8_t* dst = static_cast<uint8_t*>(col.data) + s_vdst[vi * TR + r];
         const uint64_t len = s_vlen[vi * TR + r];
-        if (col.kind == MDSX_KIND_STR) {
-          const bool bad = wave_copy<true, kUnroll, kNT>(src, dst, len, lane);
-          if (lane == 0 && col.flags && bad) col.flags[row] = 1;
-        } else {
-          wave_copy<false, kUnroll, kNT>(src, dst, len, lane);
+        // str rows: validated below, once the tile's rows are copied (the check fused into
+        // the copy loop costs the kernel a wave per SIMD: 125 vs 87 VGPRs)
+        wave_copy<false, kUnroll, kNT>(src, dst, len, lane);
+      }
+    }
+  }
+
+  // ---- medium-row ragged columns: four rows per wave, one per 16-lane group
+  if constexpr (kRagged) {
+    if (a.any_group) {  // launch-uniform
+      const int g = lane >> 4;
+      for (int r0 = wave * 4; r0 < int(v.nrows); r0 += kBlock / 16) {
+        const int r = min(r0 + g, int(v.nrows) - 1);
+        const bool live = r0 + g < int(v.nrows) && s_ok[r];
+        for (int c = 0; c < a.ncols; ++c) {
+          const DevCol& col = a.cols[c];
+          if (!col.group) continue;
+          const int vi = col.var_index;
+          group_copy<kGroupUnroll, kNT>(v.shard + s_src[c * TR + r],
+                                               static_cast<uint8_t*>(col.data) +
+                                                   s_vdst[vi * TR + r],
+                                               live ? s_vlen[vi * TR + r] : 0, lane);
         }
       }
     }
   }
+
+  // ---- strict UTF-8 of this tile's str rows (encodings.py:80-81), re-read from the packed
+  // output while it is L2-resident: four rows per wave, one per 16-lane group
+  if constexpr (kRagged) {
+    if (!a.any_wave_str) return;  // launch-uniform
+    __threadfence_block();
+    __syncthreads();
+    const int g = lane >> 4;
+    for (int r0 = wave * 4; r0 < int(v.nrows); r0 += kBlock / 16) {
+      const int r = min(r0 + g, int(v.nrows) - 1);
+      const bool live = r0 + g < int(v.nrows) && s_ok[r];
+      for (int c = 0; c < a.ncols; ++c) {
+        const DevCol& col = a.cols[c];
+        if (col.kind != MDSX_KIND_STR || !col.flags || col.gather) continue;
+        const int vi = col.var_index;
+        const uint64_t len = live ? s_vlen[vi * TR + r] : 0;
+        const bool bad = group_utf8_bad<2>(static_cast<const uint8_t*>(col.data),
+                                           s_vdst[vi * TR + r], len, lane);
+        if ((lane & 15) == 0 && len && bad) col.flags[v.d.row0 + v.r0 + r] = 1;
+      }
+    }
+  }
+
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -592,12 +637,20 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
     // Short ragged rows keep a wave's lanes busy only when copied destination-major.
     d.gather = s.kind != MDSX_KIND_FIXED && b->rows > 0 &&
                outs[c].capacity < uint64_t(plan->gather_min) * b->rows;
+    // Medium rows (a few hundred bytes): four per wave, one per 16-lane group (decided below).
+    d.group = s.kind != MDSX_KIND_FIXED && !d.gather && b->rows > 0 &&
+              outs[c].capacity < uint64_t(plan->group_max) * b->rows;
     if (s.kind == MDSX_KIND_FIXED) {
       if (!d.data) return mdsx::fail(MDSX_E_ARG, "mdsx: null data pointer for a fixed column");
     } else {
       if (!d.offsets || (!d.data && d.capacity > 0))
         return mdsx::fail(MDSX_E_ARG, "mdsx: null offsets/data for a ragged column");
     }
+  }
+  for (int c = 0; c < plan->ncols; ++c) {
+    const DevCol& d = a->cols[c];
+    if (d.group) a->any_group = 1;
+    if (d.kind == MDSX_KIND_STR && d.flags && !d.gather) a->any_wave_str = 1;
   }
   for (int v = 0; v < plan->nvar; ++v) {  // gather workgroups of each ragged column, in order
     a->gather_block0[v] = gblocks;
@@ -919,6 +972,7 @@ int mdsx_decode_shards(const mdsx_plan* plan, const mdsx_batch* batch,
     }                                                     \
   } while (0)
   if (plan->unroll == 6) MDSX_DECODE_U(6);
+  else if (plan->unroll == 2) MDSX_DECODE_U(2);
   else MDSX_DECODE_U(4);
 #undef MDSX_DECODE_U
 #undef MDSX_DECODE

@@ -185,7 +185,9 @@ void apply_tuning(mdsx_plan* p) {
       if (4 * int64_t(p->ncols) * v <= 64 * 1024) p->encode_tile_rows = int(v);
     } else if (key == "gmin" && v >= 0) {
       p->gather_min = int(v);
-    } else if (key == "unroll" && (v == 4 || v == 6)) {
+    } else if (key == "gmax" && v >= 0) {
+      p->group_max = int(v);
+    } else if (key == "unroll" && (v == 2 || v == 4 || v == 6)) {
       p->unroll = int(v);
     } else if (key == "gk" && (v == 1 || v == 2 || v == 4)) {
       p->gather_chunks = int(v);

@@ -1,0 +1,155 @@
+"""GPU parity of every ragged-column copy mode of the decoder, each forced through the
+measurement knobs (MDSX_TUNE, read at plan creation): destination-major gather kernel
+(short rows), four rows per wave in 16-lane groups (medium rows), one row per wave (long rows).
+Whatever mode a column gets, the bytes, offsets and UTF-8 flags must equal the reference's.
+"""
+
+import json
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import mds_oracle
+from streaming_amd import MDSWriter
+from streaming_amd.decoder import Plan, decode_batch, stage_shards
+from streaming_amd.synth import var_c_shards
+from tests import golden_util as gu
+from tests.test_device_decode import _device_digests
+
+pytestmark = pytest.mark.gpu
+
+MODES = {
+    'gather': 'gmin=1000000000',
+    'group': 'gmin=0,gmax=1000000000',
+    'wave': 'gmin=0,gmax=0',
+}
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _needs_gpu():
+    if not torch.cuda.is_available():
+        pytest.fail('GPU tests need an MI355X (torch.cuda.is_available() is False)')
+
+
+@pytest.fixture(params=sorted(MODES))
+def mode(request, monkeypatch):
+    monkeypatch.setenv('MDSX_TUNE', MODES[request.param])
+    return request.param
+
+
+def _plan(info):
+    return Plan(info['column_names'], info['column_encodings'], info['column_sizes'])
+
+
+@pytest.mark.parametrize('name', ['config_c_small', 'bad_utf8', 'config_a', 'dynamic', 'wide',
+                                  'images', 'kat'])
+def test_golden_sets(mode, name):
+    idx = gu.index(name)
+    plan = _plan(idx['shards'][0])
+    data = [gu.shard_bytes(name, s) for s in idx['shards']]
+    dec = decode_batch(plan, stage_shards(data, [s['samples'] for s in idx['shards']], plan))
+    assert _device_digests(plan, dec) == gu.manifest()[name]['columns']
+
+
+def test_alignment_sweep(mode):
+    """All 16 source alignments x lengths 0..300 and up to 5000, bytes and 2-byte UTF-8 rows,
+    in one shard per alignment; four rows of very different lengths share each wave."""
+    rng = np.random.default_rng(11)
+    for pad in range(16):
+        name = 'a' * (pad + 1)
+        cols = {name: 'bytes', 'z' + name: 'str'}
+        lens = list(range(0, 301)) + [int(x) for x in rng.integers(0, 5000, 60)]
+        rng.shuffle(lens)
+        rows = [{name: rng.bytes(n), 'z' + name: 'é' * (n % 97) + 'x' * (n % 3)} for n in lens]
+        with tempfile.TemporaryDirectory() as t:
+            with MDSWriter(columns=cols, out=t, size_limit=None) as w:
+                for r in rows:
+                    w.write(r)
+            info = json.load(open(os.path.join(t, 'index.json')))['shards'][0]
+            raw = open(os.path.join(t, info['raw_data']['basename']), 'rb').read()
+        p = _plan(info)
+        dec = decode_batch(p, stage_shards([raw], [info['samples']], p))
+        b, s = dec[name], dec['z' + name]
+        bv, bo = b.values.cpu().numpy(), b.offsets.cpu().numpy()
+        sv, so = s.values.cpu().numpy(), s.offsets.cpu().numpy()
+        for k, r in enumerate(rows):
+            assert bv[bo[k]:bo[k + 1]].tobytes() == r[name], (mode, pad, k)
+            assert sv[so[k]:so[k + 1]].tobytes().decode() == r['z' + name], (mode, pad, k)
+        assert int(s.flags.sum()) == 0
+
+
+def test_invalid_utf8_rows_between_valid_ones(mode):
+    """Bad sequences at every position of rows of 1..700 bytes: flags equal Python's decoder."""
+    rng = np.random.default_rng(3)
+    bad_bits = [b'\xc0\x80', b'\xed\xa0\x80', b'\xf4\x90\x80\x80', b'\xe2\x82', b'\x80', b'\xff']
+    rows, want = [], []
+    for k in range(1500):
+        n = int(rng.integers(1, 700))
+        body = bytearray(('ü' * n).encode()[:n])
+        if k % 3 == 0:
+            pos = int(rng.integers(0, n))
+            body[pos:pos] = bad_bits[k % len(bad_bits)]
+        data = bytes(body)
+        rows.append(data)
+        try:
+            data.decode('utf-8')
+            want.append(0)
+        except UnicodeDecodeError:
+            want.append(1)
+    # write the raw bytes as 'str' values through the bytes encoding path of the writer
+    with tempfile.TemporaryDirectory() as t:
+        with MDSWriter(columns={'s': 'bytes', 'k': 'int'}, out=t, size_limit=None) as w:
+            for k, r in enumerate(rows):
+                w.write({'s': r, 'k': k})
+        info = json.load(open(os.path.join(t, 'index.json')))['shards'][0]
+        raw = open(os.path.join(t, info['raw_data']['basename']), 'rb').read()
+    info = dict(info, column_encodings=['int', 'str'])  # columns are sorted: k, s
+    p = _plan(info)
+    dec = decode_batch(p, stage_shards([raw], [info['samples']], p))
+    s = dec['s']
+    v, o = s.values.cpu().numpy(), s.offsets.cpu().numpy()
+    for k, r in enumerate(rows):
+        assert v[o[k]:o[k + 1]].tobytes() == r
+    assert s.flags.cpu().numpy().tolist() == want
+
+
+def test_config_c_full_shards(mode):
+    shards, counts, src = var_c_shards(32_000, seed=8)
+    plan = Plan(['b', 'n', 's'], ['bytes', 'int', 'str'], [None, 8, None])
+    dec = decode_batch(plan, stage_shards(shards, counts, plan))
+    assert np.array_equal(dec['n'].cpu().numpy(), src['n'])
+    assert np.array_equal(dec['b'].values.cpu().numpy(), src['b_pool'])
+    assert np.array_equal(dec['s'].values.cpu().numpy(), src['s_pool'])
+    assert np.array_equal(dec['s'].offsets.cpu().numpy(),
+                          np.concatenate([[0], np.cumsum(src['s_len'])]))
+    assert int(dec['s'].flags.sum()) == 0
+
+
+def test_oracle_on_random_rows(mode, tmp_path):
+    rng = np.random.default_rng(17)
+    cols = {'a': 'bytes', 'b': 'str', 'c': 'int'}
+    with MDSWriter(columns=cols, out=str(tmp_path), size_limit=1 << 16) as w:
+        for _ in range(3000):
+            w.write({'a': rng.bytes(int(rng.choice([0, 3, 64, 255, 256, 257, 900, 2000]))),
+                     'b': 'abé中\U0001f600' * int(rng.integers(0, 60)),
+                     'c': int(rng.integers(-2**40, 2**40))})
+    idx = json.load(open(tmp_path / 'index.json'))
+    plan = _plan(idx['shards'][0])
+    data = [open(tmp_path / s['raw_data']['basename'], 'rb').read() for s in idx['shards']]
+    dec = decode_batch(plan, stage_shards(data, [s['samples'] for s in idx['shards']], plan))
+    base = {'a': 0, 'b': 0}
+    row = 0
+    for info in idx['shards']:
+        want = mds_oracle.decode_shard_columns(str(tmp_path), None, info)
+        n = info['samples']
+        for c in ('a', 'b'):
+            got = dec[c]
+            offs = got.offsets.cpu().numpy()[row:row + n + 1]
+            vals = got.values.cpu().numpy()[offs[0]:offs[-1]]
+            assert np.array_equal(offs - offs[0], want[c][2]), (mode, c)
+            assert np.array_equal(vals, want[c][1]), (mode, c)
+            base[c] += len(vals)
+        row += n
