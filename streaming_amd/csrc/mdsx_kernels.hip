@@ -179,24 +179,29 @@ __global__ __launch_bounds__(kBlock) void scan_tiles_kernel(const DevArgs a) {
 }
 
 // Pass 1b: exclusive scan of the tile totals of one ragged column (one workgroup per column).
+// Thread t owns the contiguous run [t * per, (t + 1) * per) of tiles: it sums its run, one block
+// scan of the 256 run sums gives every run its base, then each thread writes its run's prefixes
+// (one pass over the totals instead of ntiles / 256 dependent block scans).
 __global__ __launch_bounds__(kBlock) void scan_totals_kernel(const DevArgs a) {
   __shared__ int64_t s_wsum[kBlock / 64];
   const int vi = blockIdx.x;
   const int64_t* in = a.tile_total + uint64_t(vi) * a.ntiles;
   int64_t* out = a.tile_prefix + uint64_t(vi) * a.ntiles;
-  int64_t carry = 0;
-  for (uint32_t base = 0; base < a.ntiles; base += kBlock) {
-    const uint32_t k = base + threadIdx.x;
-    const int64_t x = k < a.ntiles ? in[k] : 0;
-    int64_t total;
-    const int64_t excl = block_exclusive_scan(x, s_wsum, &total);
-    if (k < a.ntiles) out[k] = carry + excl;
-    carry += total;
+  const uint32_t per = (a.ntiles + kBlock - 1) / kBlock;
+  const uint32_t lo = min(a.ntiles, threadIdx.x * per), hi = min(a.ntiles, lo + per);
+  int64_t run = 0;
+  for (uint32_t k = lo; k < hi; ++k) run += in[k];
+  int64_t total;
+  int64_t base = block_exclusive_scan(run, s_wsum, &total);
+  for (uint32_t k = lo; k < hi; ++k) {
+    const int64_t x = in[k];
+    out[k] = base;
+    base += x;
   }
   if (threadIdx.x == 0) {
-    if (a.totals) a.totals[vi] = carry;
+    if (a.totals) a.totals[vi] = total;
     for (int c = 0; c < a.ncols; ++c)
-      if (a.cols[c].var_index == vi) a.cols[c].offsets[a.rows] = carry;
+      if (a.cols[c].var_index == vi) a.cols[c].offsets[a.rows] = total;
   }
 }
 
