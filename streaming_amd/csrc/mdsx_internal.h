@@ -37,7 +37,8 @@ struct mdsx_plan {
   int nvar = 0;
   int tile_rows = 256;
   int encode_tile_rows = 16;  // rows per workgroup of the encode kernel
-  int unroll = 4;       // 16-byte chunks per lane in flight in the row copy (4 or 6)
+  int unroll = 0;       // 16-byte chunks per lane in flight in the row copy (2, 4 or 6); 0 =
+                        // chosen per launch from the row sizes (mdsx_decode_shards)
   int nontemporal = 0;  // non-temporal loads/stores in the row copy
   int gather_chunks = 2;  // 16-byte chunks per lane in the ragged gather (tile = 4 KiB x this)
   int gather_min = 256;   // ragged columns averaging fewer bytes per row use the gather kernel

@@ -262,17 +262,18 @@ int mdsx_plan_create(const char* const* encodings, const int64_t* column_sizes, 
   // Tile = rows of one workgroup. All-fixed plans: about 32 KiB of rows per tile (>= 4 rows),
   // so the resident workgroups stream through a narrow window of the shard buffer -- measured
   // on config B (4 KiB rows): 4-8-row tiles 5.87 TB/s, 16: 5.66, 64: 5.52, and the plain copy
-  // probe 5.42 on the same box (scripts/tune_decode.py). Ragged plans: 64-row tiles, which keep
-  // the per-tile scan totals few (config C: 16 rows 3.69, 32: 3.86, 64: 3.84 TB/s). LDS per
-  // tile: a u32 source offset per (row, column), and per ragged column a u32 length and a u64
-  // destination offset per row (<= 16.4 KiB at 64 columns and 64 rows).
+  // probe 5.42 on the same box (scripts/tune_decode.py). Ragged plans: 32-row tiles (config C,
+  // 4 KiB blobs + ~340-byte strings: 4.19 vs 3.99 TB/s at 64 rows; 256-1024-byte blobs +
+  // 64-256-code-point strings: 1.99 vs 1.99; 32-256-byte rows 0.81 vs 0.86). LDS per tile: a u32
+  // source offset per (row, column), and per ragged column a u32 length and a u64 destination
+  // offset per row (<= 16.4 KiB at 64 columns and 64 rows).
   if (p->nvar == 0) {
     const int64_t per_row = p->fixed_sum > 0 ? p->fixed_sum : 1;
     int tr = 4;
     while (tr < 256 && int64_t(tr) * 2 * per_row <= 32 * 1024) tr *= 2;
     p->tile_rows = tr;
   } else {
-    p->tile_rows = 64;
+    p->tile_rows = 32;
   }
   // Encoder tiles: 16 rows (config B encode 5.06 TB/s vs 4.94 at 8 and 4.76 at 64; config C
   // 4.12 vs 3.74 at 64).
