@@ -50,7 +50,7 @@ def test_plan_for_every_golden_schema(name):
             assert col.row_bytes == size
     assert plan.num_var == sum(1 for s in info['column_sizes'] if not s)
     if plan.num_var:
-        assert plan.tile_rows == 64
+        assert plan.tile_rows == 32
     else:  # about 32 KiB of rows per decode tile, 4..256 rows
         per_row = sum(info['column_sizes'])
         assert plan.tile_rows in (4, 8, 16, 32, 64, 128, 256)
