@@ -13,7 +13,8 @@ collectives are the timing barrier and the max-over-ranks reduction outside the 
 Prints ONE JSON line (rank 0) with the metric, a ``roofline`` object for the decode kernel
 (algorithmic bytes R+W per launch / HIP-event kernel time, vs the 8 TB/s HBM3E peak) and a
 ``cpu_baseline`` object: the oracle's per-sample reader (a port of the reference algorithm,
-oracle/mds_oracle.py) timed on one host core over a bounded sample of the same workload.
+oracle/mds_oracle.py) timed on 16 host cores (one process each, 2 s: ~32 s of CPU work) over a
+bounded sample of the same workload.
 """
 
 from __future__ import annotations
@@ -42,10 +43,11 @@ def parse_args():
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--config', choices=['B', 'C'], default='B')
     ap.add_argument('--samples', type=int, default=1_000_000, help='samples per GPU')
-    ap.add_argument('--cpu-seconds', type=float, default=10.0,
+    ap.add_argument('--cpu-seconds', type=float, default=2.0,
                     help='CPU baseline time budget (0 disables)')
-    ap.add_argument('--cpu-procs', type=int, default=1,
-                    help='CPU baseline processes (disjoint shard copies, one per core)')
+    ap.add_argument('--cpu-procs', type=int, default=16,
+                    help='CPU baseline processes (disjoint shard copies, one per core; 16 = the '
+                         'host-core share of one GPU on the MI355X boxes)')
     ap.add_argument('--no-verify', action='store_true')
     ap.add_argument('--no-copy-probe', dest='copy_probe', action='store_false',
                     help='skip the same-run copy-ceiling measurement')
@@ -174,7 +176,7 @@ def cpu_baseline(args):
         'sample': (f'oracle per-sample MDSReader loop (open/seek/read + frombuffer per sample, '
                    f'mds/reader.py:103-149; encodings.py:760-773) over a 64 MiB config-'
                    f'{args.config} shard from page cache per process, {procs} process(es), '
-                   f'{done} samples in {dt:.1f} s'),
+                   f'{done} samples in {dt:.1f} s ({done / dt / procs:.0f} samples/s per core)'),
     }
 
 
