@@ -772,7 +772,7 @@ __global__ __launch_bounds__(kBlock) void gather_fixed_kernel(const uint8_t* src
       wave_copy<false, 4, kNT, false>(src + uint64_t(r) * row_bytes, dst + k * row_bytes,
                                       row_bytes, lane);
     else
-      wave_copy<false, 4, kNT, true>(src + uint64_t(r) * row_bytes, dst + k * row_bytes,
+      wave_copy<false, 4, kNT, true, true>(src + uint64_t(r) * row_bytes, dst + k * row_bytes,
                                      row_bytes, lane);
   }
 }
@@ -854,7 +854,9 @@ __global__ __launch_bounds__(kBlock) void gather_copy_kernel(
     if (k0 + i >= m) break;
     const int64_t len = s_len[i];
     if (len <= 0) continue;  // wave-uniform
-    wave_copy<false, 4, kNT, true>(src_vals + s_src[i], dst_vals + s_dst[i], uint64_t(len), lane);
+    // the source is a caller's tensor, not a padded batch: load only chunks touching the row
+    wave_copy<false, 4, kNT, true, true>(src_vals + s_src[i], dst_vals + s_dst[i], uint64_t(len),
+                                         lane);
   }
 }
 

@@ -163,9 +163,11 @@ class ShardPipeline:
         raw, tile_shard, row0, rows, tiles = _tables(sizes, [s.samples for s in group], offsets,
                                                      self.plan.tile_rows)
         dev = self.device
-        return DeviceBatch(slot.dev[:total], torch.from_numpy(raw).to(dev, non_blocking=False),
-                           torch.from_numpy(tile_shard).to(dev) if tiles else torch.zeros(
-                               1, dtype=torch.int32, device=dev), offsets, sizes,
+        # small tables: pinned + async on the compute stream (no host wait on the device)
+        descs = torch.from_numpy(raw).pin_memory().to(dev, non_blocking=True)
+        tiles_t = (torch.from_numpy(tile_shard).pin_memory().to(dev, non_blocking=True)
+                   if tiles else torch.zeros(1, dtype=torch.int32, device=dev))
+        return DeviceBatch(slot.dev[:total], descs, tiles_t, offsets, sizes,
                            [s.samples for s in group], row0, tiles, rows, self.plan.tile_rows)
 
     def __iter__(self) -> Iterator[DecodedBatch]:
@@ -207,11 +209,17 @@ class ShardPipeline:
                 for got, shard in zip(hex_digests(self.validate_hash, digests), group):
                     if got != shard.hashes[self.validate_hash]:
                         raise ValueError(f'Checksum failure: {shard.path}')
-            nxt = gi + len(self.slots)
-            if nxt < ngroups:
-                # the host buffer may be refilled once its H2D copy has completed
-                slot.copied.synchronize()
-                pending.append((slot, *self._stage(slot, self.groups[nxt]), self.groups[nxt]))
+            # Refill the PREVIOUS batch's host buffer now: its H2D copy was queued ahead of this
+            # one's, so waiting for it keeps this copy in flight and the next one can be queued
+            # right behind it (back-to-back H2D, the end-to-end bound).
+            # (One slot: refill it as soon as its own copy is done.)
+            lag = 1 if len(self.slots) > 1 else 0
+            if gi >= lag:
+                prev = self.slots[(gi - lag) % len(self.slots)]
+                nxt = gi - lag + len(self.slots)
+                if nxt < ngroups:
+                    prev.copied.synchronize()
+                    pending.append((prev, *self._stage(prev, self.groups[nxt]), self.groups[nxt]))
             yield out
         # surface kernel-reported errors of the last batches
         for slot in self.slots:

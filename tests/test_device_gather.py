@@ -78,3 +78,25 @@ def test_gather_config_b_full_size_permutation():
     g = dec.gather(perm)
     assert torch.equal(g['id'], synth.sources['id'][perm])
     assert torch.equal(g['x'].view(torch.int32), synth.sources['x'].view(torch.int32)[perm])
+
+
+def test_ragged_gather_reads_only_inside_the_source_tensor():
+    """The ragged gather copies from caller tensors with no padding: a row at the very start (or
+    end) of a freshly mapped values allocation, landing at a misaligned destination, must be
+    copied without touching bytes outside the tensor (it would fault)."""
+    from streaming_amd.decoder import DecodedBatch
+    torch.cuda.empty_cache()
+    n_bytes = (96 << 20) + 3  # its own segment, not a multiple of 16
+    values = torch.randint(0, 256, (n_bytes, ), dtype=torch.uint8, device='cuda')
+    lens = [5, 17, 1, 33] + [4096 + 7] * 1000
+    lens.append(n_bytes - sum(lens))
+    offsets = torch.tensor(np.concatenate([[0], np.cumsum(lens)]), dtype=torch.int64,
+                           device='cuda')
+    col = RaggedColumn(values, offsets, None)
+    n = len(lens)
+    ids = [1, 0, 2, n - 1, 3, 0, n - 1] + list(range(4, n - 1))
+    got = DecodedBatch({'v': col}, n).gather(ids)['v']
+    v, o = got.values.cpu().numpy(), got.offsets.cpu().numpy()
+    src, so = values.cpu().numpy(), offsets.cpu().numpy()
+    for k, r in enumerate(ids):
+        assert np.array_equal(v[o[k]:o[k + 1]], src[so[r]:so[r + 1]]), k

@@ -36,15 +36,16 @@ def _merge(parts):
     return merged
 
 
-@pytest.mark.parametrize('name,per', [('zstd', 1), ('config_c_small', 1), ('config_a', 5),
-                                      ('config_a', 64), ('wide', 3)])
-def test_pipeline_matches_reference(name, per):
+@pytest.mark.parametrize('name,per,depth', [('zstd', 1, 2), ('config_c_small', 1, 2),
+                                            ('config_a', 5, 2), ('config_a', 64, 2),
+                                            ('wide', 3, 2), ('config_a', 7, 1), ('config_a', 3, 3)])
+def test_pipeline_matches_reference(name, per, depth):
     d = os.path.join(gu.GOLDEN, name)
     idx = gu.index(name)
     info = idx['shards'][0]
     plan = Plan(info['column_names'], info['column_encodings'], info['column_sizes'])
     files = shard_files_from_index(d, idx)
-    pipe = ShardPipeline(plan, files, shards_per_batch=per, depth=2, workers=4)
+    pipe = ShardPipeline(plan, files, shards_per_batch=per, depth=depth, workers=4)
     parts = []
     for b in pipe:
         parts.append({k: (RaggedColumn(v.values.clone(), v.offsets.clone()) if isinstance(
