@@ -85,6 +85,14 @@ def _fill(view: np.ndarray, shard: ShardFile, host_hash: Optional[str] = None) -
         raise ValueError(f'Checksum failure: {shard.path}')
 
 
+def _fill_after(event: Optional[torch.cuda.Event], view: np.ndarray, shard: ShardFile,
+                host_hash: Optional[str]) -> None:
+    """Fill a staging slice once the slot's previous H2D copy (``event``) has completed."""
+    if event is not None:
+        event.synchronize()
+    _fill(view, shard, host_hash)
+
+
 class _Slot:
 
     def __init__(self, total: int, device: torch.device) -> None:
@@ -148,13 +156,16 @@ class ShardPipeline:
         self.copy_stream = torch.cuda.Stream(dev)
         self._lock = threading.Lock()
 
-    def _stage(self, slot: _Slot, group: Sequence[ShardFile]):
+    def _stage(self, slot: _Slot, group: Sequence[ShardFile], after: bool = False):
+        """Read / decompress ``group`` into the slot's pinned buffer on the pool threads; with
+        ``after``, each task first waits for the slot's previous H2D copy to complete."""
         sizes = [s.raw_bytes for s in group]
         offsets, total = _layout(sizes)
         view = slot.host.numpy()
         host_hash = self.validate_hash if self.validate_hash and not self._device_hash else None
+        event = slot.copied if after else None
         futs = [
-            self.pool.submit(_fill, view[o:o + s.raw_bytes], s, host_hash)
+            self.pool.submit(_fill_after, event, view[o:o + s.raw_bytes], s, host_hash)
             for o, s in zip(offsets, group)
         ]
         return futs, sizes, offsets, total
@@ -188,6 +199,13 @@ class ShardPipeline:
                 slot.dev[:total].copy_(slot.host[:total], non_blocking=True)
                 slot.copied.record(self.copy_stream)
             compute.wait_event(slot.copied)
+            # Restage this slot for batch gi + depth right away: the pool threads wait for this
+            # copy to land, then refill the pinned buffer, while this loop moves on (copies are
+            # queued back to back; host reads / decompression of later batches overlap).
+            nxt = gi + len(self.slots)
+            if nxt < ngroups:
+                pending.append((slot, *self._stage(slot, self.groups[nxt], after=True),
+                                self.groups[nxt]))
             batch = self._batch(slot, group, sizes, offsets, total)
             digests = None
             if self._device_hash:
@@ -209,17 +227,6 @@ class ShardPipeline:
                 for got, shard in zip(hex_digests(self.validate_hash, digests), group):
                     if got != shard.hashes[self.validate_hash]:
                         raise ValueError(f'Checksum failure: {shard.path}')
-            # Refill the PREVIOUS batch's host buffer now: its H2D copy was queued ahead of this
-            # one's, so waiting for it keeps this copy in flight and the next one can be queued
-            # right behind it (back-to-back H2D, the end-to-end bound).
-            # (One slot: refill it as soon as its own copy is done.)
-            lag = 1 if len(self.slots) > 1 else 0
-            if gi >= lag:
-                prev = self.slots[(gi - lag) % len(self.slots)]
-                nxt = gi - lag + len(self.slots)
-                if nxt < ngroups:
-                    prev.copied.synchronize()
-                    pending.append((prev, *self._stage(prev, self.groups[nxt]), self.groups[nxt]))
             yield out
         # surface kernel-reported errors of the last batches
         for slot in self.slots:
