@@ -751,14 +751,30 @@ __global__ __launch_bounds__(64) void xxh_seq_kernel(const HashArgs a) {
     if (lo < mybody) {
       const int steps = int(min(uint64_t(kWin), mybody - lo) / kStripeBytes);
       const uint8_t* win = reinterpret_cast<const uint8_t*>(s_win[w & 1][ls]);
+      // The chain's inputs are read from LDS 16 at a time ahead of the dependent rounds (and
+      // their lane * PRIME products formed off the chain).
+      constexpr int kBatch = 16;
+      int i = 0;
       if constexpr (k64) {
         const uint64_t* src = reinterpret_cast<const uint64_t*>(win) + k;
-#pragma unroll 8
-        for (int i = 0; i < steps; ++i) v64 = round64(v64, src[4 * i]);
+        for (; i + kBatch <= steps; i += kBatch) {
+          uint64_t t[kBatch];
+#pragma unroll
+          for (int j = 0; j < kBatch; ++j) t[j] = src[4 * (i + j)] * P64_2;
+#pragma unroll
+          for (int j = 0; j < kBatch; ++j) v64 = rotl64(v64 + t[j], 31) * P64_1;
+        }
+        for (; i < steps; ++i) v64 = round64(v64, src[4 * i]);
       } else {
         const uint32_t* src = reinterpret_cast<const uint32_t*>(win) + k;
-#pragma unroll 8
-        for (int i = 0; i < steps; ++i) v32 = round32(v32, src[4 * i]);
+        for (; i + kBatch <= steps; i += kBatch) {
+          uint32_t t[kBatch];
+#pragma unroll
+          for (int j = 0; j < kBatch; ++j) t[j] = src[4 * (i + j)] * P32_2;
+#pragma unroll
+          for (int j = 0; j < kBatch; ++j) v32 = rotl32(v32 + t[j], 13) * P32_1;
+        }
+        for (; i < steps; ++i) v32 = round32(v32, src[4 * i]);
       }
     }
     __syncthreads();  // every lane is done with buffer (w + 1) & 1's previous window
