@@ -267,7 +267,9 @@ __device__ __forceinline__ bool wave_copy(const uint8_t* src, uint8_t* dst, uint
 // Partial chunks at a row's ends are stored one byte per lane of the group. (str rows are
 // validated afterwards by group_utf8_bad: fused here the check costs the decode kernel a wave per
 // SIMD, 118 vs 89 VGPRs.)
-template <int kUnroll, bool kNT>
+// kClamp: the source is a caller's tensor (not a padded batch): only aligned chunks touching
+// [src, src + len) are loaded.
+template <int kUnroll, bool kNT, bool kClamp = false>
 __device__ __forceinline__ void group_copy(const uint8_t* src, uint8_t* dst, uint64_t len,
                                            int lane) {
   const int gl = lane & 15;
@@ -289,10 +291,15 @@ __device__ __forceinline__ void group_copy(const uint8_t* src, uint8_t* dst, uin
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       const uint64_t k = base + uint64_t(u) * 16 + gl;
-      lo[u] = k < nload ? ld16<kNT>(sal + k) : make_uint4(0, 0, 0, 0);
+      const bool live = k < nload && (!kClamp || chunk_touches(sal + k, src, len));
+      lo[u] = live ? ld16<kNT>(sal + k) : make_uint4(0, 0, 0, 0);
     }
     uint4 tail = make_uint4(0, 0, 0, 0);
-    if (sh != 0 && gl == 15 && base + 16 * kUnroll < nload) tail = ld16<kNT>(sal + base + 16 * kUnroll);
+    {
+      const uint64_t k = base + 16 * kUnroll;
+      if (sh != 0 && gl == 15 && k < nload && (!kClamp || chunk_touches(sal + k, src, len)))
+        tail = ld16<kNT>(sal + k);
+    }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       const uint64_t k0 = base + uint64_t(u) * 16;

@@ -818,8 +818,9 @@ __global__ __launch_bounds__(kBlock) void scan_tile_totals_kernel(const int64_t*
   }
 }
 
-// Ragged column, pass 2: final offsets, flags, and one row per wave copied.
-template <bool kNT>
+// Ragged column, pass 2: final offsets, flags, and the rows copied: one per wave, or (kGroup,
+// rows of a few hundred bytes) four per wave, one per 16-lane group.
+template <bool kNT, bool kGroup>
 __global__ __launch_bounds__(kBlock) void gather_copy_kernel(
     const uint8_t* src_vals, const int64_t* src_off, const uint8_t* src_flags, uint64_t nsrc,
     const int64_t* idx, uint64_t m, uint8_t* dst_vals, uint64_t capacity, int64_t* dst_off,
@@ -850,13 +851,25 @@ __global__ __launch_bounds__(kBlock) void gather_copy_kernel(
     s_len[threadIdx.x] = len;
   }
   __syncthreads();
-  for (int i = wave; i < kGatherRowTile; i += kBlock / 64) {
-    if (k0 + i >= m) break;
-    const int64_t len = s_len[i];
-    if (len <= 0) continue;  // wave-uniform
-    // the source is a caller's tensor, not a padded batch: load only chunks touching the row
-    wave_copy<false, 4, kNT, true, true>(src_vals + s_src[i], dst_vals + s_dst[i], uint64_t(len),
-                                         lane);
+  // the source is a caller's tensor, not a padded batch: load only chunks touching the row
+  if constexpr (kGroup) {
+    const int g = lane >> 4;
+    for (int r0 = wave * 4; r0 < kGatherRowTile; r0 += kBlock / 16) {
+      if (k0 + r0 >= m) break;  // wave-uniform
+      const int i = r0 + g;
+      const bool live = k0 + i < m && s_len[i] > 0;
+      group_copy<2, kNT, true>(live ? src_vals + s_src[i] : src_vals,
+                               live ? dst_vals + s_dst[i] : dst_vals,
+                               live ? uint64_t(s_len[i]) : 0, lane);
+    }
+  } else {
+    for (int i = wave; i < kGatherRowTile; i += kBlock / 64) {
+      if (k0 + i >= m) break;
+      const int64_t len = s_len[i];
+      if (len <= 0) continue;  // wave-uniform
+      wave_copy<false, 4, kNT, true, true>(src_vals + s_src[i], dst_vals + s_dst[i],
+                                           uint64_t(len), lane);
+    }
   }
 }
 
@@ -1115,9 +1128,16 @@ int mdsx_gather_ragged_copy(const uint8_t* src_values, const int64_t* src_offset
     return mdsx::fail(MDSX_E_ARG, "mdsx_gather_ragged_copy: bad argument");
   if (m == 0) return MDSX_OK;
   const unsigned tiles = unsigned((m + kGatherRowTile - 1) / kGatherRowTile);
-  hipLaunchKernelGGL((gather_copy_kernel<true>), dim3(tiles), dim3(kBlock), 0,
-                     static_cast<hipStream_t>(stream), src_values, src_offsets, src_flags,
-                     src_rows, idx, m, dst_values, dst_capacity, dst_offsets, dst_flags, tp, st);
+  // rows averaging under 1 KiB: four per wave (as the decode's medium rows)
+  const bool group = dst_capacity < uint64_t(1024) * m;
+  if (group)
+    hipLaunchKernelGGL((gather_copy_kernel<true, true>), dim3(tiles), dim3(kBlock), 0,
+                       static_cast<hipStream_t>(stream), src_values, src_offsets, src_flags,
+                       src_rows, idx, m, dst_values, dst_capacity, dst_offsets, dst_flags, tp, st);
+  else
+    hipLaunchKernelGGL((gather_copy_kernel<true, false>), dim3(tiles), dim3(kBlock), 0,
+                       static_cast<hipStream_t>(stream), src_values, src_offsets, src_flags,
+                       src_rows, idx, m, dst_values, dst_capacity, dst_offsets, dst_flags, tp, st);
   return hip_check(hipGetLastError(), "gather_copy_kernel launch");
 }
 

@@ -80,15 +80,17 @@ def test_gather_config_b_full_size_permutation():
     assert torch.equal(g['x'].view(torch.int32), synth.sources['x'].view(torch.int32)[perm])
 
 
-def test_ragged_gather_reads_only_inside_the_source_tensor():
+@pytest.mark.parametrize('row', [4096 + 7, 300])
+def test_ragged_gather_reads_only_inside_the_source_tensor(row):
     """The ragged gather copies from caller tensors with no padding: a row at the very start (or
     end) of a freshly mapped values allocation, landing at a misaligned destination, must be
-    copied without touching bytes outside the tensor (it would fault)."""
+    copied without touching bytes outside the tensor (it would fault). Long rows (one per wave)
+    and medium rows (four per wave)."""
     from streaming_amd.decoder import DecodedBatch
     torch.cuda.empty_cache()
     n_bytes = (96 << 20) + 3  # its own segment, not a multiple of 16
     values = torch.randint(0, 256, (n_bytes, ), dtype=torch.uint8, device='cuda')
-    lens = [5, 17, 1, 33] + [4096 + 7] * 1000
+    lens = [5, 17, 1, 33] + [row] * ((n_bytes - (1 << 20)) // row)
     lens.append(n_bytes - sum(lens))
     offsets = torch.tensor(np.concatenate([[0], np.cumsum(lens)]), dtype=torch.int64,
                            device='cuda')
