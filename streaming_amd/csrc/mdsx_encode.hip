@@ -38,6 +38,8 @@ struct EncCol {
   uint64_t bytes;  // size of data (bounds of the ragged offsets)
   uint32_t row_bytes;
   int32_t var_index;
+  int32_t group;  // ragged rows averaging < 1 KiB: four rows per wave (group_copy)
+  int32_t pad_;
 };
 
 struct EncArgs {
@@ -207,11 +209,23 @@ __global__ __launch_bounds__(kEncBlock) void encode_kernel(const EncArgs a) {
       store_small(file + s_pos[c * TR + t], v, col.row_bytes);
     }
   }
-  // larger fixed columns and ragged rows: one row per wave
+  // larger fixed columns and ragged rows: one row per wave; medium ragged rows four per wave
   for (int c = 0; c < a.ncols; ++c) {
     const EncCol& col = a.cols[c];
     const bool var = col.var_index >= 0;
     if (!var && col.row_bytes <= 16) continue;
+    if (var && col.group) {
+      const int gi = lane >> 4;
+      for (int q0 = wave * 4; q0 < nrows; q0 += kEncBlock / 16) {
+        const int r = q0 + gi;
+        const bool live = r < nrows;
+        const uint64_t g = e.d.row0 + r0 + uint64_t(live ? r : 0);
+        const int64_t b = live ? col.offsets[g] : 0;
+        const uint64_t len = live ? uint64_t(col.offsets[g + 1] - b) : 0;
+        group_copy<2, kNT, true>(col.data + b, file + (live ? s_pos[c * TR + r] : 0), len, lane);
+      }
+      continue;
+    }
     for (int r = wave; r < nrows; r += kEncBlock / 64) {
       const uint64_t g = e.d.row0 + r0 + r;
       const uint8_t* src;
@@ -245,6 +259,7 @@ bool fill_args(const mdsx_plan* plan, const mdsx_column_in* cols, uint64_t rows,
     d.var_index = spec.var_index;
     if (spec.var_index >= 0) {
       if (!d.offsets || (rows && !d.data)) return false;
+      d.group = rows && d.bytes < uint64_t(1024) * rows;
     } else {
       d.row_bytes = uint32_t(spec.row_bytes);
       fixed += spec.row_bytes;
