@@ -48,6 +48,9 @@ def parse_args():
     ap.add_argument('--cpu-procs', type=int, default=16,
                     help='CPU baseline processes (disjoint shard copies, one per core; 16 = the '
                          'host-core share of one GPU on the MI355X boxes)')
+    ap.add_argument('--single', action='store_true',
+                    help='ragged configs: single-pass decode (look-back scan inside the decode '
+                    'kernel, outputs at the payload bound) instead of scan + decode')
     ap.add_argument('--no-verify', action='store_true')
     ap.add_argument('--no-copy-probe', dest='copy_probe', action='store_false',
                     help='skip the same-run copy-ceiling measurement')
@@ -222,7 +225,7 @@ def main():
     from streaming_amd.decoder import BatchDecoder, output_bytes
 
     plan, batch, sources, workload = build_workload(args, rank, world)
-    dec = BatchDecoder(plan, batch)
+    dec = BatchDecoder(plan, batch, single=args.single)
     out = dec.run()
     dec.check()
     if not args.no_verify:

@@ -167,6 +167,22 @@ int mdsx_decode_shards(const mdsx_plan* plan, const mdsx_batch* batch,
                        const mdsx_column_out* outs, void* d_workspace, uint64_t workspace_bytes,
                        void* stream);
 
+/* Single-pass decode: passes 1 and 2 in one launch sequence, with no host round trip for the
+ * totals. Each tile of the decode kernel scans its own ragged lengths and finds its base by
+ * decoupled look-back over the tiles before it (tiles are taken in dispatch order from a
+ * ticket), so ragged outputs are sized BEFORE the totals are known: outs[c].capacity of a ragged
+ * column is its allocation (an upper bound such as the batch's sample bytes); a column that
+ * needs more reports MDSX_E_CAPACITY. offsets[rows] and d_totals (device int64[num_var], may be
+ * NULL) receive the totals. Same outputs as mdsx_scan_shards + mdsx_decode_shards.
+ *   mode_bytes : host uint64[num_columns] (may be NULL): the expected bytes of each ragged column
+ *                (e.g. the previous batch's totals). It only picks the copy mode and the grid of
+ *                the destination-major copy -- a wrong guess is slower, never wrong; NULL uses
+ *                the capacities. Replaces the same reader path as the two passes. */
+int mdsx_decode_shards_single(const mdsx_plan* plan, const mdsx_batch* batch,
+                              const mdsx_column_out* outs, const uint64_t* mode_bytes,
+                              void* d_workspace, uint64_t workspace_bytes, int64_t* d_totals,
+                              void* stream);
+
 /* ---- batch gather by sample id ---------------------------------------------
  * out[k] = column[idx[k]] over already-decoded columns: the device side of the reference's
  * per-sample iteration over a worker's sample ids (StreamingDataset.__iter__ ->

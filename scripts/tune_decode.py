@@ -4,7 +4,8 @@
 
 Each variant builds its own plan (MDSX_TUNE is read at plan creation) over the SAME resident
 shard batch (tile tables rebuilt for its tile size), is verified bit-exact, then all variants are
-timed round-robin for --rounds rounds with HIP events around the decode kernel. Also times a
+timed round-robin for --rounds rounds with HIP events around the scan + decode kernels (a
+variant holding 'single' runs the single-pass decode). Also times a
 torch device-to-device copy of the shard bytes (the measured HBM copy ceiling on this box).
 """
 
@@ -57,11 +58,12 @@ def main():
     decs = {}
     for v in args.variants:
         # 'enc=a|b|c' overrides the column encodings (e.g. read a str column as bytes)
-        knobs = [kv for kv in v.split(',') if not kv.startswith('enc=')]
+        # 'single' runs the single-pass decode (mdsx_decode_shards_single) for that variant
+        knobs = [kv for kv in v.split(',') if not kv.startswith('enc=') and kv != 'single']
         encs = [kv[4:].split('|') for kv in v.split(',') if kv.startswith('enc=')]
         os.environ['MDSX_TUNE'] = ','.join(knobs)
         plan = Plan(names[0], encs[0] if encs else names[1], names[2])
-        dec = BatchDecoder(plan, retile(base_batch, plan))
+        dec = BatchDecoder(plan, retile(base_batch, plan), single='single' in v.split(','))
         out = dec.run()
         dec.check()
         if args.config == 'B':
@@ -90,7 +92,7 @@ def main():
             for e in evs:
                 dec.run(e)
             torch.cuda.synchronize()
-            times[v].extend(e[1].elapsed_time(e[2]) for e in evs)
+            times[v].extend(e[0].elapsed_time(e[2]) for e in evs)  # scan (if any) + decode
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         for _ in range(args.iters):

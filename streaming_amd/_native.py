@@ -55,6 +55,7 @@ EXPORTED_SYMBOLS = (
     'mdsx_workspace_bytes',
     'mdsx_scan_shards',
     'mdsx_decode_shards',
+    'mdsx_decode_shards_single',
     'mdsx_copy_probe',
     'mdsx_gather_workspace_bytes',
     'mdsx_gather_fixed',
@@ -160,6 +161,10 @@ def _declare(handle: ctypes.CDLL) -> None:
     handle.mdsx_scan_shards.argtypes = [vp, pb, ctypes.POINTER(ColumnOut), vp, c_u64, vp, vp]
     handle.mdsx_decode_shards.restype = c_int
     handle.mdsx_decode_shards.argtypes = [vp, pb, ctypes.POINTER(ColumnOut), vp, c_u64, vp]
+    handle.mdsx_decode_shards_single.restype = c_int
+    handle.mdsx_decode_shards_single.argtypes = [
+        vp, pb, ctypes.POINTER(ColumnOut), ctypes.POINTER(c_u64), vp, c_u64, vp, vp
+    ]
     handle.mdsx_copy_probe.restype = c_int
     handle.mdsx_copy_probe.argtypes = [vp, vp, c_u64, vp]
     handle.mdsx_ndarray_meta.restype = c_int

@@ -32,6 +32,7 @@
 // the shard before it is touched.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 
@@ -68,6 +69,8 @@ struct DevArgs {
   int64_t* totals;       // [nvar] or null
   uint64_t* src_abs;     // [nvar][rows]  byte index into the batch of each row's ragged value
   uint32_t* row_map;     // [nvar][map_len] first row of every gather tile
+  uint64_t* lookback;    // [nvar][ntiles] single-pass look-back status words
+  uint32_t* ticket;      // single-pass tile ticket counter
   uint64_t map_len;
   uint64_t rows;
   uint32_t ntiles;
@@ -232,9 +235,21 @@ __global__ __launch_bounds__(kBlock) void scan_totals_kernel(const DevArgs a) {
 }
 
 
+// Look-back status word of one (ragged column, tile): flag in the top 2 bits (0 not yet
+// published, 1 the tile's own aggregate, 2 the inclusive prefix), a byte count below.
+constexpr uint64_t kLbAggregate = 1ull << 62, kLbInclusive = 2ull << 62;
+constexpr uint64_t kLbValue = (1ull << 62) - 1;
+typedef __attribute__((address_space(1))) uint64_t gu64;
+
 // Pass 2: per-row column boundaries; fixed columns decoded; ragged columns prepared for the
 // destination-major gather (final offsets, per-row source addresses, gather-tile row map).
-template <int kUnroll, bool kNT, bool kRagged, bool kEdges>
+// kSingle: one pass, no scan kernels before it (mdsx_decode_shards_single). Tiles are taken in
+// dispatch order from a ticket counter, so every tile a workgroup waits on is held by a
+// workgroup that is already running; each tile block-scans its ragged lengths, publishes its
+// aggregate per ragged column and finds its base by decoupled look-back over the earlier tiles'
+// status words. Flag and value share one 8-byte word written and read with agent-scope atomics,
+// so no fence orders them.
+template <int kUnroll, bool kNT, bool kRagged, bool kEdges, bool kSingle>
 __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int TR = a.tile_rows;
@@ -242,27 +257,37 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
   uint32_t* s_src = reinterpret_cast<uint32_t*>(s_vdst + a.nvar * TR);  // [ncols][TR]
   uint32_t* s_vlen = s_src + a.ncols * TR;                               // [nvar][TR]
   uint8_t* s_ok = reinterpret_cast<uint8_t*>(s_vlen + a.nvar * TR);     // [TR]
+  __shared__ uint32_t s_tile;
+  __shared__ int64_t s_wsum[kBlock / 64];
+  __shared__ int64_t s_base[kSingle ? MDSX_MAX_COLUMNS : 1];
 
-  const TileView v = tile_view(a, blockIdx.x);
   const int t = threadIdx.x;
   const int lane = t & 63, wave = t >> 6;
+  uint32_t tile = blockIdx.x;
+  if constexpr (kSingle) {
+    if (t == 0) s_tile = atomicAdd(a.ticket, 1u);
+    __syncthreads();
+    tile = s_tile;
+  }
+  const TileView v = tile_view(a, tile);
 
   if (!v.table_ok) {
-    if (t == 0 && blockIdx.x == v.d.tile0) report(a.status, MDSX_E_HEADER, v.shard_idx, -1, -1);
-    return;  // block-uniform
+    if (t == 0 && tile == v.d.tile0) report(a.status, MDSX_E_HEADER, v.shard_idx, -1, -1);
+    if constexpr (!kSingle) return;  // block-uniform (kSingle: the tile still publishes zeros)
   }
-  if (t == 0 && blockIdx.x == v.d.tile0) {
+  if (t == 0 && tile == v.d.tile0 && v.table_ok) {
     // Header written by encode_joint_shard (mds/writer.py:133-144): u32 N, then N+1 offsets.
     const uint32_t n = *reinterpret_cast<const uint32_t*>(v.shard);
     const uint32_t first = v.offs[0];
     if (n != v.d.samples || first < v.hdr_end || v.offs[v.d.samples] > v.d.bytes)
       report(a.status, MDSX_E_HEADER, v.shard_idx, -1, -1);
   }
+  const int nrows = v.table_ok ? int(v.nrows) : 0;
 
-  // ---- column boundaries of this lane's row (MDSReader.decode_sample, mds/reader.py:111-125)
-  if (t < int(v.nrows)) {
+  // ---- column boundaries of this lane's row (MDSReader.decode_sample, mds/reader.py:111-125).
+  // A row failing any check keeps zero ragged lengths (the scan pass's rule).
+  if (t < nrows) {
     const uint32_t i = v.r0 + t;
-    const uint64_t row = v.d.row0 + i;
     uint32_t b = 0, e = 0;
     int rc = sample_range(v, i, &b, &e);
     bool ok = rc == MDSX_OK;
@@ -285,14 +310,101 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
       ok = false;
       rc = MDSX_E_BOUNDS;
     }
-    // Ragged columns: final offset = tile prefix + the local offset the scan pass left in
-    // offsets[row]; then either the destination for this kernel's wave copy, or (gather
-    // columns) the row's source address and the 4 KiB output grains whose first byte it holds.
+    if (!ok) {
+      for (int vi = 0; vi < a.nvar; ++vi) s_vlen[vi * TR + t] = 0;
+      if (rc != MDSX_OK) report(a.status, rc, v.shard_idx, int(i), -1);
+    }
+    s_ok[t] = ok ? 1 : 0;
+  }
+
+  if constexpr (kSingle) {
+    // ---- this tile's ragged offsets: block scan of the lengths, then the look-back for the base
+    __shared__ int64_t s_agg[MDSX_MAX_COLUMNS];
+    __syncthreads();
+    for (int vi = 0; vi < a.nvar; ++vi) {
+      const int64_t x = t < nrows ? int64_t(s_vlen[vi * TR + t]) : 0;
+      int64_t tot;
+      const int64_t excl = block_exclusive_scan(x, s_wsum, &tot);
+      if (t < nrows) s_vdst[vi * TR + t] = uint64_t(excl);
+      if (t == 0) s_agg[vi] = tot;
+    }
+    __syncthreads();
+    if (wave == 0) {
+      // Wave-parallel look-back, every ragged column at once: the wave splits into segments of W
+      // lanes, one per column (groups of 64 / W columns in turn); lane k of a segment reads the
+      // status of tile j - k. A segment sums its window up to the nearest inclusive prefix (tiles
+      // before 0 read as an inclusive zero), retrying while a tile inside that span has not
+      // published yet, and steps back W tiles when the window holds no inclusive prefix.
+      const int nv = a.nvar;
+      const int W = nv <= 1 ? 64 : nv <= 2 ? 32 : nv <= 4 ? 16 : 8;
+      const int kk = lane & (W - 1);
+      const int seg0 = lane & ~(W - 1);
+      const uint64_t wmask = W == 64 ? ~0ull : (1ull << W) - 1;
+      for (int g0 = 0; g0 < nv; g0 += 64 / W) {
+        const int vi = g0 + lane / W;
+        const bool mine = vi < nv;
+        gu64* st = (gu64*)(a.lookback + uint64_t(mine ? vi : 0) * a.ntiles);
+        const uint64_t agg = mine ? uint64_t(s_agg[vi]) : 0;
+        if (mine && kk == 0)
+          __hip_atomic_store(st + tile, (tile == 0 ? kLbInclusive : kLbAggregate) | agg,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t base = 0;
+        int64_t j = int64_t(tile) - 1;
+        bool done = !mine || tile == 0;
+        uint32_t polls = 0;
+        while (__ballot(!done) != 0) {
+          const int64_t k = j - kk;
+          const uint64_t w = (!done && k >= 0) ? __hip_atomic_load(st + k, __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT)
+                                               : kLbInclusive;
+          const uint64_t incl = (__ballot((w >> 62) == 2) >> seg0) & wmask;
+          const uint64_t none = (__ballot((w >> 62) == 0) >> seg0) & wmask;
+          const uint64_t span = incl ? ((incl & (0 - incl)) << 1) - 1 : wmask;  // lanes <= first
+          // an earlier tile's workgroup is still scanning its rows (it is running: it holds a
+          // ticket); the bound only keeps a broken invariant from hanging the launch
+          const bool wait = !done && (none & span) != 0 && ++polls < (1u << 22);
+          uint64_t x = (!done && !wait && ((span >> kk) & 1)) ? (w & kLbValue) : 0;
+          for (int o = W >> 1; o > 0; o >>= 1) x += __shfl_xor(x, o);
+          if (!done && !wait) {
+            if ((none & span) != 0 && kk == 0) report(a.status, MDSX_E_HIP, v.shard_idx, -1, -1);
+            base += x;
+            if (incl) done = true;
+            else j -= W;
+          }
+          if (__ballot(wait) != 0) __builtin_amdgcn_s_sleep(1);
+        }
+        if (mine && kk == 0) {
+          if (tile != 0)
+            __hip_atomic_store(st + tile, kLbInclusive | (base + agg), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+          s_base[vi] = int64_t(base);
+          if (tile + 1 == a.ntiles) {  // the batch's last tile: column totals
+            for (int c = 0; c < a.ncols; ++c)
+              if (a.cols[c].var_index == vi) a.cols[c].offsets[a.rows] = int64_t(base + agg);
+            if (a.totals) a.totals[vi] = int64_t(base + agg);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (!v.table_ok) return;  // block-uniform; published its zero aggregates above
+  }
+
+  // ---- ragged columns: final offsets; the destination of this kernel's copies, or (gather
+  // columns) the row's source address and the 4 KiB output grains whose first byte it holds.
+  if (t < nrows) {
+    const uint32_t i = v.r0 + t;
+    const uint64_t row = v.d.row0 + i;
+    bool ok = s_ok[t] != 0;
     for (int c = 0; c < a.ncols; ++c) {
       const DevCol& col = a.cols[c];
       if (col.var_index < 0) continue;
       const int vi = col.var_index;
-      const int64_t off = a.tile_prefix[uint64_t(vi) * a.ntiles + blockIdx.x] + col.offsets[row];
+      int64_t off;
+      if constexpr (kSingle)
+        off = s_base[vi] + int64_t(s_vdst[vi * TR + t]);
+      else  // the scan pass left the tile-local offset in offsets[row]
+        off = a.tile_prefix[uint64_t(vi) * a.ntiles + tile] + col.offsets[row];
       col.offsets[row] = off;
       s_vdst[vi * TR + t] = uint64_t(off);
       if (col.flags) col.flags[row] = 0;
@@ -312,7 +424,6 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
           map[g] = uint32_t(row);
       }
     }
-    if (!ok && rc != MDSX_OK) report(a.status, rc, v.shard_idx, int(i), -1);
     s_ok[t] = ok ? 1 : 0;
   }
   __syncthreads();
@@ -582,28 +693,31 @@ __global__ __launch_bounds__(kBlock) void gather_ragged_kernel(const DevArgs a) 
   int ci = 0;
   while (a.cols[ci].var_index != vi) ++ci;
   const DevCol& col = a.cols[ci];
-  const uint64_t g = blockIdx.x - a.gather_block0[vi];
   const int64_t tot = col.offsets[a.rows];
-  const int64_t T0 = int64_t(g * kGatherTile);
-  if (T0 >= tot) return;
-  if (a.status->code != 0 || (g + 1) * kGatherChunks >= a.map_len) return;  // decode failed
+  if (a.status->code != 0) return;  // decode failed
   const uint32_t* map = a.row_map + uint64_t(vi) * a.map_len;
-  const uint64_t r0 = map[g * kGatherChunks];
-  const uint64_t r1 =
-      (T0 + int64_t(kGatherTile) < tot) ? uint64_t(map[(g + 1) * kGatherChunks]) : a.rows - 1;
-  if (r0 >= a.rows || r1 >= a.rows || r1 < r0) return;  // never for a status-clean decode
-  const int n = int(r1 - r0 + 1);
   const uint64_t* src = a.src_abs + uint64_t(vi) * a.rows;
-  if (n <= kGatherRows) {
-    for (int i = threadIdx.x; i <= n; i += kBlock) {
-      s_off[i] = col.offsets[r0 + i];
-      if (i < n) s_src[i] = src[r0 + i];
+  const uint64_t stride = a.gather_block0[vi + 1] - a.gather_block0[vi];
+  for (uint64_t g = blockIdx.x - a.gather_block0[vi];; g += stride) {  // block-uniform loop
+    const int64_t T0 = int64_t(g * kGatherTile);
+    if (T0 >= tot || (g + 1) * kGatherChunks >= a.map_len) return;
+    const uint64_t r0 = map[g * kGatherChunks];
+    const uint64_t r1 =
+        (T0 + int64_t(kGatherTile) < tot) ? uint64_t(map[(g + 1) * kGatherChunks]) : a.rows - 1;
+    if (r0 >= a.rows || r1 >= a.rows || r1 < r0) return;  // never for a status-clean decode
+    const int n = int(r1 - r0 + 1);
+    __syncthreads();  // the previous tile's readers of s_off / s_src / s_edge
+    if (n <= kGatherRows) {
+      for (int i = threadIdx.x; i <= n; i += kBlock) {
+        s_off[i] = col.offsets[r0 + i];
+        if (i < n) s_src[i] = src[r0 + i];
+      }
+      __syncthreads();
+      gather_tile<kNT, kGatherChunks>(a, col, RowsLds{s_off, s_src}, n, r0, T0, tot, s_edge);
+    } else {
+      gather_tile<kNT, kGatherChunks>(a, col, RowsGlobal{col.offsets + r0, src + r0}, n, r0,
+                                      T0, tot, s_edge);
     }
-    __syncthreads();
-    gather_tile<kNT, kGatherChunks>(a, col, RowsLds{s_off, s_src}, n, r0, T0, tot, s_edge);
-  } else {
-    gather_tile<kNT, kGatherChunks>(a, col, RowsGlobal{col.offsets + r0, src + r0}, n, r0, T0,
-                                    tot, s_edge);
   }
 }
 
@@ -613,6 +727,10 @@ struct Layout {
 };
 
 __host__ uint64_t round256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
+
+// Host code below uses std::min / std::max: HIP's global host min / max are int-only and
+// truncate 64-bit sizes.
+constexpr uint64_t kTicketOffset = 128;  // single-pass tile ticket, inside the status block
 
 Layout workspace_layout(const mdsx_plan* plan, const mdsx_batch* b) {
   Layout L;
@@ -626,8 +744,12 @@ Layout workspace_layout(const mdsx_plan* plan, const mdsx_batch* b) {
   return L;
 }
 
+// mode_bytes (host, [ncols], may be null): the expected bytes of each ragged column, which pick
+// its copy mode and size its gather grid; null = outs[c].capacity (the two-pass decode, where the
+// capacity is the scanned total or close to it).
 int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out* outs,
-               void* d_workspace, uint64_t workspace_bytes, int64_t* d_totals, DevArgs* a) {
+               void* d_workspace, uint64_t workspace_bytes, int64_t* d_totals, DevArgs* a,
+               const uint64_t* mode_bytes = nullptr) {
   if (!plan || !b || !b->data || !b->shards || !b->tile_shard || !d_workspace ||
       b->nshards <= 0)
     return mdsx::fail(MDSX_E_ARG, "mdsx: null argument or empty batch");
@@ -645,6 +767,8 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   a->tile_prefix = reinterpret_cast<int64_t*>(ws + L.tile_prefix);
   a->src_abs = reinterpret_cast<uint64_t*>(ws + L.src_abs);
   a->row_map = reinterpret_cast<uint32_t*>(ws + L.row_map);
+  a->lookback = reinterpret_cast<uint64_t*>(ws + L.tile_total);  // single pass: no tile totals
+  a->ticket = reinterpret_cast<uint32_t*>(ws + kTicketOffset);
   a->map_len = L.map_len;
   a->totals = d_totals;
   a->rows = b->rows;
@@ -665,14 +789,17 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
     d.row_bytes = uint32_t(s.row_bytes);
     d.kind = int8_t(s.kind);
     d.var_index = int8_t(s.var_index);
+    const uint64_t expect =
+        mode_bytes ? std::min(mode_bytes[c], outs[c].capacity) : outs[c].capacity;
     // Short ragged rows keep a wave's lanes busy only when copied destination-major.
     d.gather = s.kind != MDSX_KIND_FIXED && b->rows > 0 &&
-               outs[c].capacity < uint64_t(plan->gather_min) * b->rows;
+               expect < uint64_t(plan->gather_min) * b->rows;
     // Medium rows (a few hundred bytes): four per wave, one per 16-lane group (decided below).
     d.group = s.kind != MDSX_KIND_FIXED && !d.gather && b->rows > 0 &&
-              outs[c].capacity < uint64_t(plan->group_max) * b->rows;
+              expect < uint64_t(plan->group_max) * b->rows;
     if (s.kind == MDSX_KIND_FIXED) {
-      if (!d.data) return mdsx::fail(MDSX_E_ARG, "mdsx: null data pointer for a fixed column");
+      if (!d.data && b->rows > 0)
+        return mdsx::fail(MDSX_E_ARG, "mdsx: null data pointer for a fixed column");
     } else {
       if (!d.offsets || (!d.data && d.capacity > 0))
         return mdsx::fail(MDSX_E_ARG, "mdsx: null offsets/data for a ragged column");
@@ -686,8 +813,12 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   for (int v = 0; v < plan->nvar; ++v) {  // gather workgroups of each ragged column, in order
     a->gather_block0[v] = gblocks;
     for (int c = 0; c < plan->ncols; ++c)
-      if (plan->cols[c].var_index == v && a->cols[c].gather)
-        gblocks += uint32_t((outs[c].capacity + tile - 1) / tile);
+      if (plan->cols[c].var_index == v && a->cols[c].gather) {
+        // every workgroup loops over the column's tiles with the column's grid as its stride
+        const uint64_t expect =
+            mode_bytes ? std::min(mode_bytes[c], outs[c].capacity) : outs[c].capacity;
+        gblocks += uint32_t(expect > tile ? (expect + tile - 1) / tile : 1);
+      }
   }
   a->gather_block0[plan->nvar] = gblocks;
   return MDSX_OK;
@@ -986,14 +1117,13 @@ int mdsx_scan_shards(const mdsx_plan* plan, const mdsx_batch* batch, const mdsx_
   return hip_check(hipGetLastError(), "scan_totals_kernel launch");
 }
 
-int mdsx_decode_shards(const mdsx_plan* plan, const mdsx_batch* batch,
-                       const mdsx_column_out* outs, void* d_workspace, uint64_t workspace_bytes,
-                       void* stream) {
-  DevArgs a;
-  int rc = build_args(plan, batch, outs, d_workspace, workspace_bytes, nullptr, &a);
-  if (rc != MDSX_OK) return rc;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  if (a.ntiles == 0) return MDSX_OK;
+}  // extern "C"
+
+// The decode kernel (single: with its own look-back scan) and, for gather columns, the
+// destination-major copy.
+static int launch_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s, bool single,
+                         const uint64_t* mode_bytes) {
+  int rc = MDSX_OK;
   const size_t lds =
       size_t(plan->tile_rows) * (12 * size_t(plan->nvar) + 4 * size_t(plan->ncols) + 1) + 16;
   const bool nt = plan->nontemporal != 0, ragged = plan->nvar > 0;
@@ -1004,20 +1134,23 @@ int mdsx_decode_shards(const mdsx_plan* plan, const mdsx_batch* batch,
     if (plan->cols[c].kind == MDSX_KIND_FIXED && plan->cols[c].row_bytes > kSmallMax &&
         plan->cols[c].row_bytes % 16 != 0)
       edges = true;
-#define MDSX_DECODE(U, NT, RG, ED) \
-  hipLaunchKernelGGL((decode_kernel<U, NT, RG, ED>), dim3(a.ntiles), dim3(kBlock), lds, s, a)
-#define MDSX_DECODE_U(U)                                  \
-  do {                                                    \
-    if (ragged) {                                         \
-      if (nt) MDSX_DECODE(U, true, true, true);           \
-      else MDSX_DECODE(U, false, true, true);             \
-    } else if (edges) {                                   \
-      if (nt) MDSX_DECODE(U, true, false, true);          \
-      else MDSX_DECODE(U, false, false, true);            \
-    } else {                                              \
-      if (nt) MDSX_DECODE(U, true, false, false);         \
-      else MDSX_DECODE(U, false, false, false);           \
-    }                                                     \
+#define MDSX_DECODE(U, NT, RG, ED, SG) \
+  hipLaunchKernelGGL((decode_kernel<U, NT, RG, ED, SG>), dim3(a.ntiles), dim3(kBlock), lds, s, a)
+#define MDSX_DECODE_U(U)                                                 \
+  do {                                                                   \
+    if (ragged && single) {                                              \
+      if (nt) MDSX_DECODE(U, true, true, true, true);                    \
+      else MDSX_DECODE(U, false, true, true, true);                      \
+    } else if (ragged) {                                                 \
+      if (nt) MDSX_DECODE(U, true, true, true, false);                   \
+      else MDSX_DECODE(U, false, true, true, false);                     \
+    } else if (edges) {                                                  \
+      if (nt) MDSX_DECODE(U, true, false, true, false);                  \
+      else MDSX_DECODE(U, false, false, true, false);                    \
+    } else {                                                             \
+      if (nt) MDSX_DECODE(U, true, false, false, false);                 \
+      else MDSX_DECODE(U, false, false, false, false);                   \
+    }                                                                    \
   } while (0)
   // 16-byte chunks per lane in flight in the whole-wave row copy: enough for the longest rows
   // copied that way, no more (every extra chunk costs registers, and waves per SIMD). Measured
@@ -1029,9 +1162,10 @@ int mdsx_decode_shards(const mdsx_plan* plan, const mdsx_batch* batch,
     for (int c = 0; c < plan->ncols; ++c) {
       const DevCol& d = a.cols[c];
       if (d.kind == MDSX_KIND_FIXED)
-        widest = max(widest, uint64_t(d.row_bytes > uint32_t(kSmallMax) ? d.row_bytes : 0));
+        widest = std::max(widest, uint64_t(d.row_bytes > uint32_t(kSmallMax) ? d.row_bytes : 0));
       else if (!d.gather && !d.group && a.rows)
-        widest = max(widest, d.capacity / a.rows);
+        widest = std::max(
+            widest, (mode_bytes ? std::min(mode_bytes[c], d.capacity) : d.capacity) / a.rows);
     }
     unroll = !ragged ? 4 : widest == 0 ? 2 : widest >= 2048 ? 6 : 4;
   }
@@ -1058,6 +1192,42 @@ int mdsx_decode_shards(const mdsx_plan* plan, const mdsx_batch* batch,
   return hip_check(hipGetLastError(), "gather_ragged_kernel launch");
 }
 
+
+extern "C" {
+
+int mdsx_decode_shards(const mdsx_plan* plan, const mdsx_batch* batch,
+                       const mdsx_column_out* outs, void* d_workspace, uint64_t workspace_bytes,
+                       void* stream) {
+  DevArgs a;
+  int rc = build_args(plan, batch, outs, d_workspace, workspace_bytes, nullptr, &a);
+  if (rc != MDSX_OK || a.ntiles == 0) return rc;
+  return launch_decode(plan, a, static_cast<hipStream_t>(stream), false, nullptr);
+}
+
+int mdsx_decode_shards_single(const mdsx_plan* plan, const mdsx_batch* batch,
+                              const mdsx_column_out* outs, const uint64_t* mode_bytes,
+                              void* d_workspace, uint64_t workspace_bytes, int64_t* d_totals,
+                              void* stream) {
+  DevArgs a;
+  int rc = build_args(plan, batch, outs, d_workspace, workspace_bytes, d_totals, &a, mode_bytes);
+  if (rc != MDSX_OK) return rc;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // status record + ticket (the first 256 bytes) and the look-back words, zeroed together
+  const uint64_t zero = 256 + round256(uint64_t(plan->nvar) * a.ntiles * 8);
+  rc = hip_check(hipMemsetAsync(d_workspace, 0, zero, s), "hipMemsetAsync");
+  if (rc != MDSX_OK) return rc;
+  if (a.ntiles == 0) {  // no rows: ragged offsets are the single 0
+    for (int c = 0; c < plan->ncols; ++c)
+      if (plan->cols[c].var_index >= 0 && outs[c].offsets) {
+        rc = hip_check(hipMemsetAsync(outs[c].offsets, 0, 8, s), "hipMemsetAsync");
+        if (rc != MDSX_OK) return rc;
+      }
+    if (d_totals && plan->nvar)
+      rc = hip_check(hipMemsetAsync(d_totals, 0, 8 * size_t(plan->nvar), s), "hipMemsetAsync");
+    return rc;
+  }
+  return launch_decode(plan, a, s, plan->nvar > 0, mode_bytes);
+}
 
 uint64_t mdsx_gather_workspace_bytes(uint64_t m) {
   const uint64_t tiles = (m + kGatherRowTile - 1) / kGatherRowTile;

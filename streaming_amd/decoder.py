@@ -429,16 +429,51 @@ def _status_error(status: _native.Status, plan: Plan) -> Exception:
     return RuntimeError(f'mdsx device error {code} ({where}).')
 
 
+class _PendingRagged(RaggedColumn):
+    """A ragged column of a single-pass decode: ``values`` is the output buffer cut to the
+    column's total, which is read back (one wait on the decode) the first time it is needed."""
+
+    def __init__(self, buf: torch.Tensor, offsets: torch.Tensor, flags: Optional[torch.Tensor],
+                 total) -> None:
+        self._buf, self._total, self._values = buf, total, None
+        self.offsets, self.flags = offsets, flags
+
+    @property
+    def values(self) -> torch.Tensor:
+        if self._values is None:
+            self._values = self._buf[:self._total()]
+        return self._values
+
+    @values.setter
+    def values(self, v: torch.Tensor) -> None:
+        self._values = v
+
+
+def payload_bound(plan: Plan, batch: DeviceBatch) -> int:
+    """Bytes any one ragged column of ``batch`` can hold at most: the sample bytes of its shards
+    less every sample's column-size heads and fixed columns (mds/writer.py:133-144 layout)."""
+    heads = sum(4 * (n + 2) for n in batch.samples)  # u32 count + N + 1 offsets
+    per_row = 4 * plan.num_var + plan.fixed_row_bytes()
+    return max(0, batch.shard_bytes - heads - per_row * batch.total_rows)
+
+
 class BatchDecoder:
     """Decode a :class:`DeviceBatch` on the device, reusing outputs across calls.
 
     ``run()`` enqueues the scan + decode kernels on the current torch stream with no host sync
     once the ragged capacities are known (first call, or given ``capacities``), so it can be
     timed / captured. ``check()`` synchronizes and raises the first kernel-reported error.
+
+    ``single=True`` runs ``mdsx_decode_shards_single`` instead: one decode launch that scans its
+    own ragged lengths (decoupled look-back), with ragged outputs allocated at their upper bound
+    (:func:`payload_bound`) unless ``capacities`` are given -- no host round trip at all, the
+    first call included. The exact ragged totals are read back only when a column's ``values``
+    is first used. Copy modes follow the previous call's totals (the bound split evenly before
+    any call has finished).
     """
 
     def __init__(self, plan: Plan, batch: DeviceBatch,
-                 capacities: Optional[dict[str, int]] = None) -> None:
+                 capacities: Optional[dict[str, int]] = None, single: bool = False) -> None:
         if plan.tile_rows != batch.tile_rows:
             raise ValueError('batch was staged for a different tile size')
         self.plan = plan
@@ -467,6 +502,18 @@ class BatchDecoder:
         self._capacities = dict(capacities or {})
         self._outs = (ColumnOut * max(len(plan.columns), 1))()
         self._sized = plan.num_var == 0
+        self.single = single
+        if single and plan.num_var:
+            bound = payload_bound(plan, batch)
+            if not capacities:
+                capacities = {c.name: bound for c in plan.columns if not c.is_fixed}
+            self._capacities = dict(capacities)
+            self._mode = (ctypes.c_uint64 * max(len(plan.columns), 1))()
+            for c in plan.columns:
+                self._mode[c.index] = 0 if c.is_fixed else bound // plan.num_var
+            self._host_totals = torch.zeros(plan.num_var, dtype=torch.int64, pin_memory=True)
+            self._totals_ready: Optional[torch.cuda.Event] = None
+            self._totals_valid = False
         if capacities:
             self._resize(capacities)
 
@@ -499,14 +546,52 @@ class BatchDecoder:
                                             self.workspace.data_ptr(), self.workspace.numel(),
                                             self.totals.data_ptr(), stream), 'mdsx_scan_shards')
 
+    def _run_single(self, stream: int, events) -> DecodedBatch:
+        if self._totals_ready is not None and self._totals_ready.query():
+            vi = 0  # the last finished call's totals pick this call's copy modes
+            for col in self.plan.columns:
+                if not col.is_fixed:
+                    self._mode[col.index] = int(self._host_totals[vi])
+                    vi += 1
+        if events is not None:
+            events[0].record()
+            events[1].record()
+        _check(
+            self.plan._lib.mdsx_decode_shards_single(self.plan.handle, ctypes.byref(self._abi),
+                                                     self._outs, self._mode,
+                                                     self.workspace.data_ptr(),
+                                                     self.workspace.numel(),
+                                                     self.totals.data_ptr(), stream),
+            'mdsx_decode_shards_single')
+        if events is not None:
+            events[2].record()
+        self._host_totals.copy_(self.totals[:self.plan.num_var], non_blocking=True)
+        self._totals_ready = torch.cuda.Event()
+        self._totals_ready.record()
+        self._totals_valid = False
+        return self.result()
+
+    def _single_total(self, vi: int, cap: int):
+        def total() -> int:
+            if self._totals_ready is None:
+                return 0
+            if not self._totals_valid:
+                self._totals_ready.synchronize()
+                self._totals_valid = True
+            return min(int(self._host_totals[vi]), cap)
+        return total
+
     def run(self, events: Optional[Sequence[torch.cuda.Event]] = None) -> DecodedBatch:
         """Enqueue the decode of the whole batch; returns the (device) decoded columns.
 
         ``events``: optional three CUDA events recorded on the stream before the scan pass,
-        between the scan and the decode kernel, and after the decode kernel (kernel timing).
+        between the scan and the decode kernel, and after the decode kernel (kernel timing; a
+        single-pass decode records the first two together).
         """
         stream = torch.cuda.current_stream(self.device).cuda_stream
         self._fill_outs()
+        if self.single and self.plan.num_var:
+            return self._run_single(stream, events)
         if events is not None:
             events[0].record()
         self._scan(stream)  # resets the status record; ragged plans: offsets + totals
@@ -533,9 +618,15 @@ class BatchDecoder:
 
     def result(self) -> DecodedBatch:
         cols: dict[str, Union[torch.Tensor, RaggedColumn]] = {}
+        single = self.single and self.plan.num_var
+        vi = 0
         for col in self.plan.columns:
             out = self.outputs[col.name]
-            if isinstance(out, RaggedColumn):
+            if isinstance(out, RaggedColumn) and single:
+                out = _PendingRagged(out.values, out.offsets, out.flags,
+                                     self._single_total(vi, int(out.values.numel())))
+                vi += 1
+            elif isinstance(out, RaggedColumn):
                 cap = self._capacities.get(col.name, 0)
                 out = RaggedColumn(out.values[:cap], out.offsets, out.flags)
             cols[col.name] = out
@@ -555,9 +646,11 @@ class BatchDecoder:
             raise _status_error(st, self.plan)
 
 
-def decode_batch(plan: Plan, batch: DeviceBatch, check: bool = True) -> DecodedBatch:
-    """Decode every shard of ``batch`` (scan + decode) and, by default, check the status."""
-    dec = BatchDecoder(plan, batch)
+def decode_batch(plan: Plan, batch: DeviceBatch, check: bool = True,
+                 single: bool = False) -> DecodedBatch:
+    """Decode every shard of ``batch`` (scan + decode, or ``single``: one look-back pass) and,
+    by default, check the status."""
+    dec = BatchDecoder(plan, batch, single=single)
     out = dec.run()
     if check:
         dec.check()
