@@ -15,14 +15,33 @@ int hip_check(hipError_t e, const char* what);
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+// Every byte these kernels touch outside LDS is device (global) memory. Accesses go through
+// address-space-1 pointers so they compile to global_* instructions: a flat_* access also counts
+// in lgkmcnt (every LDS wait then waits for the outstanding stores as well) and retires out of
+// order, which explicit vmcnt bookkeeping (the LDS-DMA ring) cannot tolerate.
+#define MDSX_G __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ MDSX_G T* gp(T* p) {
+  return (MDSX_G T*)p;
+}
+template <class T>
+__device__ __forceinline__ const MDSX_G T* gp(const T* p) {
+  return (const MDSX_G T*)p;
+}
+template <class T>
+__device__ __forceinline__ MDSX_G T* gp_at(uint64_t a) {
+  return (MDSX_G T*)a;
+}
+
 // 16-byte global load / store, optionally non-temporal (streamed once: no reuse in L2/MALL).
 template <bool kNT>
 __device__ __forceinline__ uint4 ld16(const uint4* p) {
   if constexpr (kNT) {
-    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    const u32x4 v = __builtin_nontemporal_load((const MDSX_G u32x4*)p);
     return make_uint4(v.x, v.y, v.z, v.w);
   } else {
-    return *p;
+    const u32x4 v = *(const MDSX_G u32x4*)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
   }
 }
 
@@ -30,9 +49,10 @@ template <bool kNT>
 __device__ __forceinline__ void st16(uint64_t addr, const uint4 v) {
   if constexpr (kNT) {
     const u32x4 w = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(addr));
+    __builtin_nontemporal_store(w, gp_at<u32x4>(addr));
   } else {
-    *reinterpret_cast<uint4*>(addr) = v;
+    const u32x4 w = {v.x, v.y, v.z, v.w};
+    *gp_at<u32x4>(addr) = w;
   }
 }
 
@@ -51,7 +71,7 @@ __device__ __forceinline__ void report(mdsx_status* st, int code, int shard, int
 // u32 at any byte address (reads the two aligned dwords that cover it).
 __device__ __forceinline__ uint32_t load_u32_any(const uint8_t* p) {
   const uint64_t a = reinterpret_cast<uint64_t>(p);
-  const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uint64_t(3));
+  const MDSX_G uint32_t* q = gp_at<const uint32_t>(a & ~uint64_t(3));
   return alignbyte(q[1], q[0], uint32_t(a & 3));
 }
 
@@ -179,7 +199,7 @@ __device__ __forceinline__ void wave_edge_store(const uint4 chunk, int le, uint6
   const uint64_t A = D + uint64_t(lane);
   if (lane < 16 && A >= d0 && A < dend) {
     const uint32_t w = lane < 4 ? w0 : lane < 8 ? w1 : lane < 12 ? w2 : w3;
-    *reinterpret_cast<uint8_t*>(A) = uint8_t(w >> (8 * (lane & 3)));
+    *gp_at<uint8_t>(A) = uint8_t(w >> (8 * (lane & 3)));
   }
 }
 
@@ -330,7 +350,7 @@ __device__ __forceinline__ void group_copy(const uint8_t* src, uint8_t* dst, uin
           const uint64_t A = E + uint64_t(gl);
           if (on && A >= d0 && A < dend) {
             const uint32_t w = gl < 4 ? w0 : gl < 8 ? w1 : gl < 12 ? w2 : w3;
-            *reinterpret_cast<uint8_t*>(A) = uint8_t(w >> (8 * (gl & 3)));
+            *gp_at<uint8_t>(A) = uint8_t(w >> (8 * (gl & 3)));
           }
         }
       }
@@ -360,7 +380,8 @@ __device__ __forceinline__ bool group_utf8_bad(const uint8_t* values, uint64_t o
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       const uint64_t k = base + uint64_t(u) * 16 + gl;
-      v[u] = k < nchunks ? *reinterpret_cast<const uint4*>(dbeg + 16 * k) : make_uint4(0, 0, 0, 0);
+      v[u] = k < nchunks ? ld16<false>(reinterpret_cast<const uint4*>(dbeg + 16 * k))
+                         : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
@@ -380,9 +401,10 @@ __device__ __forceinline__ bool group_utf8_bad(const uint8_t* values, uint64_t o
 
 // Fixed column of 1..16 bytes: one row per lane. dst is aligned to the largest power of two
 // dividing the row size (outputs are 256-byte aligned tensors).
-__device__ __forceinline__ void gather_small(const uint8_t* p, uint8_t* dst, uint32_t size) {
+__device__ __forceinline__ void gather_small(const uint8_t* p, uint8_t* dst_, uint32_t size) {
   const uint64_t a = reinterpret_cast<uint64_t>(p);
-  const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uint64_t(3));
+  const MDSX_G uint32_t* q = gp_at<const uint32_t>(a & ~uint64_t(3));
+  MDSX_G uint8_t* dst = gp(dst_);
   const uint32_t r = uint32_t(a & 3);
   const uint32_t nd = (size + 6) >> 2;  // dwords covering r + size bytes for any r <= 3
   const uint32_t w0 = q[0];
@@ -394,15 +416,18 @@ __device__ __forceinline__ void gather_small(const uint8_t* p, uint8_t* dst, uin
                              alignbyte(w4, w3, r));
   switch (size) {
     case 1: *dst = uint8_t(o.x); break;
-    case 2: *reinterpret_cast<uint16_t*>(dst) = uint16_t(o.x); break;
-    case 4: *reinterpret_cast<uint32_t*>(dst) = o.x; break;
-    case 8: *reinterpret_cast<uint2*>(dst) = make_uint2(o.x, o.y); break;
-    case 12:
-      reinterpret_cast<uint32_t*>(dst)[0] = o.x;
-      reinterpret_cast<uint32_t*>(dst)[1] = o.y;
-      reinterpret_cast<uint32_t*>(dst)[2] = o.z;
+    case 2: *(MDSX_G uint16_t*)dst = uint16_t(o.x); break;
+    case 4: *(MDSX_G uint32_t*)dst = o.x; break;
+    case 8:
+      ((MDSX_G uint32_t*)dst)[0] = o.x;
+      ((MDSX_G uint32_t*)dst)[1] = o.y;
       break;
-    case 16: *reinterpret_cast<uint4*>(dst) = o; break;
+    case 12:
+      ((MDSX_G uint32_t*)dst)[0] = o.x;
+      ((MDSX_G uint32_t*)dst)[1] = o.y;
+      ((MDSX_G uint32_t*)dst)[2] = o.z;
+      break;
+    case 16: *(MDSX_G u32x4*)dst = u32x4{o.x, o.y, o.z, o.w}; break;
     default:
       for (uint32_t j = 0; j < size; ++j) dst[j] = uint8_t(byte_of(o, int(j)));
   }

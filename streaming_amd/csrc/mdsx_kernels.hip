@@ -80,6 +80,8 @@ struct DevArgs {
   int32_t tile_rows;
   int16_t any_group;     // some ragged column uses group_copy
   int16_t any_wave_str;  // some str column is copied by decode_kernel (validated there)
+  int16_t any_wave_ragged;  // some ragged column is copied one row per wave
+  int16_t pad_;
   uint32_t gather_block0[MDSX_MAX_COLUMNS + 1];  // first gather workgroup of each ragged column
   DevCol cols[MDSX_MAX_COLUMNS];
 };
@@ -235,6 +237,172 @@ __global__ __launch_bounds__(kBlock) void scan_totals_kernel(const DevArgs a) {
 }
 
 
+// ---------------------------------------------------------------------------------------------
+// Long ragged rows through an LDS-DMA ring (kSlots > 0 in decode_kernel). Each wave streams its
+// rows' source bytes into a private ring of kSlots 1 KiB slots with global_load_lds_dwordx4 (no
+// VGPR destination, so the bytes in flight per CU are bounded by LDS, not by registers) running
+// up to kSlots KiB ahead of the copy, across row boundaries; the copy side reads each slot and
+// its successor back (lane k: chunks k and k + 1), realigns with v_alignbyte and writes aligned
+// 16-byte chunks. The DMA is issued from inline asm, so the compiler neither counts nor waits
+// for it: the ring waits with explicit `s_waitcnt vmcnt(n)`, n = the vector-memory operations
+// this wave issued after the slot's DMA (DMAs, and stores certain to issue; any other store
+// only makes the wait stricter). Only the issuing wave reads its slots, so its vmcnt orders the
+// reads (MI355X_MICROARCH.md: nothing else orders a ds_read behind a pending LDS-DMA).
+template <bool kNT>
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds) {
+  const uint32_t lds_dst = __builtin_amdgcn_readfirstlane(lds);  // wave-uniform by construction
+  uint32_t keep;
+  if constexpr (kNT)
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(lds_dst)
+        : "memory");
+  else
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(lds_dst)
+        : "memory");
+}
+
+// s_waitcnt vmcnt(m) for the largest listed m <= n (a smaller count only waits longer).
+__device__ __forceinline__ void wait_vm_at_most(uint32_t n) {
+  if (n >= 48) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+  else if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+  else if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (n >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if (n >= 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// One long-row job of a wave: row r of ragged column c, as aligned 16-byte chunks.
+struct RingJob {
+  const uint4* sal;  // first aligned source chunk
+  uint64_t dbeg, d0, dend;
+  uint32_t nchunks, nload, nslots, sh;
+  int r, c;  // c < 0: no more jobs
+};
+
+__device__ __forceinline__ bool ring_column(const DevCol& col) {
+  return col.var_index >= 0 && !col.gather && !col.group;
+}
+
+// Advance j to this wave's next (row, column) with bytes to copy (rows r, r + 4, ...).
+__device__ __forceinline__ void ring_next(const DevArgs& a, const DevCol* cols, const TileView& v,
+                                          int TR,
+                                          const uint32_t* s_src, const uint64_t* s_vdst,
+                                          const uint32_t* s_vlen, const uint8_t* s_ok,
+                                          RingJob& j) {
+  int r = j.r, c = j.c;
+  for (;;) {
+    if (r >= int(v.nrows)) {
+      j.c = -1;
+      return;
+    }
+    ++c;
+    while (c < a.ncols && !ring_column(cols[c])) ++c;
+    if (c >= a.ncols || !s_ok[r]) {
+      r += kBlock / 64;
+      c = -1;
+      continue;
+    }
+    const int vi = cols[c].var_index;
+    const uint32_t len = s_vlen[vi * TR + r];
+    if (len == 0) continue;
+    const uint64_t d0 = reinterpret_cast<uint64_t>(cols[c].data) + s_vdst[vi * TR + r];
+    const uint64_t dend = d0 + len;
+    const uint64_t dbeg = d0 & ~uint64_t(15);
+    const uint64_t sfirst =
+        reinterpret_cast<uint64_t>(v.shard + s_src[c * TR + r]) - (d0 - dbeg);
+    j.r = r;
+    j.c = c;
+    j.d0 = d0;
+    j.dend = dend;
+    j.dbeg = dbeg;
+    j.sh = uint32_t(sfirst & 15);
+    j.sal = reinterpret_cast<const uint4*>(sfirst & ~uint64_t(15));
+    j.nchunks = uint32_t((((dend + 15) & ~uint64_t(15)) - dbeg) >> 4);
+    j.nload = j.nchunks + (j.sh ? 1u : 0u);
+    j.nslots = (j.nload + 63) / 64;
+    return;
+  }
+}
+
+template <int kSlots, bool kNT>
+__device__ __forceinline__ void ring_copy(const DevArgs& a, const DevCol* cols, const TileView& v,
+                                          int TR,
+                                          const uint32_t* s_src, const uint64_t* s_vdst,
+                                          const uint32_t* s_vlen, const uint8_t* s_ok,
+                                          const uint4* ring, uint32_t ring_lds, int wave,
+                                          int lane) {
+  RingJob P, Q;  // producer (DMA) and consumer (copy) cursors, wave-uniform
+  P.r = wave;
+  P.c = -1;
+  ring_next(a, cols, v, TR, s_src, s_vdst, s_vlen, s_ok, P);
+  if (P.c < 0) return;
+  Q = P;
+  uint32_t p = 0;           // next slot of job P to load
+  uint32_t issued = 0, consumed = 0, ops = 0;
+  uint32_t op_at = 0;       // lane i: `ops` when ring slot i was loaded
+  auto pump = [&]() {
+    while (P.c >= 0 && issued - consumed < uint32_t(kSlots)) {
+      const uint32_t k = p * 64 + uint32_t(lane);
+      const uint32_t slot = issued % kSlots;
+      glds16<kNT>(P.sal + (k < P.nload ? k : 0u), ring_lds + slot * 1024u);
+      if (lane == int(slot)) op_at = ops;
+      ++ops;
+      ++issued;
+      if (++p == P.nslots) {
+        p = 0;
+        ring_next(a, cols, v, TR, s_src, s_vdst, s_vlen, s_ok, P);
+      }
+    }
+  };
+  pump();
+  while (Q.c >= 0) {
+    const bool head_partial = Q.dbeg < Q.d0 || Q.dbeg + 16 > Q.dend;
+    const bool tail_partial = Q.nchunks > 1 && (Q.dend & 15) != 0;
+    const uint32_t kf0 = Q.d0 > Q.dbeg ? 1u : 0u;            // full chunks: [kf0, kf1)
+    const uint32_t kf1 = uint32_t((Q.dend - Q.dbeg) >> 4);
+    for (uint32_t q = 0; q < Q.nslots; ++q) {
+      const uint32_t x = consumed % kSlots;
+      const uint32_t need = (Q.sh != 0 && q + 1 < Q.nslots) ? (consumed + 1) % kSlots : x;
+      wait_vm_at_most(ops - __builtin_amdgcn_readlane(op_at, need) - 1);
+      const uint32_t k0 = q * 64;
+      if (k0 < Q.nchunks) {  // wave-uniform: the slot holds output chunks
+        const uint32_t k = k0 + uint32_t(lane);
+        const uint4 lo = ring[x * 64 + lane];
+        uint4 out = lo;
+        if (Q.sh != 0) {
+          const uint4 hi = lane < 63 ? ring[x * 64 + lane + 1] : ring[need * 64];
+          out = funnel16(lo, hi, Q.sh);
+        }
+        const uint64_t D = Q.dbeg + 16ull * k;
+        if (k < Q.nchunks && D >= Q.d0 && D + 16 <= Q.dend) st16<kNT>(D, out);
+        if (max(kf0, k0) < min(kf1, k0 + 64)) ++ops;  // that store was issued
+        if (q == 0 && head_partial) wave_edge_store(out, 0, Q.dbeg, Q.d0, Q.dend, lane);
+        if (tail_partial && Q.nchunks - 1 >= k0 && Q.nchunks - 1 < k0 + 64)
+          wave_edge_store(out, int(Q.nchunks - 1 - k0), Q.dbeg + 16ull * (Q.nchunks - 1), Q.d0,
+                          Q.dend, lane);
+      }
+      ++consumed;
+      pump();
+    }
+    ring_next(a, cols, v, TR, s_src, s_vdst, s_vlen, s_ok, Q);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+
 // Look-back status word of one (ragged column, tile): flag in the top 2 bits (0 not yet
 // published, 1 the tile's own aggregate, 2 the inclusive prefix), a byte count below.
 constexpr uint64_t kLbAggregate = 1ull << 62, kLbInclusive = 2ull << 62;
@@ -249,7 +417,8 @@ typedef __attribute__((address_space(1))) uint64_t gu64;
 // aggregate per ragged column and finds its base by decoupled look-back over the earlier tiles'
 // status words. Flag and value share one 8-byte word written and read with agent-scope atomics,
 // so no fence orders them.
-template <int kUnroll, bool kNT, bool kRagged, bool kEdges, bool kSingle>
+// kSlots > 0: long ragged rows copied through the LDS-DMA ring (ring_copy) instead of wave_copy.
+template <int kUnroll, bool kNT, bool kRagged, bool kEdges, bool kSingle, int kSlots = 0>
 __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int TR = a.tile_rows;
@@ -263,12 +432,20 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
 
   const int t = threadIdx.x;
   const int lane = t & 63, wave = t >> 6;
+  // Ring variant: the column table in LDS. Indexed by a loop variable, kernel-argument fields
+  // compile to vector-memory loads, and the compiler waits for one with a vmcnt(0) that would
+  // also drain the ring's LDS-DMA in flight. (The register-copy variants keep reading the
+  // kernel arguments: measured faster on config B than the LDS table plus its barrier.)
+  __shared__ DevCol s_cols[kSlots > 0 ? MDSX_MAX_COLUMNS : 1];
+  const DevCol* const cols = kSlots > 0 ? s_cols : a.cols;
+  if constexpr (kSlots > 0)
+    for (int i = t; i < a.ncols; i += kBlock) s_cols[i] = a.cols[i];
   uint32_t tile = blockIdx.x;
   if constexpr (kSingle) {
     if (t == 0) s_tile = atomicAdd(a.ticket, 1u);
-    __syncthreads();
-    tile = s_tile;
   }
+  if constexpr (kSingle || kSlots > 0) __syncthreads();
+  if constexpr (kSingle) tile = s_tile;
   const TileView v = tile_view(a, tile);
 
   if (!v.table_ok) {
@@ -297,7 +474,7 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
     }
     uint64_t pos = uint64_t(b) + 4ull * a.nvar;
     for (int c = 0; c < a.ncols; ++c) {
-      const DevCol& col = a.cols[c];
+      const DevCol& col = cols[c];
       uint64_t len = col.row_bytes;
       if (col.var_index >= 0) {
         len = ok ? load_u32_any(v.shard + b + 4u * uint32_t(col.var_index)) : 0u;
@@ -380,7 +557,7 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
           s_base[vi] = int64_t(base);
           if (tile + 1 == a.ntiles) {  // the batch's last tile: column totals
             for (int c = 0; c < a.ncols; ++c)
-              if (a.cols[c].var_index == vi) a.cols[c].offsets[a.rows] = int64_t(base + agg);
+              if (cols[c].var_index == vi) cols[c].offsets[a.rows] = int64_t(base + agg);
             if (a.totals) a.totals[vi] = int64_t(base + agg);
           }
         }
@@ -397,7 +574,7 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
     const uint64_t row = v.d.row0 + i;
     bool ok = s_ok[t] != 0;
     for (int c = 0; c < a.ncols; ++c) {
-      const DevCol& col = a.cols[c];
+      const DevCol& col = cols[c];
       if (col.var_index < 0) continue;
       const int vi = col.var_index;
       int64_t off;
@@ -432,7 +609,7 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
   if (t < int(v.nrows) && s_ok[t]) {
     const uint64_t row = v.d.row0 + v.r0 + t;
     for (int c = 0; c < a.ncols; ++c) {
-      const DevCol& col = a.cols[c];
+      const DevCol& col = cols[c];
       if (col.var_index >= 0 || col.row_bytes > uint32_t(kSmallMax)) continue;
       gather_small(v.shard + s_src[c * TR + t],
                    static_cast<uint8_t*>(col.data) + row * col.row_bytes, col.row_bytes);
@@ -444,13 +621,13 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
     if (!s_ok[r]) continue;  // wave-uniform
     const uint64_t row = v.d.row0 + v.r0 + r;
     for (int c = 0; c < a.ncols; ++c) {
-      const DevCol& col = a.cols[c];
+      const DevCol& col = cols[c];
       const uint8_t* src = v.shard + s_src[c * TR + r];
       if (col.var_index < 0) {
         if (col.row_bytes <= uint32_t(kSmallMax)) continue;
         wave_copy<false, kUnroll, kNT, kEdges>(
             src, static_cast<uint8_t*>(col.data) + row * col.row_bytes, col.row_bytes, lane);
-      } else if (kRagged && !col.gather && !col.group) {
+      } else if (kRagged && kSlots == 0 && !col.gather && !col.group) {
         const int vi = col.var_index;
         uint8_t* dst = static_cast<uint8_t*>(col.data) + s_vdst[vi * TR + r];
         const uint64_t len = s_vlen[vi * TR + r];
@@ -458,6 +635,18 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
         // the copy loop costs the kernel a wave per SIMD: 125 vs 87 VGPRs)
         wave_copy<false, kUnroll, kNT>(src, dst, len, lane);
       }
+    }
+  }
+
+  if constexpr (kRagged && kSlots > 0) {
+    if (a.any_wave_ragged) {  // launch-uniform
+      const size_t head = (size_t(TR) * (12 * size_t(a.nvar) + 4 * size_t(a.ncols) + 1) + 15) &
+                          ~size_t(15);
+      const uint4* ring = reinterpret_cast<const uint4*>(smem + head) + wave * kSlots * 64;
+      const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(
+          reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const uint4*)ring)));
+      ring_copy<kSlots, kNT>(a, cols, v, TR, s_src, s_vdst, s_vlen, s_ok, ring, ring_lds,
+                             __builtin_amdgcn_readfirstlane(wave), lane);
     }
   }
 
@@ -469,7 +658,7 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
         const int r = min(r0 + g, int(v.nrows) - 1);
         const bool live = r0 + g < int(v.nrows) && s_ok[r];
         for (int c = 0; c < a.ncols; ++c) {
-          const DevCol& col = a.cols[c];
+          const DevCol& col = cols[c];
           if (!col.group) continue;
           const int vi = col.var_index;
           group_copy<kGroupUnroll, kNT>(v.shard + s_src[c * TR + r],
@@ -492,11 +681,12 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
       const int r = min(r0 + g, int(v.nrows) - 1);
       const bool live = r0 + g < int(v.nrows) && s_ok[r];
       for (int c = 0; c < a.ncols; ++c) {
-        const DevCol& col = a.cols[c];
+        const DevCol& col = cols[c];
         if (col.kind != MDSX_KIND_STR || !col.flags || col.gather) continue;
         const int vi = col.var_index;
         const uint64_t len = live ? s_vlen[vi * TR + r] : 0;
-        const bool bad = group_utf8_bad<2>(static_cast<const uint8_t*>(col.data),
+        // (the ring variant: 1 chunk per lane in flight, which keeps it at 72 VGPRs = 7 waves)
+        const bool bad = group_utf8_bad<(kSlots > 0 ? 1 : 2)>(static_cast<const uint8_t*>(col.data),
                                            s_vdst[vi * TR + r], len, lane);
         if ((lane & 15) == 0 && len && bad) col.flags[v.d.row0 + v.r0 + r] = 1;
       }
@@ -808,6 +998,7 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   for (int c = 0; c < plan->ncols; ++c) {
     const DevCol& d = a->cols[c];
     if (d.group) a->any_group = 1;
+    if (d.kind != MDSX_KIND_FIXED && !d.gather && !d.group) a->any_wave_ragged = 1;
     if (d.kind == MDSX_KIND_STR && d.flags && !d.gather) a->any_wave_str = 1;
   }
   for (int v = 0; v < plan->nvar; ++v) {  // gather workgroups of each ragged column, in order
@@ -875,14 +1066,14 @@ __global__ __launch_bounds__(kBlock) void gather_fixed_kernel(const uint8_t* src
       if (r < 0 || uint64_t(r) >= nsrc) {
         report(st, MDSX_E_BOUNDS, -1, int(k), -1);
       } else {
-        const uint8_t* p = src + uint64_t(r) * row_bytes;  // both rows aligned to row_bytes'
-        uint8_t* q = dst + k * row_bytes;                    // power-of-two factor
+        const MDSX_G uint8_t* p = gp(src + uint64_t(r) * row_bytes);  // both rows aligned to
+        MDSX_G uint8_t* q = gp(dst + k * row_bytes);  // row_bytes' power-of-two factor
         switch (row_bytes) {
           case 1: *q = *p; break;
-          case 2: *reinterpret_cast<uint16_t*>(q) = *reinterpret_cast<const uint16_t*>(p); break;
-          case 4: *reinterpret_cast<uint32_t*>(q) = *reinterpret_cast<const uint32_t*>(p); break;
-          case 8: *reinterpret_cast<uint2*>(q) = *reinterpret_cast<const uint2*>(p); break;
-          case 16: *reinterpret_cast<uint4*>(q) = *reinterpret_cast<const uint4*>(p); break;
+          case 2: *(MDSX_G uint16_t*)q = *(const MDSX_G uint16_t*)p; break;
+          case 4: *(MDSX_G uint32_t*)q = *(const MDSX_G uint32_t*)p; break;
+          case 8: *(MDSX_G uint64_t*)q = *(const MDSX_G uint64_t*)p; break;
+          case 16: *(MDSX_G u32x4*)q = *(const MDSX_G u32x4*)p; break;
           default:
             for (uint32_t j = 0; j < row_bytes; ++j) q[j] = p[j];
         }
@@ -1152,26 +1343,59 @@ static int launch_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s,
       else MDSX_DECODE(U, false, false, false, false);                   \
     }                                                                    \
   } while (0)
+#define MDSX_RING(U, K)                                                                    \
+  do {                                                                                     \
+    const size_t rl = ((lds + 15) & ~size_t(15)) + size_t(kBlock / 64) * (K)*1024;         \
+    if (single) {                                                                          \
+      if (nt)                                                                              \
+        hipLaunchKernelGGL((decode_kernel<U, true, true, true, true, K>), dim3(a.ntiles),  \
+                           dim3(kBlock), rl, s, a);                                        \
+      else                                                                                 \
+        hipLaunchKernelGGL((decode_kernel<U, false, true, true, true, K>), dim3(a.ntiles), \
+                           dim3(kBlock), rl, s, a);                                        \
+    } else {                                                                               \
+      if (nt)                                                                              \
+        hipLaunchKernelGGL((decode_kernel<U, true, true, true, false, K>), dim3(a.ntiles), \
+                           dim3(kBlock), rl, s, a);                                        \
+      else                                                                                 \
+        hipLaunchKernelGGL((decode_kernel<U, false, true, true, false, K>), dim3(a.ntiles), \
+                           dim3(kBlock), rl, s, a);                                        \
+    }                                                                                      \
+  } while (0)
   // 16-byte chunks per lane in flight in the whole-wave row copy: enough for the longest rows
   // copied that way, no more (every extra chunk costs registers, and waves per SIMD). Measured
   // on 32-row tiles: 4 KiB blobs + ~340-byte strings 4.30 TB/s at 6 vs 4.19 at 4; rows of a few
   // hundred bytes (all copied four per wave) 2.17 at 2 vs 1.99 at 4.
   int unroll = plan->unroll;
-  if (unroll == 0) {
-    uint64_t widest = 0;  // bytes per row of the widest column copied by whole waves
-    for (int c = 0; c < plan->ncols; ++c) {
-      const DevCol& d = a.cols[c];
-      if (d.kind == MDSX_KIND_FIXED)
-        widest = std::max(widest, uint64_t(d.row_bytes > uint32_t(kSmallMax) ? d.row_bytes : 0));
-      else if (!d.gather && !d.group && a.rows)
-        widest = std::max(
-            widest, (mode_bytes ? std::min(mode_bytes[c], d.capacity) : d.capacity) / a.rows);
+  uint64_t widest = 0, widest_fixed = 0;  // bytes per row of the widest column copied by waves
+  for (int c = 0; c < plan->ncols; ++c) {
+    const DevCol& d = a.cols[c];
+    if (d.kind == MDSX_KIND_FIXED) {
+      widest_fixed =
+          std::max(widest_fixed, uint64_t(d.row_bytes > uint32_t(kSmallMax) ? d.row_bytes : 0));
+    } else if (!d.gather && !d.group && a.rows) {
+      widest = std::max(
+          widest, (mode_bytes ? std::min(mode_bytes[c], d.capacity) : d.capacity) / a.rows);
     }
-    unroll = !ragged ? 4 : widest == 0 ? 2 : widest >= 2048 ? 6 : 4;
   }
-  if (unroll == 6) MDSX_DECODE_U(6);
-  else if (unroll == 2) MDSX_DECODE_U(2);
-  else MDSX_DECODE_U(4);
+  if (ragged && a.any_wave_ragged && plan->ring_slots > 0) {
+    // long ragged rows go through the LDS-DMA ring; the unroll serves large fixed columns only
+    const int u = unroll ? unroll : widest_fixed >= 2048 ? 4 : 2;
+    if (plan->ring_slots == 4) {
+      if (u == 2) MDSX_RING(2, 4); else MDSX_RING(4, 4);
+    } else if (plan->ring_slots == 6) {
+      if (u == 2) MDSX_RING(2, 6); else MDSX_RING(4, 6);
+    } else {
+      if (u == 2) MDSX_RING(2, 8); else MDSX_RING(4, 8);
+    }
+  } else {
+    widest = std::max(widest, widest_fixed);
+    if (unroll == 0) unroll = !ragged ? 4 : widest == 0 ? 2 : widest >= 2048 ? 6 : 4;
+    if (unroll == 6) MDSX_DECODE_U(6);
+    else if (unroll == 2) MDSX_DECODE_U(2);
+    else MDSX_DECODE_U(4);
+  }
+#undef MDSX_RING
 #undef MDSX_DECODE_U
 #undef MDSX_DECODE
   rc = hip_check(hipGetLastError(), "decode_kernel launch");

@@ -193,6 +193,8 @@ void apply_tuning(mdsx_plan* p) {
       p->gather_chunks = int(v);
     } else if (key == "nt") {
       p->nontemporal = v ? 1 : 0;
+    } else if (key == "ring" && (v == 0 || v == 4 || v == 6 || v == 8)) {
+      p->ring_slots = int(v);
     }
   }
 }
@@ -279,6 +281,10 @@ int mdsx_plan_create(const char* const* encodings, const int64_t* column_sizes, 
   // 4.12 vs 3.74 at 64).
   p->encode_tile_rows = 16;
   p->nontemporal = 1;  // shard bytes are read once and outputs written once: stream them
+  // Long ragged rows (one per wave) through a 4 KiB LDS-DMA ring per wave: config C 1.96 vs
+  // 2.13 ms from registers, 1-3 KiB blobs + 200-400-code-point strings 1.67 vs 1.89; 6 and 8
+  // slots lose the waves per CU their LDS costs (scripts/tune_decode.py, ring=0/4/6/8).
+  p->ring_slots = p->nvar > 0 ? 4 : 0;
   apply_tuning(p);
   *out = p;
   return MDSX_OK;

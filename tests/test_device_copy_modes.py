@@ -1,6 +1,7 @@
 """GPU parity of every ragged-column copy mode of the decoder, each forced through the
 measurement knobs (MDSX_TUNE, read at plan creation): destination-major gather kernel
-(short rows), four rows per wave in 16-lane groups (medium rows), one row per wave (long rows).
+(short rows), four rows per wave in 16-lane groups (medium rows), one row per wave (long rows),
+the last either from registers or through the per-wave LDS-DMA ring (8 or 4 slots).
 Whatever mode a column gets, the bytes, offsets and UTF-8 flags must equal the reference's.
 """
 
@@ -24,7 +25,9 @@ pytestmark = pytest.mark.gpu
 MODES = {
     'gather': 'gmin=1000000000',
     'group': 'gmin=0,gmax=1000000000',
-    'wave': 'gmin=0,gmax=0',
+    'wave': 'gmin=0,gmax=0,ring=0',
+    'ring': 'gmin=0,gmax=0,ring=8',   # one row per wave through the LDS-DMA ring
+    'ring4': 'gmin=0,gmax=0,ring=4',
 }
 
 
