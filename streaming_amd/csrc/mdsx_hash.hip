@@ -536,10 +536,6 @@ __device__ __forceinline__ uint64_t xxh3_chain(const HashArgs& a, int seg, int k
     else
       return S[b * 8];
   };
-  auto load = [&](uint64_t* t, uint64_t b) {
-#pragma unroll
-    for (int i = 0; i < kAhead; ++i) t[i] = ld(b + i);
-  };
   auto steps = [&](const uint64_t* t) {
 #pragma unroll
     for (int i = 0; i < kAhead; ++i) {

@@ -64,8 +64,8 @@ struct DevArgs {
   const mdsx_shard_desc* shards;
   const uint32_t* tile_shard;
   mdsx_status* status;
-  int64_t* tile_total;   // [nvar][ntiles]
-  int64_t* tile_prefix;  // [nvar][ntiles]
+  int64_t* tile_total;   // [nvar][nscan] ragged bytes of each scan block (scan_per tiles)
+  int64_t* tile_prefix;  // [nvar][nscan] their exclusive prefix
   int64_t* totals;       // [nvar] or null
   uint64_t* src_abs;     // [nvar][rows]  byte index into the batch of each row's ragged value
   uint32_t* row_map;     // [nvar][map_len] first row of every gather tile
@@ -74,6 +74,8 @@ struct DevArgs {
   uint64_t map_len;
   uint64_t rows;
   uint32_t ntiles;
+  uint32_t nscan;     // scan blocks: ceil(ntiles / scan_per)
+  uint32_t scan_per;  // tiles per scan block (kBlock / tile_rows)
   int32_t nshards;
   int32_t ncols;
   int32_t nvar;
@@ -148,13 +150,14 @@ __device__ __forceinline__ int64_t block_exclusive_scan(int64_t x, int64_t* s_ws
 }
 
 // ---------------------------------------------------------------------------------------------
-// Pass 1a: per-row ragged lengths -> local exclusive offsets + per-tile totals.
-// One workgroup covers 256 / tile_rows consecutive tiles (tile_rows <= 256, a power of two): one
-// thread per row; a block-wide exclusive scan, made tile-local by subtracting the value at each
-// tile's first thread.
+// Pass 1a: per-row ragged lengths -> block-local exclusive offsets + per-block totals.
+// One workgroup (a scan block) covers scan_per = 256 / tile_rows consecutive tiles (tile_rows <=
+// 256, a power of two): one thread per row, one block-wide exclusive scan. Tiles are in output
+// row order and a partial tile's missing rows count zero, so the scan is the output order; the
+// decode adds the scan block's prefix. Totals per scan block, not per tile, keep pass 1b an
+// eighth as long (32-row tiles).
 __global__ __launch_bounds__(kBlock) void scan_tiles_kernel(const DevArgs a) {
   __shared__ int64_t s_wsum[kBlock / 64];
-  __shared__ int64_t s_excl[kBlock];
   const int t = threadIdx.x;
   const int TR = a.tile_rows;
   const int per_block = kBlock / TR;
@@ -187,27 +190,22 @@ __global__ __launch_bounds__(kBlock) void scan_tiles_kernel(const DevArgs a) {
     const int64_t len = ok ? int64_t(load_u32_any(v.shard + b + 4u * uint32_t(vi))) : 0;
     int64_t total;
     const int64_t excl = block_exclusive_scan(len, s_wsum, &total);
-    s_excl[t] = excl;
-    __syncthreads();
-    const int first = t - tt;
-    const int64_t local = excl - s_excl[first];
-    if (in_tile) col.offsets[v.d.row0 + i] = local;
-    if (tt == TR - 1 && tile_ok) a.tile_total[uint64_t(vi) * a.ntiles + tile] = local + len;
-    __syncthreads();
+    if (in_tile) col.offsets[v.d.row0 + i] = excl;
+    if (t == 0) a.tile_total[uint64_t(vi) * a.nscan + blockIdx.x] = total;
   }
 }
 
-// Pass 1b: exclusive scan of the tile totals of one ragged column (one workgroup per column).
-// Thread t owns the contiguous run [t * per, (t + 1) * per) of tiles: it sums its run, one block
+// Pass 1b: exclusive scan of the scan-block totals of one ragged column (one workgroup per
+// column). Thread t owns the contiguous run [t * per, (t + 1) * per) of blocks: it sums its run, one block
 // scan of the 256 run sums gives every run its base, then each thread writes its run's prefixes
 // (one pass over the totals instead of ntiles / 256 dependent block scans).
 __global__ __launch_bounds__(kBlock) void scan_totals_kernel(const DevArgs a) {
   __shared__ int64_t s_wsum[kBlock / 64];
   const int vi = blockIdx.x;
-  const int64_t* in = a.tile_total + uint64_t(vi) * a.ntiles;
-  int64_t* out = a.tile_prefix + uint64_t(vi) * a.ntiles;
-  const uint32_t per = (a.ntiles + kBlock - 1) / kBlock;
-  const uint32_t lo = min(a.ntiles, threadIdx.x * per), hi = min(a.ntiles, lo + per);
+  const int64_t* in = a.tile_total + uint64_t(vi) * a.nscan;
+  int64_t* out = a.tile_prefix + uint64_t(vi) * a.nscan;
+  const uint32_t per = (a.nscan + kBlock - 1) / kBlock;
+  const uint32_t lo = min(a.nscan, threadIdx.x * per), hi = min(a.nscan, lo + per);
   constexpr uint32_t kBatch = 16;  // loads in flight per thread
   int64_t run = 0;
   for (uint32_t k0 = lo; k0 < hi; k0 += kBatch) {
@@ -580,8 +578,8 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
       int64_t off;
       if constexpr (kSingle)
         off = s_base[vi] + int64_t(s_vdst[vi * TR + t]);
-      else  // the scan pass left the tile-local offset in offsets[row]
-        off = a.tile_prefix[uint64_t(vi) * a.ntiles + tile] + col.offsets[row];
+      else  // the scan pass left the scan-block-local offset in offsets[row]
+        off = a.tile_prefix[uint64_t(vi) * a.nscan + tile / a.scan_per] + col.offsets[row];
       col.offsets[row] = off;
       s_vdst[vi * TR + t] = uint64_t(off);
       if (col.flags) col.flags[row] = 0;
@@ -963,6 +961,8 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   a->totals = d_totals;
   a->rows = b->rows;
   a->ntiles = b->ntiles;
+  a->scan_per = plan->tile_rows > 0 && plan->tile_rows <= kBlock ? uint32_t(kBlock / plan->tile_rows) : 1u;
+  a->nscan = (b->ntiles + a->scan_per - 1) / a->scan_per;
   a->nshards = b->nshards;
   a->ncols = plan->ncols;
   a->nvar = plan->nvar;
@@ -1298,9 +1298,7 @@ int mdsx_scan_shards(const mdsx_plan* plan, const mdsx_batch* batch, const mdsx_
   rc = hip_check(hipMemsetAsync(d_workspace, 0, sizeof(mdsx_status), s), "hipMemsetAsync");
   if (rc != MDSX_OK || plan->nvar == 0) return rc;
   if (a.ntiles > 0) {
-    const uint32_t per_block = uint32_t(kBlock / plan->tile_rows);
-    hipLaunchKernelGGL(scan_tiles_kernel, dim3((a.ntiles + per_block - 1) / per_block),
-                       dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(scan_tiles_kernel, dim3(a.nscan), dim3(kBlock), 0, s, a);
     rc = hip_check(hipGetLastError(), "scan_tiles_kernel launch");
     if (rc != MDSX_OK) return rc;
   }
