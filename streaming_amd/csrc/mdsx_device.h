@@ -75,6 +75,37 @@ __device__ __forceinline__ uint32_t load_u32_any(const uint8_t* p) {
   return alignbyte(q[1], q[0], uint32_t(a & 3));
 }
 
+// The u32 size heads of a sample (MDSReader.decode_sample, mds/reader.py:111-116) at p, any byte
+// alignment, up to kHeadRegs of them held in registers: one or two dword-aligned 16-byte loads
+// per row instead of two dword loads per head (per-row memory requests bound the scan pass).
+// Reads up to 31 bytes past the heads: inside the sample or the batch's 256-byte slack.
+constexpr int kHeadRegs = 7;
+typedef unsigned int u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+struct Heads {
+  uint32_t w[8];
+  uint32_t sh;
+  __device__ __forceinline__ void load(const uint8_t* p, int n) {
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const MDSX_G u32x4a4* q = gp_at<const u32x4a4>(a & ~uint64_t(3));
+    sh = uint32_t(a & 3);
+    const u32x4a4 x = q[0];
+    w[0] = x.x, w[1] = x.y, w[2] = x.z, w[3] = x.w;
+    if (4 * n + int(sh) > 16) {
+      const u32x4a4 y = q[1];
+      w[4] = y.x, w[5] = y.y, w[6] = y.z, w[7] = y.w;
+    } else {
+      w[4] = w[5] = w[6] = w[7] = 0;
+    }
+  }
+  // Head k (< kHeadRegs; k may differ per lane only through the select chain, no indexing).
+  __device__ __forceinline__ uint32_t get(int k) const {
+    uint32_t r = 0;
+#pragma unroll
+    for (int j = 0; j < kHeadRegs; ++j) r = k == j ? alignbyte(w[j + 1], w[j], sh) : r;
+    return r;
+  }
+};
+
 // ---------------------------------------------------------------------------------------------
 // Realignment: bytes [sh, sh + 16) of the 32-byte pair (lo, hi). sh is wave-uniform.
 __device__ __forceinline__ uint4 funnel16(const uint4 lo, const uint4 hi, uint32_t sh) {

@@ -173,21 +173,26 @@ __global__ __launch_bounds__(kBlock) void scan_tiles_kernel(const DevArgs a) {
   if (in_tile) {
     const int rc = sample_range(v, i, &b, &e);
     ok = rc == MDSX_OK && uint64_t(b) + 4ull * a.nvar <= e;
-    if (ok) {  // the whole sample must hold its heads and columns; else emit zero lengths
-      uint64_t need = 4ull * a.nvar;
-      for (int c = 0; c < a.ncols; ++c) {
-        const DevCol& col = a.cols[c];
-        need += col.var_index >= 0 ? load_u32_any(v.shard + b + 4u * uint32_t(col.var_index))
-                                   : col.row_bytes;
-      }
-      ok = uint64_t(b) + need <= e;
+  }
+  const bool few = a.nvar <= kHeadRegs;  // heads in registers (else re-read per column)
+  Heads h;
+  if (ok && few) h.load(v.shard + b, a.nvar);
+  auto head = [&](int vi) -> uint32_t {
+    return few ? h.get(vi) : load_u32_any(v.shard + b + 4u * uint32_t(vi));
+  };
+  if (ok) {  // the whole sample must hold its heads and columns; else emit zero lengths
+    uint64_t need = 4ull * a.nvar;
+    for (int c = 0; c < a.ncols; ++c) {
+      const DevCol& col = a.cols[c];
+      need += col.var_index >= 0 ? head(col.var_index) : col.row_bytes;
     }
+    ok = uint64_t(b) + need <= e;
   }
   for (int c = 0; c < a.ncols; ++c) {
     const DevCol& col = a.cols[c];
     if (col.var_index < 0) continue;
     const int vi = col.var_index;
-    const int64_t len = ok ? int64_t(load_u32_any(v.shard + b + 4u * uint32_t(vi))) : 0;
+    const int64_t len = ok ? int64_t(head(vi)) : 0;
     int64_t total;
     const int64_t excl = block_exclusive_scan(len, s_wsum, &total);
     if (in_tile) col.offsets[v.d.row0 + i] = excl;
@@ -471,11 +476,15 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
       rc = MDSX_E_BOUNDS;
     }
     uint64_t pos = uint64_t(b) + 4ull * a.nvar;
+    const bool few = a.nvar <= kHeadRegs;
+    Heads h;
+    if (kRagged && ok && few) h.load(v.shard + b, a.nvar);
     for (int c = 0; c < a.ncols; ++c) {
       const DevCol& col = cols[c];
       uint64_t len = col.row_bytes;
       if (col.var_index >= 0) {
-        len = ok ? load_u32_any(v.shard + b + 4u * uint32_t(col.var_index)) : 0u;
+        const int vi = col.var_index;
+        len = !ok ? 0u : few ? h.get(vi) : load_u32_any(v.shard + b + 4u * uint32_t(vi));
         s_vlen[col.var_index * TR + t] = uint32_t(len);
       }
       s_src[c * TR + t] = uint32_t(pos);
