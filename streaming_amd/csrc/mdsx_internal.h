@@ -40,6 +40,7 @@ struct mdsx_plan {
   int unroll = 0;       // 16-byte chunks per lane in flight in the row copy (2, 4 or 6); 0 =
                         // chosen per launch from the row sizes (mdsx_decode_shards)
   int nontemporal = 0;  // non-temporal loads/stores in the row copy
+  int str_cached = 0;   // medium str rows stored temporally (the UTF-8 re-read then hits L2)
   int ring_slots = 0;   // long ragged rows through a per-wave LDS-DMA ring of this many KiB (0: off)
   int gather_chunks = 2;  // 16-byte chunks per lane in the ragged gather (tile = 4 KiB x this)
   int gather_min = 256;   // ragged columns averaging fewer bytes per row use the gather kernel

@@ -83,7 +83,7 @@ struct DevArgs {
   int16_t any_group;     // some ragged column uses group_copy
   int16_t any_wave_str;  // some str column is copied by decode_kernel (validated there)
   int16_t any_wave_ragged;  // some ragged column is copied one row per wave
-  int16_t pad_;
+  int16_t str_cached;  // plan->str_cached
   uint32_t gather_block0[MDSX_MAX_COLUMNS + 1];  // first gather workgroup of each ragged column
   DevCol cols[MDSX_MAX_COLUMNS];
 };
@@ -668,10 +668,13 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
           const DevCol& col = cols[c];
           if (!col.group) continue;
           const int vi = col.var_index;
-          group_copy<kGroupUnroll, kNT>(v.shard + s_src[c * TR + r],
-                                               static_cast<uint8_t*>(col.data) +
-                                                   s_vdst[vi * TR + r],
-                                               live ? s_vlen[vi * TR + r] : 0, lane);
+          const uint8_t* src = v.shard + s_src[c * TR + r];
+          uint8_t* dst = static_cast<uint8_t*>(col.data) + s_vdst[vi * TR + r];
+          const uint32_t len = live ? s_vlen[vi * TR + r] : 0;
+          if (a.str_cached && col.kind == MDSX_KIND_STR)  // re-read below for the UTF-8 check
+            group_copy<kGroupUnroll, false>(src, dst, len, lane);
+          else
+            group_copy<kGroupUnroll, kNT>(src, dst, len, lane);
         }
       }
     }
@@ -1009,6 +1012,7 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
     if (d.group) a->any_group = 1;
     if (d.kind != MDSX_KIND_FIXED && !d.gather && !d.group) a->any_wave_ragged = 1;
     if (d.kind == MDSX_KIND_STR && d.flags && !d.gather) a->any_wave_str = 1;
+    a->str_cached = int16_t(plan->str_cached);
   }
   for (int v = 0; v < plan->nvar; ++v) {  // gather workgroups of each ragged column, in order
     a->gather_block0[v] = gblocks;

@@ -193,6 +193,8 @@ void apply_tuning(mdsx_plan* p) {
       p->gather_chunks = int(v);
     } else if (key == "nt") {
       p->nontemporal = v ? 1 : 0;
+    } else if (key == "strc") {
+      p->str_cached = v ? 1 : 0;
     } else if (key == "ring" && (v == 0 || v == 4 || v == 6 || v == 8)) {
       p->ring_slots = int(v);
     }
@@ -285,6 +287,10 @@ int mdsx_plan_create(const char* const* encodings, const int64_t* column_sizes, 
   // 2.13 ms from registers, 1-3 KiB blobs + 200-400-code-point strings 1.67 vs 1.89; 6 and 8
   // slots lose the waves per CU their LDS costs (scripts/tune_decode.py, ring=0/4/6/8).
   p->ring_slots = p->nvar > 0 ? 4 : 0;
+  // Medium str rows written with temporal stores, so the UTF-8 check's re-read of the packed
+  // output hits L2 instead of HBM: config C 1.94-2.01 vs 2.06-2.10 ms; 1-3 KiB blobs + 200-400-
+  // code-point strings 1.51 vs 1.56 ms (tune/strc_*.json).
+  p->str_cached = 1;
   apply_tuning(p);
   *out = p;
   return MDSX_OK;

@@ -25,6 +25,7 @@ pytestmark = pytest.mark.gpu
 MODES = {
     'gather': 'gmin=1000000000',
     'group': 'gmin=0,gmax=1000000000',
+    'group_nt': 'gmin=0,gmax=1000000000,strc=0',  # str rows streamed (non-temporal) too
     'wave': 'gmin=0,gmax=0,ring=0',
     'ring': 'gmin=0,gmax=0,ring=8',   # one row per wave through the LDS-DMA ring
     'ring4': 'gmin=0,gmax=0,ring=4',
