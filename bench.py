@@ -4,24 +4,39 @@ One step = one decode of the rank's whole HBM-resident shard batch through libmd
 (``mdsx_scan_shards`` + ``mdsx_decode_shards``): offsets-table scan, per-sample byte-range gather
 and per-column decode of every sample of every shard, outputs materialised as torch tensors.
 
-Default workload (N=1): BASELINE.json configs[1] = config B, 1M samples of
-``{id: int32, x: ndarray:float32:1024}`` in 62 x 64 MiB shards. With
-``--gpus N`` under torch.distributed.run every rank owns its own 1M-sample shard set
-(per-GPU shard ownership, no collectives on the data path: weak scaling); the only
-collectives are the timing barrier and the max-over-ranks reduction outside the timed region.
+Workloads (synthetic shards built on the device, bit-identical to the reference
+writer's layout, verified against their sources before and after the timed region):
 
-Prints ONE JSON line (rank 0) with the metric, a ``roofline`` object for the decode kernel
-(algorithmic bytes R+W per launch / HIP-event kernel time, vs the 8 TB/s HBM3E peak) and a
-``cpu_baseline`` object: the oracle's per-sample reader (a port of the reference algorithm,
-oracle/mds_oracle.py) timed on 16 host cores (one process each, 2 s: ~32 s of CPU work) over a
-bounded sample of the same workload.
+* config B (the headline line): ``{id: int32, x: ndarray:float32:1024}``, 62 full 64 MiB shards
+  (1 013 824 samples) per GPU;
+* config C (the ``config_c`` object of the same line): ``{n: int, b: bytes U[3072,5120], s: str}``,
+  64 full 64 MiB shards (~1M samples) per GPU, written by the device MDS encoder.
+
+Multi-GPU: the dataset is ``N x shards_per_gpu`` global shards; global shard ``g``
+is generated from seed ``base + g`` and owned by rank ``g % N`` (``streaming_amd.distributed.
+owned_shards``): weak scaling, no collective on the data path. ``python bench.py --gpus N``
+starts N child processes itself (one per GPU, ``RANK`` / ``LOCAL_RANK`` / ``WORLD_SIZE`` /
+``MASTER_*`` as ``torch.distributed.run`` sets them, the reference's env contract,
+``streaming/base/distributed.py:23-56``) before anything touches the GPU; under
+``torch.distributed.run`` it runs as the given rank. A world size different from ``--gpus`` is an
+error. Only the timing barriers and the max-over-ranks reduction are collectives.
+
+Rank 0 prints ONE JSON line with the metric, a ``roofline`` object per config (algorithmic bytes
+R+W per launch / HIP-event kernel time on the launch stream, vs the 8 TB/s HBM3E peak and the
+6.29 TB/s float4 copy the microarchitecture guide records; ``traffic`` from a committed
+rocprofv3 PMC summary of the SAME workload and kernel, else null) and a ``cpu_baseline`` object
+per config: the reference reader restated with its per-call coder construction
+(``oracle/mds_oracle.py``, kind "port") timed on host cores, 1 core and all cores of the box's share.
 """
 
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import tempfile
 import time
@@ -33,40 +48,91 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 METRIC = 'decoded samples/sec + MDS GiB/s, device-resident, at 1/2/4/8 MI355X'
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 measured copy)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+COPY_MEASURED_GBS = 6290.0  # MI355X_MICROARCH.md: float4 copy measured on MI355X
+SEED_B, SEED_C = 1000, 2000
+SHARDS_PER_GPU = {'B': 62, 'C': 64}
 
 
-def parse_args():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--config', choices=['B', 'C'], default='B')
-    ap.add_argument('--samples', type=int, default=1_000_000, help='samples per GPU')
+    ap.add_argument('--config', choices=['B', 'C', 'BC'], default='BC',
+                    help='B = headline line only; BC = B plus the config_c object')
+    ap.add_argument('--shards', type=int, default=0,
+                    help='shards per GPU (0: 62 for B, 64 for C = ~1M samples)')
     ap.add_argument('--cpu-seconds', type=float, default=2.0,
-                    help='CPU baseline time budget (0 disables)')
-    ap.add_argument('--cpu-procs', type=int, default=16,
-                    help='CPU baseline processes (disjoint shard copies, one per core; 16 = the '
-                         'host-core share of one GPU on the MI355X boxes)')
+                    help='CPU baseline seconds per leg (0 disables)')
+    ap.add_argument('--cpu-procs', type=int, default=0,
+                    help='all-core CPU leg processes (0: the box share, see cpu_cores())')
     ap.add_argument('--single', action='store_true',
                     help='ragged configs: single-pass decode (look-back scan inside the decode '
-                    'kernel, outputs at the payload bound) instead of scan + decode')
+                    'kernel) instead of scan + decode')
     ap.add_argument('--no-verify', action='store_true')
     ap.add_argument('--no-copy-probe', dest='copy_probe', action='store_false',
                     help='skip the same-run copy-ceiling measurement')
-    return ap.parse_args()
+    ap.add_argument('--dry-run', action='store_true',
+                    help='no GPU: exercise the launcher, process group (gloo) and shard '
+                    'ownership only (CPU test hook)')
+    return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------------------------
+# launcher: N fresh child processes, started before any GPU call of this process
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def launch(args, argv) -> int:
+    """Run ``bench.py`` as ``--gpus`` ranks (one child process per GPU) and return the exit code
+    (the first failing rank's, else 0). Rank 0's stdout is the benchmark line."""
+    port = _free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR='127.0.0.1',
+                   MASTER_PORT=str(port))
+        env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                                      env=env, stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in procs:  # one rank failed: the others would wait in a collective
+                    q.kill()
+        time.sleep(0.05)
+    return rc
 
 
 def init_dist(args):
     from streaming_amd.distributed import rank_info
     info = rank_info()
     world, rank, local = info.world_size, info.rank, info.local_rank
+    if world != args.gpus:
+        raise SystemExit(f'bench.py: --gpus {args.gpus} but WORLD_SIZE={world}')
+    if args.dry_run:
+        if world > 1:
+            torch.distributed.init_process_group('gloo')
+        return world, rank, local, torch.device('cpu')
+    if torch.cuda.device_count() < local + 1:
+        raise SystemExit(f'bench.py: rank {rank} needs GPU {local}, '
+                         f'{torch.cuda.device_count()} visible')
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
     if world > 1:
-        torch.cuda.set_device(local)
-        torch.distributed.init_process_group('nccl', device_id=torch.device('cuda', local))
-    else:
-        torch.cuda.set_device(0)
-    return world, rank, local
+        torch.distributed.init_process_group('nccl', device_id=dev)
+    return world, rank, local, dev
 
 
 def barrier(world):
@@ -74,67 +140,79 @@ def barrier(world):
         torch.distributed.barrier()
 
 
-def build_workload(args, rank, world):
-    """Shards this rank owns, resident in HBM, plus what to verify them against."""
-    from streaming_amd.synth import fixed_b_batch_on_device, var_c_shards
-    from streaming_amd.decoder import Plan, stage_shards
-    if args.config == 'B':
-        synth = fixed_b_batch_on_device(args.samples, seed=1000 + rank,
-                                        first_id=rank * args.samples)
-        workload = (f'B: {args.samples} samples/GPU {{id:int32, x:ndarray:float32:1024}}, '
-                    f'{len(synth.samples_per_shard)} x 64 MiB shards/GPU, HBM-resident')
-        return synth.plan, synth.batch, synth.sources, workload
-    shards, counts, src = var_c_shards(args.samples, seed=2000 + rank)
-    plan = Plan(['b', 'n', 's'], ['bytes', 'int', 'str'], [None, 8, None])
-    batch = stage_shards(shards, counts, plan)
-    workload = (f'C: {args.samples} samples/GPU {{n:int, b:bytes U[3072,5120], s:str U[16,256] '
-                f'cp}}, {len(counts)} x 64 MiB shards/GPU, HBM-resident')
-    return plan, batch, src, workload
+def gather_objects(world, obj):
+    if world == 1:
+        return [obj]
+    out = [None] * world
+    torch.distributed.all_gather_object(out, obj)
+    return out
 
 
-def verify(args, plan, out, sources):
-    if args.config == 'B':
+# ---------------------------------------------------------------------------------------------
+# workloads
+def shard_plan(args, config, rank, world):
+    from streaming_amd.distributed import owned_shards
+    per_gpu = args.shards or SHARDS_PER_GPU[config]
+    total = per_gpu * world
+    return owned_shards(total, rank, world), total
+
+
+def build_workload(config, shard_ids):
+    """This rank's shards (global ids ``shard_ids``) resident in HBM + their source columns."""
+    from streaming_amd.synth import fixed_b_batch_on_device, var_c_batch_on_device
+    if config == 'B':
+        synth = fixed_b_batch_on_device(0, seed=SEED_B, shard_ids=shard_ids)
+        desc = (f'B: {{id:int32, x:ndarray:float32:1024}}, {len(shard_ids)} full 64 MiB '
+                f'shards/GPU ({synth.batch.total_rows} samples), HBM-resident')
+    else:
+        synth = var_c_batch_on_device(shard_ids, seed=SEED_C)
+        desc = (f'C: {{n:int, b:bytes U[3072,5120], s:str U[16,256] code points of 1-4 UTF-8 '
+                f'bytes}}, {len(shard_ids)} full 64 MiB shards/GPU ({synth.batch.total_rows} '
+                f'samples), HBM-resident')
+    return synth, desc
+
+
+def verify(config, out, sources):
+    if config == 'B':
         ok = torch.equal(out['id'], sources['id']) and torch.equal(
             out['x'].view(torch.int32), sources['x'].view(torch.int32))
     else:
-        ok = np.array_equal(out['n'].cpu().numpy(), sources['n'])
-        ok &= np.array_equal(out['b'].values.cpu().numpy(), sources['b_pool'])
-        ok &= np.array_equal(out['s'].values.cpu().numpy(), sources['s_pool'])
+        ok = torch.equal(out['n'], sources['n'])
+        for name in ('b', 's'):
+            ok &= torch.equal(out[name].offsets - out[name].offsets[0],
+                              sources[name].offsets - sources[name].offsets[0])
+            ok &= torch.equal(out[name].values, sources[name].values)
         ok &= int(out['s'].flags.sum()) == 0
     if not ok:
-        raise SystemExit('PARITY FAILURE: decoded columns differ from the encoded sources')
+        raise SystemExit(f'PARITY FAILURE: config {config} decoded columns differ from the '
+                         f'encoded sources')
 
 
-def _cpu_shard(config, seed):
-    """One 64 MiB shard of the workload written to a temp dir (oracle reader input)."""
-    from streaming_amd.synth import var_c_shards
-    from streaming_amd.writer import encode_fixed_shard, shard_config_bytes
-    if config == 'B':
-        n = 16352
-        names, encs, sizes = ['id', 'x'], ['int32', 'ndarray:float32:1024'], [4, 4096]
-        cfg = shard_config_bytes(names, encs, sizes, None, [], 1 << 26)
-        rng = np.random.default_rng(seed)
-        raw = encode_fixed_shard(cfg, [np.arange(n, dtype=np.int32),
-                                       rng.integers(0, 2**32, (n, 1024), dtype=np.uint32)])
-    else:
-        shards, counts, _ = var_c_shards(16000, seed=seed)
-        raw, n = shards[0], counts[0]
-        names, encs, sizes = ['b', 'n', 's'], ['bytes', 'int', 'str'], [None, 8, None]
-    return raw, n, names, encs, sizes
+def workload_key(config, batch, W):
+    """What a committed PMC summary must match to be this run's traffic evidence."""
+    return f'{config}:shards={batch.nshards}:rows={batch.total_rows}:R={batch.shard_bytes}:W={W}'
 
 
-def _cpu_worker(config, seed, seconds, q):
-    """Oracle per-sample reader loop over one shard for `seconds` (one process = one core)."""
-    from oracle.mds_oracle import OracleMDSReader
-    raw, n, names, encs, sizes = _cpu_shard(config, seed)
-    tmp = tempfile.mkdtemp(prefix='mdsx_cpu_')
-    path = os.path.join(tmp, 'shard.00000.mds')
-    with open(path, 'wb') as f:
-        f.write(raw)
-    info = {'raw_data': {'basename': 'shard.00000.mds'}, 'column_names': names,
+# ---------------------------------------------------------------------------------------------
+# CPU baseline: the reference reader restated (oracle, per-call coder construction), host cores
+def cpu_cores():
+    """Processes for the all-core leg: the CPUs this process may run on
+    (``len(os.sched_getaffinity(0))``), capped by the box's CPU share
+    (``OMP_NUM_THREADS``, 16 per GPU on the MI355X boxes) -- returns (used, affinity, share)."""
+    aff = len(os.sched_getaffinity(0))
+    share = int(os.environ.get('OMP_NUM_THREADS', '0') or 0)
+    return (min(aff, share) if share > 0 else aff), aff, share
+
+
+def _cpu_worker(path, n, names, encs, sizes, seconds, q):
+    """Per-sample reader loop over one shard file for ``seconds`` (one process = one core)."""
+    from oracle.mds_oracle import ReferenceCostMDSReader
+    info = {'raw_data': {'basename': os.path.basename(path)}, 'column_names': names,
             'column_encodings': encs, 'column_sizes': sizes, 'samples': n}
-    reader = OracleMDSReader(tmp, None, info)
-    offs = np.frombuffer(raw[4:4 + 4 * (n + 1)], np.uint32).astype(np.int64)
+    reader = ReferenceCostMDSReader(os.path.dirname(path), None, info)
+    with open(path, 'rb') as f:
+        raw = f.read(4 + 4 * (n + 1))
+    offs = np.frombuffer(raw[4:], np.uint32).astype(np.int64)
     row_bytes = np.diff(offs).tolist()
     for i in range(min(n, 256)):  # warm the page cache and the interpreter
         reader.get_item(i)
@@ -147,61 +225,87 @@ def _cpu_worker(config, seed, seconds, q):
         i = i + 1 if i + 1 < n else 0
         if (done & 255) == 0 and time.perf_counter() - t0 >= seconds:
             break
-    dt = time.perf_counter() - t0
-    os.remove(path)
-    os.rmdir(tmp)
-    q.put((done, nbytes, dt))
+    q.put((done, nbytes, time.perf_counter() - t0))
 
 
-def cpu_baseline(args):
-    """The reference algorithm (oracle port) timed on host cores: `--cpu-procs` processes, each
-    looping the per-sample reader over its own shard; aggregate samples/s."""
+def _cpu_leg(files, meta, procs, seconds):
     import multiprocessing as mp
-    procs = max(1, args.cpu_procs)
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    ps = [ctx.Process(target=_cpu_worker, args=(args.config, 7 + k, args.cpu_seconds, q))
+    ps = [ctx.Process(target=_cpu_worker, args=(*files[k % len(files)], *meta, seconds, q))
           for k in range(procs)]
     for p in ps:
         p.start()
-    res = [q.get() for _ in ps]
+    res = [q.get(timeout=seconds + 300) for _ in ps]
     for p in ps:
         p.join()
     done = sum(r[0] for r in res)
     nbytes = sum(r[1] for r in res)
     dt = max(r[2] for r in res)
+    return done / dt, nbytes / dt / 2**30, done, dt
+
+
+def cpu_baseline(args, config, synth, tmpdir):
+    """1-core and all-core legs over shard files copied from this rank's device workload."""
+    used, aff, share = cpu_cores()
+    procs = args.cpu_procs or used
+    batch, plan = synth.batch, synth.plan
+    nfiles = min(batch.nshards, max(procs, 1))
+    files = []
+    for s in range(nfiles):
+        o = batch.offsets[s]
+        path = os.path.join(tmpdir, f'{config}.{s:05d}', f'shard.{s:05d}.mds')
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, 'wb') as f:
+            f.write(batch.buffer[o:o + batch.sizes[s]].cpu().numpy().tobytes())
+        files.append((path, batch.samples[s]))
+    meta = (plan.names, [c.encoding for c in plan.columns],
+            [c.row_bytes if c.is_fixed else None for c in plan.columns])
+    one = _cpu_leg(files, meta, 1, args.cpu_seconds)
+    allc = _cpu_leg(files, meta, procs, args.cpu_seconds)
     return {
-        'value': done / dt,
+        'value': allc[0],
         'unit': 'samples/s',
-        'gib_per_s': nbytes / dt / 2**30,
+        'gib_per_s': allc[1],
         'cores': procs,
         'kind': 'port',
-        'sample': (f'oracle per-sample MDSReader loop (open/seek/read + frombuffer per sample, '
-                   f'mds/reader.py:103-149; encodings.py:760-773) over a 64 MiB config-'
-                   f'{args.config} shard from page cache per process, {procs} process(es), '
-                   f'{done} samples in {dt:.1f} s ({done / dt / procs:.0f} samples/s per core)'),
+        'one_core': {'value': one[0], 'unit': 'samples/s', 'gib_per_s': one[1]},
+        'sample': (f'reference MDSReader.get_item restated (oracle ReferenceCostMDSReader: '
+                   f'open/seek/read per sample, mds/reader.py:128-149; per-column coder built per '
+                   f'call as _get_coder does, encodings.py:697-714,760-773) over full 64 MiB '
+                   f'config-{config} shards of this workload copied to page-cached files: 1 '
+                   f'process {one[2]} samples in {one[3]:.1f} s; {procs} processes '
+                   f'(min(sched_getaffinity={aff}, box share OMP_NUM_THREADS={share or "unset"}))'
+                   f', {allc[2]} samples in {allc[3]:.1f} s'),
     }
 
 
-def committed_traffic(config):
-    """Per-launch HBM bytes of the decode kernel from the newest committed rocprofv3 PMC run of
-    this benchmark (FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM, + WRITE_SIZE)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(HERE, 'profiles', 'r*', f'pmc_bench_{config}_summary.json')))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        summ = json.load(f)
-    return summ.get('hbm_traffic_bytes_per_launch'), os.path.relpath(files[-1], HERE)
+# ---------------------------------------------------------------------------------------------
+# measurement
+def committed_traffic(key, kernel):
+    """Per-launch HBM bytes of ``kernel`` on workload ``key`` from a committed rocprofv3 PMC
+    summary (FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM, + WRITE_SIZE), or (None, None)
+    when no summary was taken on this exact workload and kernel."""
+    for path in sorted(glob.glob(os.path.join(HERE, 'profiles', 'r*', '**', 'pmc_*.json'),
+                                 recursive=True), reverse=True):
+        try:
+            with open(path) as f:
+                summ = json.load(f)
+        except (OSError, ValueError):
+            continue
+        for e in summ.get('entries', []):
+            if e.get('workload_key') == key and kernel and kernel in e.get('kernel', ''):
+                return e.get('hbm_traffic_bytes_per_launch'), os.path.relpath(path, HERE)
+    return None, None
 
 
-def copy_ceiling(batch, dev, iters=10):
+def copy_ceiling(batch, iters=10):
     """Median rate of a read+write streaming copy of the batch's shard bytes (GB/s)."""
     from streaming_amd import _native
     lib = _native.lib()
     src = batch.buffer
     dst = torch.empty_like(src)
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.current_stream(src.device)
     start = [torch.cuda.Event(enable_timing=True) for _ in range(iters + 1)]
     end = [torch.cuda.Event(enable_timing=True) for _ in range(iters + 1)]
     for i in range(iters + 1):
@@ -210,7 +314,7 @@ def copy_ceiling(batch, dev, iters=10):
         end[i].record(stream)
         if rc != 0:
             raise RuntimeError(f'mdsx_copy_probe failed: {lib.mdsx_last_error().decode()}')
-    torch.cuda.synchronize(dev)
+    torch.cuda.synchronize(src.device)
     if not torch.equal(src[-4096:], dst[-4096:]):
         raise RuntimeError('mdsx_copy_probe: copy mismatch')
     ms = float(np.median([start[i].elapsed_time(end[i]) for i in range(1, iters + 1)]))
@@ -218,23 +322,24 @@ def copy_ceiling(batch, dev, iters=10):
     return {'GBps': 2 * src.numel() / ms / 1e6, 'ms': ms, 'bytes_per_launch': 2 * src.numel()}
 
 
-def main():
-    args = parse_args()
-    world, rank, local = init_dist(args)
-    dev = torch.device('cuda', torch.cuda.current_device())
+def measure(args, config, world, rank, dev, tmpdir):
+    from streaming_amd import _native
     from streaming_amd.decoder import BatchDecoder, output_bytes
-
-    plan, batch, sources, workload = build_workload(args, rank, world)
+    mine, total_shards = shard_plan(args, config, rank, world)
+    synth, desc = build_workload(config, mine)
+    plan, batch = synth.plan, synth.batch
     dec = BatchDecoder(plan, batch, single=args.single)
     out = dec.run()
     dec.check()
+    kernel = _native.last_kernel()
     if not args.no_verify:
-        verify(args, plan, out, sources)
+        verify(config, out, synth.sources)
     for _ in range(args.warmup):
         dec.run()
     torch.cuda.synchronize(dev)
 
     K = args.steps
+    stream = torch.cuda.current_stream(dev)  # the stream the kernels are launched on
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
     barrier(world)
     torch.cuda.synchronize(dev)
@@ -248,7 +353,8 @@ def main():
     elapsed = max_over_ranks(t1 - t0, device=dev)
     dec.check()
     if not args.no_verify:
-        verify(args, plan, dec.result(), sources)
+        verify(config, dec.result(), synth.sources)
+    assert stream == torch.cuda.current_stream(dev)
 
     decode_ms = [events[k][1].elapsed_time(events[k][2]) for k in range(K)]
     scan_ms = [events[k][0].elapsed_time(events[k][1]) for k in range(K)]
@@ -256,62 +362,114 @@ def main():
     R = batch.shard_bytes
     W = output_bytes(plan, dec.result())
     rows = batch.total_rows
-    total_rows = rows * world
-    value = total_rows * K / elapsed
-    gibs = R * world * K / elapsed / 2**30
+    per_rank = gather_objects(world, {
+        'rank': rank, 'ms_per_step': (t1 - t0) / K * 1e3, 'rows': rows, 'shards': len(mine),
+        'shard_ids': f'{mine[0]}..{mine[-1]} step {world}' if mine else ''})
+    all_rows = sum(p['rows'] for p in per_rank)
     achieved = (R + W) / kern_s / 1e9
+    step_s = (float(np.mean(decode_ms)) + float(np.mean(scan_ms))) / 1e3
+    copy = copy_ceiling(batch) if args.copy_probe else None
+    key = workload_key(config, batch, W)
+    traffic, traffic_src = committed_traffic(key, kernel)
+    result = {
+        'value': all_rows * K / elapsed,
+        'unit': 'samples/s',
+        'mds_gib_per_s': R * world * K / elapsed / 2**30,
+        'ms_per_step': elapsed / K * 1e3,
+        'config': {
+            'workload': desc,
+            'workload_key': key,
+            'samples_per_gpu': rows,
+            'shards_per_gpu': batch.nshards,
+            'shards_total': total_shards,
+            'shard_bytes_per_gpu': R,
+            'output_bytes_per_gpu': W,
+            'parallelism': f'{world} GPU(s), global shard g -> rank g % {world}, no data-path '
+                           f'collectives',
+        },
+        'per_rank': per_rank,
+        'roofline': {
+            'bound': 'hbm',
+            'kernel': kernel,
+            'achieved': achieved,
+            'peak': HBM_PEAK_GBS,
+            'unit': 'GB/s',
+            'frac': achieved / HBM_PEAK_GBS,
+            'traffic': traffic,
+            'traffic_source': traffic_src,
+            'algorithmic_bytes_per_launch': R + W,
+            'kernel_ms': kern_s * 1e3,
+            'scan_ms': float(np.mean(scan_ms)),
+            'step_frac': (R + W) / step_s / 1e9 / HBM_PEAK_GBS,
+            'frac_of_measured_copy': achieved / COPY_MEASURED_GBS,
+            'copy_ceiling_same_run': copy,
+        },
+        'cpu_baseline': None,
+    }
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        result['cpu_baseline'] = cpu_baseline(args, config, synth, tmpdir)
+    del dec, out, synth
+    torch.cuda.empty_cache()
+    return result
 
-    copy = copy_ceiling(batch, dev) if args.copy_probe else None
 
+def dry_run(args, world, rank):
+    """No GPU: the launcher's ranks, their process group and shard ownership (CPU test hook)."""
+    lines = {}
+    for config in ('B', 'C') if args.config == 'BC' else (args.config, ):
+        mine, total = shard_plan(args, config, rank, world)
+        lines[config] = gather_objects(world, {'rank': rank, 'shards': mine, 'total': total})
+    barrier(world)
     if rank == 0:
-        cpu = cpu_baseline(args) if args.cpu_seconds > 0 else None
-        traffic, traffic_src = committed_traffic(args.config)
-        line = {
-            'metric': METRIC,
-            'value': value,
-            'unit': 'samples/s',
-            'mds_gib_per_s': gibs,
-            'n_gpus': world,
-            'steps': K,
-            'warmup': args.warmup,
-            'ms_per_step': elapsed / K * 1e3,
-            'higher_is_better': True,
-            'scaling': 'weak',
-            'vs_baseline': None,
-            'dtype': 'u8',
-            'data': 'synthetic',
-            'parity': 'bit-exact vs encoded source columns' if not args.no_verify else 'skipped',
-            'config': {
-                'workload': workload,
-                'samples_per_gpu': rows,
-                'shards_per_gpu': batch.nshards,
-                'shard_bytes_per_gpu': R,
-                'output_bytes_per_gpu': W,
-                'parallelism': f'{world} GPU(s), per-GPU shard ownership, no data-path collectives',
-            },
-            'roofline': {
-                'bound': 'hbm',
-                'kernel': 'mdsx_kernels::decode_kernel',
-                'achieved': achieved,
-                'peak': HBM_PEAK_GBS,
-                'unit': 'GB/s',
-                'frac': achieved / HBM_PEAK_GBS,
-                'traffic': traffic,
-                'traffic_source': traffic_src,
-                'algorithmic_bytes_per_launch': R + W,
-                'kernel_ms': kern_s * 1e3,
-                'scan_ms': float(np.mean(scan_ms)),
-                # same-run streaming copy of the shard bytes (mdsx_copy_probe, the fastest copy
-                # shape measured on this part): the practical HBM ceiling next to the 8 TB/s peak
-                'copy_ceiling': copy,
-                'frac_of_copy_ceiling': achieved / copy['GBps'] if copy else None,
-            },
-            'cpu_baseline': cpu,
-        }
-        print(json.dumps(line), flush=True)
+        print(json.dumps({'dry_run': True, 'n_gpus': world, 'ownership': lines}), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
 
 
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if args.gpus < 1:
+        raise SystemExit('--gpus must be >= 1')
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        return launch(args, argv)  # before any GPU call in this process
+    world, rank, local, dev = init_dist(args)
+    if args.dry_run:
+        dry_run(args, world, rank)
+        return 0
+    configs = ['B', 'C'] if args.config == 'BC' else [args.config]
+    with tempfile.TemporaryDirectory(prefix='mdsx_cpu_') as tmpdir:
+        results = {c: measure(args, c, world, rank, dev, tmpdir) for c in configs}
+    head = results[configs[0]]
+    if rank == 0:
+        line = {
+            'metric': METRIC,
+            'value': head['value'],
+            'unit': 'samples/s',
+            'mds_gib_per_s': head['mds_gib_per_s'],
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': head['ms_per_step'],
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': 'u8',
+            'data': 'synthetic (device-generated MDS shards, bit-identical to the reference '
+                    'writer layout)',
+            'parity': 'bit-exact vs encoded source columns' if not args.no_verify else 'skipped',
+            'config': head['config'],
+            'per_rank': head['per_rank'],
+            'roofline': head['roofline'],
+            'cpu_baseline': head['cpu_baseline'],
+        }
+        if 'C' in results and configs[0] != 'C':
+            line['config_c'] = results['C']
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+    return 0
+
+
 if __name__ == '__main__':
-    main()
+    sys.exit(main())

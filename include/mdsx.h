@@ -91,6 +91,10 @@ typedef struct mdsx_status {
 /* ---- version / diagnostics ------------------------------------------------------------------ */
 const char* mdsx_version(void);
 const char* mdsx_last_error(void); /* thread-local message of the last failing call            */
+/* Template name of the decode kernel the calling thread's last mdsx_decode_shards(_single) call
+ * launched, as rocprofv3 reports it (e.g. "decode_kernel<4, true, false, false, false, 0>"):
+ * ties a measured launch to the kernel its profile names. Not part of the reference interface. */
+const char* mdsx_last_kernel(void);
 
 /* ---- plan: per-shard schema ------------------------------------------------------------------
  * Replaces the per-sample encoding dispatch: mds_decode -> _get_coder (encodings.py:697-714,
@@ -104,7 +108,8 @@ int mdsx_plan_create(const char* const* encodings, const int64_t* column_sizes, 
 void mdsx_plan_destroy(mdsx_plan* plan);
 int mdsx_plan_num_columns(const mdsx_plan* plan);
 int mdsx_plan_num_var(const mdsx_plan* plan);
-/* Rows per tile for this schema (64 by default). Tile t of shard s covers rows
+/* Rows per tile for this schema (all-fixed plans: about 32 KiB of rows, >= 4; ragged plans: 32).
+ * Tile t of shard s covers rows
  * [(t - tile0) * tile_rows, ...) of that shard; a shard has ceil(samples / tile_rows) tiles. */
 int mdsx_plan_tile_rows(const mdsx_plan* plan);
 /* Rows per tile of the encoder's batches (mdsx_encode_shards): its tile table is built with

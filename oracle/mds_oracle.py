@@ -37,7 +37,8 @@ from typing import Any, Optional
 import numpy as np
 
 __all__ = [
-    'OracleMDSReader', 'mds_decode', 'decode_shard_columns', 'decode_fixed_shard_vectorized',
+    'OracleMDSReader', 'ReferenceCostMDSReader', 'mds_decode', 'mds_decode_reference_cost',
+'decode_shard_columns', 'decode_fixed_shard_vectorized',
     'column_digests', 'utf8_is_valid', 'load_index', 'writer_split', 'encode_sample_from_columns',
     'encode_joint_shard'
 ]
@@ -150,6 +151,57 @@ class OracleMDSReader:
 
     def __len__(self) -> int:
         return self.samples
+
+
+class _CostNDArray:
+    """``NDArray`` construction as ``_get_coder`` -> ``NDArray.from_str`` does it on EVERY call
+    (encodings.py:148-193): split the config, parse the shape, assert the dtype and dims, and
+    compute the static size with ``np.prod`` (its decode is the oracle's)."""
+
+    def __init__(self, config: str) -> None:
+        args = config.split(':') if config else []
+        assert len(args) in {0, 1, 2}
+        dtype = args[0] if len(args) >= 1 else None
+        shape = tuple(map(int, args[1].split(','))) if len(args) >= 2 else None
+        if dtype is not None:
+            assert dtype in _VALUE_DTYPES.values()
+        if shape is not None:
+            for dim in shape:
+                assert 1 <= dim
+        self.size = None if dtype is None or shape is None else \
+            int(np.prod(shape)) * getattr(np, dtype)().nbytes
+        self.config = config
+
+
+def mds_decode_reference_cost(encoding: str, data: bytes) -> Any:
+    """``mds_decode`` (encodings.py:760-773) with the per-call coder construction of
+    ``_get_coder`` (encodings.py:697-714): a fresh coder object per column per sample (``cls()``,
+    ``Scalar.__init__`` computing ``dtype().nbytes``, ``NDArray.from_str``), as the reference
+    reader pays it. Same values as :func:`mds_decode`; used for the CPU baseline timing."""
+    index = encoding.find(':')
+    if index == -1:
+        if encoding in _SCALARS:
+            getattr(np, encoding)().nbytes  # Scalar.__init__ (encodings.py:308-313)
+        elif encoding not in ('bytes', 'str', 'int'):
+            raise ValueError(f'oracle does not decode encoding {encoding!r}')
+        return mds_decode(encoding, data)
+    name, config = encoding[:index], encoding[index + 1:]
+    if name != 'ndarray':
+        raise ValueError(f'oracle does not decode encoding {encoding!r}')
+    coder = _CostNDArray(config)
+    return _ndarray_decode(coder.config, data)
+
+
+class ReferenceCostMDSReader(OracleMDSReader):
+    """:class:`OracleMDSReader` whose ``decode_sample`` pays the reference's per-call coder
+    construction (:func:`mds_decode_reference_cost`): the CPU baseline of ``bench.py``."""
+
+    def decode_sample(self, data: bytes) -> dict[str, Any]:
+        return {
+            name: mds_decode_reference_cost(enc, part)
+            for name, enc, part in zip(self.column_names, self.column_encodings,
+                                       self.split_sample(data))
+        }
 
 
 def utf8_is_valid(data: bytes) -> bool:

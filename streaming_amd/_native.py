@@ -45,6 +45,7 @@ BATCH_PAD = 256
 EXPORTED_SYMBOLS = (
     'mdsx_version',
     'mdsx_last_error',
+    'mdsx_last_kernel',
     'mdsx_plan_create',
     'mdsx_plan_destroy',
     'mdsx_plan_num_columns',
@@ -134,6 +135,8 @@ def _declare(handle: ctypes.CDLL) -> None:
     handle.mdsx_version.argtypes = []
     handle.mdsx_last_error.restype = ctypes.c_char_p
     handle.mdsx_last_error.argtypes = []
+    handle.mdsx_last_kernel.restype = ctypes.c_char_p
+    handle.mdsx_last_kernel.argtypes = []
     handle.mdsx_plan_create.restype = c_int
     handle.mdsx_plan_create.argtypes = [
         ctypes.POINTER(ctypes.c_char_p),
@@ -225,6 +228,12 @@ def lib() -> ctypes.CDLL:
 def last_error() -> str:
     msg = lib().mdsx_last_error()
     return msg.decode('utf-8', 'replace') if msg else ''
+
+
+def last_kernel() -> str:
+    """Template name of the decode kernel this thread launched last (rocprofv3's name)."""
+    name = lib().mdsx_last_kernel()
+    return name.decode() if name else ''
 
 
 def raise_for_code(code: int, where: str) -> None:

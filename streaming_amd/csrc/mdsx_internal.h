@@ -29,6 +29,8 @@ struct ColumnSpec {
 };
 
 int fail(int code, const std::string& msg);
+// Template name of the last decode kernel this thread launched (mdsx_last_kernel).
+void set_last_kernel(const std::string& name);
 
 }  // namespace mdsx
 

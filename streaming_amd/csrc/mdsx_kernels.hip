@@ -1336,8 +1336,12 @@ static int launch_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s,
     if (plan->cols[c].kind == MDSX_KIND_FIXED && plan->cols[c].row_bytes > kSmallMax &&
         plan->cols[c].row_bytes % 16 != 0)
       edges = true;
-#define MDSX_DECODE(U, NT, RG, ED, SG) \
-  hipLaunchKernelGGL((decode_kernel<U, NT, RG, ED, SG>), dim3(a.ntiles), dim3(kBlock), lds, s, a)
+#define MDSX_DECODE(U, NT, RG, ED, SG)                                                           \
+  do {                                                                                           \
+    mdsx::set_last_kernel("decode_kernel<" #U ", " #NT ", " #RG ", " #ED ", " #SG ", 0>");       \
+    hipLaunchKernelGGL((decode_kernel<U, NT, RG, ED, SG>), dim3(a.ntiles), dim3(kBlock), lds, s, \
+                       a);                                                                       \
+  } while (0)
 #define MDSX_DECODE_U(U)                                                 \
   do {                                                                   \
     if (ragged && single) {                                              \
@@ -1356,6 +1360,8 @@ static int launch_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s,
   } while (0)
 #define MDSX_RING(U, K)                                                                    \
   do {                                                                                     \
+    mdsx::set_last_kernel(std::string("decode_kernel<" #U ", ") + (nt ? "true" : "false") + \
+                          ", true, true, " + (single ? "true" : "false") + ", " #K ">");     \
     const size_t rl = ((lds + 15) & ~size_t(15)) + size_t(kBlock / 64) * (K)*1024;         \
     if (single) {                                                                          \
       if (nt)                                                                              \

@@ -18,11 +18,14 @@
 namespace mdsx {
 
 thread_local std::string g_last_error;
+thread_local std::string g_last_kernel;
 
 int fail(int code, const std::string& msg) {
   g_last_error = msg;
   return code;
 }
+
+void set_last_kernel(const std::string& name) { g_last_kernel = name; }
 
 namespace {
 
@@ -209,6 +212,8 @@ using namespace mdsx;
 extern "C" {
 
 const char* mdsx_last_error(void) { return g_last_error.c_str(); }
+
+const char* mdsx_last_kernel(void) { return g_last_kernel.c_str(); }
 
 const char* mdsx_version(void) { return "mdsx 0.1.0 (gfx950)"; }
 

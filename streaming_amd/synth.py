@@ -69,48 +69,161 @@ class SynthShards:
     sources: dict[str, torch.Tensor]
 
 
+def config_b_samples_per_shard(size_limit: int = 1 << 26) -> int:
+    """Samples of a full config-B shard under the writer's size limit (16 352 at 64 MiB)."""
+    names, encs, sizes = _schema(CONFIG_B)
+    config = shard_config_bytes(names, encs, sizes, None, [], size_limit)
+    return (size_limit - 8 - len(config)) // (sum(sizes) + 4)
+
+
 def fixed_b_batch_on_device(num_samples: int,
                             seed: int = 0,
                             size_limit: int = 1 << 26,
                             device: Union[str, torch.device, None] = None,
                             keep_sources: bool = True,
-                            first_id: int = 0) -> SynthShards:
+                            first_id: int = 0,
+                            shard_ids: Optional[list[int]] = None) -> SynthShards:
     """Config B shards written directly into a device batch buffer.
 
     ``x`` rows are uniform random bytes (every float32 bit pattern; ``torch.randint`` on the
     device, seeded), ``id`` is ``first_id + i``.
+
+    With ``shard_ids``, the batch holds those shards of a larger dataset of full shards instead:
+    global shard ``g`` has ids ``g * per ..`` and ``x`` drawn from a generator seeded
+    ``seed + g``, so a shard's bytes do not depend on which rank builds it (``num_samples`` and
+    ``first_id`` are then ignored).
     """
     names, encs, sizes = _schema(CONFIG_B)
     plan = Plan(names, encs, sizes)
     config = shard_config_bytes(names, encs, sizes, None, [], size_limit)
     sample = sum(sizes)
     per = (size_limit - 8 - len(config)) // (sample + 4) if size_limit else num_samples
-    counts = [per] * (num_samples // per) + ([num_samples % per] if num_samples % per else [])
+    if shard_ids is not None:
+        counts = [per] * len(shard_ids)
+        firsts = [g * per for g in shard_ids]
+        seeds = [seed + g for g in shard_ids]
+    else:
+        counts = [per] * (num_samples // per) + ([num_samples % per] if num_samples % per else [])
+        firsts = [first_id + sum(counts[:s]) for s in range(len(counts))]
+        seeds = [None] * len(counts)
     shard_sizes = [4 + 4 * (n + 1) + len(config) + n * sample for n in counts]
     batch = make_batch(plan, shard_sizes, counts, device)
     dev = batch.device
     gen = torch.Generator(device=dev)
     gen.manual_seed(seed)
-    ids_all = torch.arange(first_id, first_id + num_samples, dtype=torch.int32, device=dev)
-    xs = []
-    row = 0
+    ids, xs = [], []
     for s, n in enumerate(counts):
+        if seeds[s] is not None:
+            gen.manual_seed(seeds[s])
         header = _fixed_header(n, sample, config)
         off = batch.offsets[s]
         batch.buffer[off:off + len(header)].copy_(torch.frombuffer(bytearray(header),
                                                                    dtype=torch.uint8))
         body = batch.buffer[off + len(header):off + shard_sizes[s]].view(n, sample)
         x = torch.randint(0, 256, (n, 4096), dtype=torch.uint8, device=dev, generator=gen)
-        body[:, :4].copy_(ids_all[row:row + n].view(torch.uint8).view(n, 4))
+        idv = torch.arange(firsts[s], firsts[s] + n, dtype=torch.int32, device=dev)
+        body[:, :4].copy_(idv.view(torch.uint8).view(n, 4))
         body[:, 4:].copy_(x)
+        ids.append(idv)
         if keep_sources:
             xs.append(x)
-        row += n
-    sources = {'id': ids_all}
+    sources = {'id': torch.cat(ids) if ids else torch.empty(0, dtype=torch.int32, device=dev)}
     if keep_sources:
         sources['x'] = torch.cat(xs).view(torch.float32) if xs else torch.empty(0, 1024)  # bits
     torch.cuda.synchronize(dev)
     return SynthShards(plan, batch, counts, sources)
+
+
+def utf8_encode_device(cp: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """UTF-8 bytes of code points ``cp`` (int64, no surrogates) on the device: returns
+    (packed bytes, bytes per code point)."""
+    nb = 1 + (cp >= 0x80).long() + (cp >= 0x800).long() + (cp >= 0x10000).long()
+    pos = torch.cumsum(nb, 0) - nb
+    out = torch.empty(int(nb.sum()), dtype=torch.uint8, device=cp.device)
+    lead = torch.where(nb == 1, cp,
+                       torch.where(nb == 2, 0xC0 | (cp >> 6),
+                                   torch.where(nb == 3, 0xE0 | (cp >> 12), 0xF0 | (cp >> 18))))
+    out[pos] = lead.to(torch.uint8)
+    for k in (1, 2, 3):  # continuation byte k of a sequence of nb bytes carries bits 6*(nb-1-k)
+        m = nb > k
+        shift = 6 * (nb[m] - 1 - k)
+        out[pos[m] + k] = (0x80 | ((cp[m] >> shift) & 0x3F)).to(torch.uint8)
+    return out, nb
+
+
+def _ragged(lengths: torch.Tensor, values: torch.Tensor) -> 'RaggedColumn':
+    from streaming_amd.decoder import RaggedColumn
+    offsets = torch.zeros(lengths.numel() + 1, dtype=torch.int64, device=lengths.device)
+    torch.cumsum(lengths, 0, out=offsets[1:])
+    return RaggedColumn(values, offsets)
+
+
+def var_c_columns_on_device(shard_ids: list[int],
+                            seed: int = 2000,
+                            size_limit: int = 1 << 26,
+                            device: Union[str, torch.device, None] = None,
+                            str_chars: tuple[int, int] = (16, 256),
+                            blob_bytes: tuple[int, int] = (3072, 5120)):
+    """Config C columns (``n: int``, ``b: bytes U[3072,5120]``, ``s: str`` of U[16,256] code
+    points, 25 % each of 1/2/3/4-byte UTF-8) for full 64 MiB shards of a larger dataset, built
+    on the device: global shard ``g`` draws from a generator seeded ``seed + g`` and holds
+    exactly the rows the writer puts into one shard (``base/writer.py:263-269``). Returns
+    (columns in decoder layout, rows per shard)."""
+    dev = torch.device(device or 'cuda')
+    if dev.index is None:
+        dev = torch.device('cuda', torch.cuda.current_device())
+    names, encs, sizes = _schema(CONFIG_C)
+    config = shard_config_bytes(names, encs, sizes, None, [], size_limit)
+    cap = size_limit - 8 - len(config)
+    rows_try = cap // (8 + blob_bytes[0] + 8 + str_chars[0] + 4) + 1
+    gen = torch.Generator(device=dev)
+    ns, bs, ss, counts = [], [], [], []
+    for g in shard_ids:
+        gen.manual_seed(seed + g)
+        kw = dict(device=dev, generator=gen)
+        b_len = torch.randint(blob_bytes[0], blob_bytes[1] + 1, (rows_try, ), **kw)
+        chars = torch.randint(str_chars[0], str_chars[1] + 1, (rows_try, ), **kw)
+        width = torch.randint(0, 4, (int(chars.sum()), ), **kw)
+        lo = torch.tensor([0x20, 0x80, 0x800, 0x10000], device=dev)[width]
+        hi = torch.tensor([0x7F, 0x800, 0x10000 - 0x800, 0x110000], device=dev)[width]
+        cp = lo + (torch.rand(width.shape, dtype=torch.float64, **kw) * (hi - lo)).long()
+        cp = torch.where((width == 2) & (cp >= 0xD800), cp + 0x800, cp)  # skip surrogates
+        nb = 1 + (cp >= 0x80).long() + (cp >= 0x800).long() + (cp >= 0x10000).long()
+        row_of_cp = torch.repeat_interleave(torch.arange(rows_try, device=dev), chars)
+        s_len = torch.zeros(rows_try, dtype=torch.int64, device=dev).index_add_(0, row_of_cp, nb)
+        cum4 = torch.cumsum(8 + b_len + 8 + s_len + 4, 0).cpu().numpy()
+        n = int(np.searchsorted(cum4, cap, side='right'))
+        b_len, s_len = b_len[:n], s_len[:n]
+        ncp = int(chars[:n].sum())
+        s_vals, _ = utf8_encode_device(cp[:ncp])
+        b_vals = torch.randint(0, 256, (int(b_len.sum()), ), dtype=torch.uint8, **kw)
+        nv = torch.randint(-2**62, 2**62, (n, ), dtype=torch.int64, **kw)
+        ns.append(nv)
+        bs.append(_ragged(b_len, b_vals))
+        ss.append(_ragged(s_len, s_vals))
+        counts.append(n)
+    from streaming_amd.encoder import concat_columns
+    cols = concat_columns([{'n': a, 'b': b, 's': s} for a, b, s in zip(ns, bs, ss)])
+    return cols, counts
+
+
+def var_c_batch_on_device(shard_ids: list[int],
+                          seed: int = 2000,
+                          size_limit: int = 1 << 26,
+                          device: Union[str, torch.device, None] = None) -> SynthShards:
+    """Config C shards (``shard_ids`` of a dataset of full shards, see
+    :func:`var_c_columns_on_device`) written by the device MDS encoder into one decode batch."""
+    from streaming_amd.encoder import encode_batch
+    names, encs, sizes = _schema(CONFIG_C)
+    plan = Plan(names, encs, sizes)
+    config = shard_config_bytes(names, encs, sizes, None, [], size_limit)
+    cols, counts = var_c_columns_on_device(shard_ids, seed, size_limit, device)
+    enc, consumed = encode_batch(plan, cols, config, size_limit)
+    if enc is None or [e - b for b, e in enc.bounds] != counts or consumed != sum(counts):
+        raise RuntimeError('config C synth: encoder split differs from the per-shard rows')
+    batch = enc.decode_batch(plan)
+    torch.cuda.synchronize(batch.device)
+    return SynthShards(plan, batch, counts, cols)
 
 
 def utf8_pool(rng: np.random.Generator, count: int) -> tuple[np.ndarray, np.ndarray]:

@@ -1,0 +1,54 @@
+"""bench.py's N-GPU launcher, on CPU: ``python bench.py --gpus N --dry-run`` starts N child ranks
+itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* as torch.distributed.run sets them), they join
+a gloo process group and report the shards they own; a world size other than ``--gpus`` fails."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env_extra=None, timeout=180):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ('RANK', 'WORLD_SIZE', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT')}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py')] + args, env=env,
+                          capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+
+
+@pytest.mark.parametrize('gpus', [2, 3])
+def test_launcher_spawns_ranks_and_partitions_shards(gpus):
+    p = _run(['--gpus', str(gpus), '--dry-run'])
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith('{')]
+    assert len(lines) == 1  # rank 0 only
+    line = lines[0]
+    assert line['n_gpus'] == gpus
+    for config, per_gpu in (('B', 62), ('C', 64)):
+        ranks = line['ownership'][config]
+        assert [r['rank'] for r in ranks] == list(range(gpus))
+        total = ranks[0]['total']
+        assert total == per_gpu * gpus
+        flat = sorted(s for r in ranks for s in r['shards'])
+        assert flat == list(range(total))  # every global shard owned exactly once
+        for r in ranks:
+            assert all(s % gpus == r['rank'] for s in r['shards'])  # owned_shards: g -> g % N
+            assert len(r['shards']) == per_gpu  # weak scaling: fixed work per GPU
+
+
+def test_world_mismatch_is_an_error():
+    p = _run(['--gpus', '2', '--dry-run'], {'WORLD_SIZE': '3', 'RANK': '0'})
+    assert p.returncode != 0
+    assert 'WORLD_SIZE=3' in p.stderr
+
+
+def test_single_rank_dry_run():
+    p = _run(['--gpus', '1', '--dry-run', '--config', 'B'])
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line['n_gpus'] == 1
+    assert line['ownership']['B'][0]['shards'] == list(range(62))

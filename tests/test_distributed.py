@@ -1,7 +1,10 @@
 """Multi-process (gloo, CPU) coverage of the N>1 path: per-rank shard ownership covers every
-shard exactly once with imbalance <= 1, each rank's owned shards decode (oracle, CPU) to the
-reference digest of its part, and the benchmark's max-over-ranks timing reduction."""
+shard exactly once with imbalance <= 1; the ranks' owned shards, read with the oracle (CPU; this
+container has no GPU) and put back in shard order, give the reference's ordered content digest of
+config A (manifest.json ``content_sha256``, written by the real reference reader); and the
+benchmark's max-over-ranks timing reduction."""
 
+import hashlib
 import os
 import socket
 
@@ -30,13 +33,13 @@ def _worker(rank, world, port, q):
         mine = owned_shards(len(idx['shards']), rank, world)
         d = os.path.join(gu.GOLDEN, 'config_a')
         samples = 0
-        numbers = []
+        items = []
         for s in mine:
             r = mds_oracle.OracleMDSReader(d, None, idx['shards'][s])
             samples += len(r)
-            numbers.extend(r.get_item(i)['number'] for i in range(len(r)))
+            items.extend((r.get_item(i)['number'], r.get_item(i)['words']) for i in range(len(r)))
         gathered = [None] * world
-        dist.all_gather_object(gathered, (mine, samples, numbers))
+        dist.all_gather_object(gathered, (mine, samples, items))
         t = max_over_ranks(float(rank + 1))
         total = sum_over_ranks(float(samples))
         q.put((rank, gathered, t, total))
@@ -74,8 +77,15 @@ def test_per_rank_shard_ownership(world):
                 n = idx['shards'][s]['samples']
                 by_shard[s] = g[2][pos:pos + n]
                 pos += n
-        allnum = np.concatenate([by_shard[s] for s in range(n_shards)])
-        assert len(allnum) == 10_000
+        h = hashlib.sha256()
+        count = 0
+        for s in range(n_shards):
+            for number, words in by_shard[s]:
+                h.update(np.int64(number).tobytes())
+                h.update(words.encode('utf-8'))
+                count += 1
+        assert count == 10_000
+        assert h.hexdigest() == gu.manifest()['config_a']['content_sha256']
 
 
 def test_owned_shards_rejects_bad_rank():
