@@ -282,10 +282,19 @@ def cpu_baseline(args, config, synth, tmpdir):
 
 # ---------------------------------------------------------------------------------------------
 # measurement
+def lib_sha() -> str:
+    """sha256 (16 hex digits) of the libmdsx.so this run loads: profiles match on it."""
+    import hashlib
+    from streaming_amd import _native
+    with open(_native.lib_path, 'rb') as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def committed_traffic(key, kernel):
     """Per-launch HBM bytes of ``kernel`` on workload ``key`` from a committed rocprofv3 PMC
     summary (FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM, + WRITE_SIZE), or (None, None)
-    when no summary was taken on this exact workload and kernel."""
+    when no summary was taken on this exact workload, kernel and library build."""
+    build = lib_sha()
     for path in sorted(glob.glob(os.path.join(HERE, 'profiles', 'r*', '**', 'pmc_*.json'),
                                  recursive=True), reverse=True):
         try:
@@ -294,7 +303,8 @@ def committed_traffic(key, kernel):
         except (OSError, ValueError):
             continue
         for e in summ.get('entries', []):
-            if e.get('workload_key') == key and kernel and kernel in e.get('kernel', ''):
+            if e.get('workload_key') == key and kernel and kernel in e.get('kernel', '') and \
+                    e.get('lib_sha') == build:
                 return e.get('hbm_traffic_bytes_per_launch'), os.path.relpath(path, HERE)
     return None, None
 
@@ -397,6 +407,7 @@ def measure(args, config, world, rank, dev, tmpdir):
             'frac': achieved / HBM_PEAK_GBS,
             'traffic': traffic,
             'traffic_source': traffic_src,
+            'lib_sha': lib_sha(),
             'algorithmic_bytes_per_launch': R + W,
             'kernel_ms': kern_s * 1e3,
             'scan_ms': float(np.mean(scan_ms)),

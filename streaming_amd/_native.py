@@ -230,6 +230,21 @@ def last_error() -> str:
     return msg.decode('utf-8', 'replace') if msg else ''
 
 
+def check_fork() -> None:
+    """Raise a clear error in a process forked after its parent initialised the GPU.
+
+    A ``torch.utils.data.DataLoader`` worker started with the default ``fork`` context inherits
+    a parent that has touched the GPU (training code usually has) and cannot use the GPU itself.
+    The device readers decode inside the worker, so such loaders need
+    ``multiprocessing_context='spawn'`` (or ``'forkserver'``)."""
+    if torch.cuda._is_in_bad_fork():
+        raise RuntimeError(
+            'streaming_amd: this process was forked after its parent initialised the GPU, so it '
+            'cannot decode shards on the GPU. Create the DataLoader with '
+            "multiprocessing_context='spawn' (or 'forkserver'), e.g. DataLoader(dataset, "
+            "num_workers=4, multiprocessing_context='spawn').")
+
+
 def last_kernel() -> str:
     """Template name of the decode kernel this thread launched last (rocprofv3's name)."""
     name = lib().mdsx_last_kernel()

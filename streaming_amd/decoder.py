@@ -476,6 +476,7 @@ class BatchDecoder:
                  capacities: Optional[dict[str, int]] = None, single: bool = False) -> None:
         if plan.tile_rows != batch.tile_rows:
             raise ValueError('batch was staged for a different tile size')
+        _native.check_fork()
         self.plan = plan
         self.batch = batch
         dev = batch.device

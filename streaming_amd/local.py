@@ -19,6 +19,7 @@ import torch
 from torch.utils.data import Dataset
 
 from streaming_amd.array import Array
+from streaming_amd.cache import DecodedShardCache
 from streaming_amd.decoder import DecodedBatch, decode_batch, stage_shards
 from streaming_amd.distributed import owned_shards
 from streaming_amd.reader import MDSReader, get_plan, load_index, reader_from_json
@@ -39,17 +40,24 @@ class LocalDataset(Array, Dataset):
         local (str): dataset directory.
         split (str, optional): split sub-directory.
         device: CUDA device for decoding (default: current device).
+        decoded_cache_bytes (int, optional): bound on the decoded shards this dataset's readers
+            keep (device + host bytes, LRU; :mod:`streaming_amd.cache`). Default: the
+            process-wide cache (``MDSX_DECODED_CACHE_BYTES``, 16 GiB).
     """
 
     def __init__(self, local: str, split: Optional[str] = None,
-                 device: Union[str, torch.device, None] = None) -> None:
+                 device: Union[str, torch.device, None] = None,
+                 decoded_cache_bytes: Optional[int] = None) -> None:
         split = split or ''
         self.local = local
         self.split = split
         self.device = device
+        self.cache = DecodedShardCache(decoded_cache_bytes) if decoded_cache_bytes is not None \
+            else None
         obj = load_index(local, split)
         self.shards: list[MDSReader] = [
-            reader_from_json(local, split, info, device=device) for info in obj['shards']
+            reader_from_json(local, split, info, device=device, cache=self.cache)
+            for info in obj['shards']
         ]
         self.num_samples = sum(shard.samples for shard in self.shards)
         self.spanner = Spanner(np.array([s.samples for s in self.shards], np.int64))

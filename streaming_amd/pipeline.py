@@ -30,10 +30,13 @@ import torch
 from streaming_amd.compression import decompress, decompress_into, get_compression_extension
 from streaming_amd.decoder import (BatchDecoder, DecodedBatch, DeviceBatch, Plan, RaggedColumn,
                                    _layout, _tables)
-from streaming_amd.hashing import (DeviceHasher, _status_check, get_hash, hex_digests,
-                                   is_device_hash, is_hash)
+from streaming_amd.hashing import DeviceHasher, _status_check, get_hash, hex_digests, is_hash
 
-__all__ = ['ShardFile', 'ShardPipeline', 'shard_files_from_index', 'to_host']
+__all__ = ['ShardFile', 'ShardPipeline', 'shard_files_from_index', 'to_host',
+           'PIPELINE_DEVICE_HASHES']
+
+# Validation hashes computed on the device by the pipeline (the rest on its host threads).
+PIPELINE_DEVICE_HASHES = frozenset({'xxh3_64', 'xxh3_128', 'xxh128'})
 
 
 @dataclass
@@ -117,9 +120,11 @@ class ShardPipeline:
         device: CUDA device.
         validate_hash: check every shard against its index.json ``raw_data.hashes[algo]``
             before its batch is handed out, raising ``ValueError('Checksum failure: ...')`` like
-            ``Stream._prepare_shard_part`` (``stream.py:401-411``). xxHash algorithms run on the
-            device over the resident batch (``streaming_amd.hashing``); hashlib ones on the
-            host threads as the shards are read.
+            ``Stream._prepare_shard_part`` (``stream.py:401-411``). xxh3_64 / xxh128 run on the
+            device over the resident batch (``streaming_amd.hashing``: 2.4-4.5 TB/s); every other
+            algorithm -- hashlib's, and xxh64 / xxh32, whose one dependent chain per shard makes
+            the device version slower than a host core -- on the host threads as
+            the shards are read.
     """
 
     def __init__(self,
@@ -142,7 +147,7 @@ class ShardPipeline:
                         f'Hash algorithm `{validate_hash}` chosen for data ' +
                         f'validation does not match with those provided during dataset ' +
                         f'creation `{sorted((s.hashes or {}).keys())}`. Provide one of those.')
-        self._device_hash = bool(validate_hash) and is_device_hash(validate_hash)
+        self._device_hash = bool(validate_hash) and validate_hash in PIPELINE_DEVICE_HASHES
         self.per = max(1, shards_per_batch)
         self.depth = max(1, depth)
         dev = torch.device(device or 'cuda')
@@ -227,11 +232,11 @@ class ShardPipeline:
                 for got, shard in zip(hex_digests(self.validate_hash, digests), group):
                     if got != shard.hashes[self.validate_hash]:
                         raise ValueError(f'Checksum failure: {shard.path}')
+            # a malformed sample fails its own batch, before the batch is handed out (the
+            # reference raises when that sample is read); waits for this batch's decode, while
+            # the next batches' reads and copies stay queued
+            slot.decoder.check()
             yield out
-        # surface kernel-reported errors of the last batches
-        for slot in self.slots:
-            if slot.decoder is not None:
-                slot.decoder.check()
 
     def close(self) -> None:
         self.pool.shutdown(wait=True)

@@ -21,6 +21,7 @@ A missing shard file raises ``FileNotFoundError`` from ``open`` exactly as the r
 
 from __future__ import annotations
 
+import itertools
 import json
 import os
 import threading
@@ -31,8 +32,11 @@ from typing import Any, Iterator, Optional, Union
 import numpy as np
 import torch
 
+from streaming_amd import _native
 from streaming_amd.array import Array
-from streaming_amd.decoder import DecodedBatch, Plan, RaggedColumn, decode_batch, stage_shards
+from streaming_amd.cache import DecodedShardCache, default_cache
+from streaming_amd.decoder import (DecodedBatch, Plan, RaggedColumn, _status_error, decode_batch,
+                                   output_bytes, stage_shards)
 from streaming_amd.encodings import (host_object_decode, is_mds_encoding_safe,
                                      ndarray_dyn_decode, parse_encoding)
 from streaming_amd.writer import bytes_to_int
@@ -198,21 +202,45 @@ class _HostShard:
     def __init__(self, plan: Plan, decoded: DecodedBatch) -> None:
         self.fixed: dict[str, np.ndarray] = {}
         self.ragged: dict[str, tuple[np.ndarray, np.ndarray]] = {}
+        self.nbytes = 0
         for col in plan.columns:
             out = decoded.columns[col.name]
             if isinstance(out, RaggedColumn):
-                self.ragged[col.name] = (out.values.cpu().numpy(), out.offsets.cpu().numpy())
+                vals, offs = out.values.cpu().numpy(), out.offsets.cpu().numpy()
+                self.ragged[col.name] = (vals, offs)
+                self.nbytes += vals.nbytes + offs.nbytes
             else:
                 rows = out.shape[0]
                 raw = out.reshape(rows, -1).view(torch.uint8).cpu().numpy()
                 raw.setflags(write=False)
                 self.fixed[col.name] = raw
+                self.nbytes += raw.nbytes
+
+
+class _Decoded:
+    """A cache entry: one decoded shard, its kernel status and (once asked for) its host copy."""
+
+    def __init__(self, decoded: DecodedBatch, status: _native.Status, nbytes: int) -> None:
+        self.decoded = decoded
+        self.status = status
+        self.nbytes = nbytes
+        self.host: Optional[_HostShard] = None
+
+
+_reader_keys = itertools.count()
 
 
 class MDSReader(JointReader):
     """Random access to the samples of an MDS shard, decoded on the GPU.
 
-    Same constructor as the reference (mds/reader.py:39-57) plus ``device``.
+    Same constructor as the reference (mds/reader.py:39-57) plus ``device`` and ``cache``.
+
+    Decoded shards live in ``cache`` (a bounded LRU shared by the readers of a process unless one
+    is given, :mod:`streaming_amd.cache`), never beyond it: a shard dropped from the cache, or
+    released by :meth:`evict` / :meth:`release`, is decoded again from its file on next use. Like
+    the reference, which re-opens the shard file for every sample, :meth:`get_item` raises
+    ``FileNotFoundError`` once the file is gone (``StreamingDataset.get_item`` then re-prepares
+    the shard and retries, ``dataset.py:1274-1291``), even if a decoded copy is still cached.
     """
 
     def __init__(self,
@@ -227,7 +255,8 @@ class MDSReader(JointReader):
                  samples: int,
                  size_limit: Optional[Union[int, str]],
                  zip_data: Optional[FileInfo],
-                 device: Union[str, torch.device, None] = None) -> None:
+                 device: Union[str, torch.device, None] = None,
+                 cache: Optional[DecodedShardCache] = None) -> None:
         super().__init__(dirname, split, compression, hashes, raw_data, samples, size_limit,
                          zip_data)
         self.column_encodings = column_encodings
@@ -236,12 +265,13 @@ class MDSReader(JointReader):
         self.device = device
         self._infos = [parse_encoding(e) for e in column_encodings]
         self._lock = threading.Lock()
-        self._decoded: Optional[DecodedBatch] = None
-        self._host: Optional[_HostShard] = None
+        self._cache = cache
+        self._key = next(_reader_keys)
 
     @classmethod
     def from_json(cls, dirname: str, split: Optional[str], obj: dict[str, Any],
-                  device: Union[str, torch.device, None] = None) -> 'MDSReader':
+                  device: Union[str, torch.device, None] = None,
+                  cache: Optional[DecodedShardCache] = None) -> 'MDSReader':
         """Initialize from an ``index.json`` shard entry (mds/reader.py:59-86)."""
         args = deepcopy(obj)
         if args['version'] != 2:
@@ -256,7 +286,7 @@ class MDSReader(JointReader):
         for key in ['raw_data', 'zip_data']:
             arg = args[key]
             args[key] = FileInfo(**arg) if arg else None
-        return cls(**args, device=device)
+        return cls(**args, device=device, cache=cache)
 
     def validate(self, allow_unsafe_types: bool) -> None:
         """Reject unsafe encodings unless allowed (mds/reader.py:88-101)."""
@@ -279,21 +309,48 @@ class MDSReader(JointReader):
         with open(self._filename(), 'rb', 0) as fp:
             return fp.read()
 
-    def decode_shard(self, check: bool = True) -> DecodedBatch:
-        """Decode every sample of this shard on the GPU (cached). Device tensors."""
+    @property
+    def cache(self) -> DecodedShardCache:
+        return self._cache if self._cache is not None else default_cache()
+
+    def _decode_entry(self) -> _Decoded:
+        """This shard's cache entry, decoding the file on a miss (FileNotFoundError if absent)."""
+
+        def create() -> tuple[_Decoded, int]:
+            _native.check_fork()
+            data = self.read_shard_bytes()
+            plan = self.plan
+            batch = stage_shards([data], [self.samples], plan, device=self.device)
+            from streaming_amd.decoder import BatchDecoder
+            dec = BatchDecoder(plan, batch)
+            out = dec.run()
+            status = dec.status()  # waits for the decode
+            nbytes = output_bytes(plan, out)
+            return _Decoded(out, status, nbytes), nbytes
+
         with self._lock:
-            if self._decoded is None:
-                data = self.read_shard_bytes()
-                plan = self.plan
-                batch = stage_shards([data], [self.samples], plan, device=self.device)
-                self._decoded = decode_batch(plan, batch, check=check)
-            return self._decoded
+            return self.cache.get_or_create(self._key, create)
+
+    def decode_shard(self, check: bool = True) -> DecodedBatch:
+        """Decode every sample of this shard on the GPU (cached, bounded). Device tensors.
+
+        With ``check`` a malformed shard raises (IndexError for an empty sample, ValueError for a
+        range or header error); without it the rows that decoded are returned as they are."""
+        entry = self._decode_entry()
+        if check and entry.status.code != 0:
+            raise _status_error(entry.status, self.plan)
+        return entry.decoded
 
     def release(self) -> None:
-        """Drop the cached decoded shard (device and host copies)."""
+        """Drop the decoded shard (device and host copies) from the cache."""
         with self._lock:
-            self._decoded = None
-            self._host = None
+            self.cache.discard(self._key)
+
+    def evict(self) -> int:
+        """Remove the shard files from the local cache (base/reader.py:128-134) and drop the
+        decoded copy, so the next access re-reads the file (or raises FileNotFoundError)."""
+        self.release()
+        return super().evict()
 
     def get_sample_data(self, idx: int) -> bytes:
         """Raw bytes of sample ``idx`` (mds/reader.py:128-149): file offsets table + range."""
@@ -308,6 +365,36 @@ class MDSReader(JointReader):
             raise IndexError(
                 f'Relative sample index {idx} is not present in the {self.raw_data.basename} file.')
         return data
+
+    def _check_row(self, entry: _Decoded, idx: int) -> None:
+        """The decode of this shard reported an error: raise only if sample ``idx`` is one of the
+        bad ones (the reference raises only when a bad sample is read, mds/reader.py:145-148)."""
+        st = entry.status
+        if st.code not in (_native.MDSX_E_EMPTY, _native.MDSX_E_BOUNDS):
+            raise _status_error(st, self.plan)  # shard-level (header) error: every sample
+        # the device checks per sample (decode_kernel): the offsets pair inside the file after
+        # the offsets table, the u32 size heads and every column inside the sample
+        size = os.stat(self._filename()).st_size
+        with open(self._filename(), 'rb', 0) as fp:
+            fp.seek((1 + idx) * 4)
+            begin, end = (int(x) for x in np.frombuffer(fp.read(8), np.uint32))
+        if not (4 + 4 * (self.samples + 1) <= begin <= end <= size):
+            raise ValueError(f'MDS sample {idx} of {self.raw_data.basename} is out of bounds '
+                             f'([{begin}, {end}) in a file of {size} bytes).')
+        data = self.get_sample_data(idx)  # IndexError for an empty sample, as the reference
+        need, pos = 0, 0
+        for size_ in self.column_sizes:
+            if size_:
+                need += int(size_)
+            else:
+                if pos + 4 > len(data):
+                    need = len(data) + 1
+                    break
+                need += 4 + int(np.frombuffer(data[pos:pos + 4], np.uint32)[0])
+                pos += 4
+        if need > len(data):
+            raise ValueError(f'MDS sample {idx} of {self.raw_data.basename}: columns exceed the '
+                             f'sample ({need} > {len(data)} bytes).')
 
     def _materialize(self, host: _HostShard, idx: int) -> dict[str, Any]:
         sample: dict[str, Any] = {}
@@ -350,13 +437,17 @@ class MDSReader(JointReader):
         if not (0 <= idx < self.samples):
             raise IndexError(
                 f'Relative sample index {idx} is not present in the {self.raw_data.basename} file.')
-        host = self._host
+        os.stat(self._filename())  # FileNotFoundError once evicted, as the reference's open()
+        entry = self._decode_entry()
+        if entry.status.code != 0:
+            self._check_row(entry, idx)
+        host = entry.host
         if host is None:
-            decoded = self.decode_shard()
             with self._lock:
-                if self._host is None:
-                    self._host = _HostShard(self.plan, decoded)
-                host = self._host
+                if entry.host is None:
+                    entry.host = _HostShard(self.plan, entry.decoded)
+                    self.cache.update(self._key, entry, entry.nbytes + entry.host.nbytes)
+                host = entry.host
         return self._materialize(host, idx)
 
     def decode_sample(self, data: bytes) -> dict[str, Any]:
@@ -371,12 +462,13 @@ class MDSReader(JointReader):
 
 
 def reader_from_json(dirname: str, split: Optional[str], obj: dict[str, Any],
-                     device: Union[str, torch.device, None] = None) -> MDSReader:
+                     device: Union[str, torch.device, None] = None,
+                     cache: Optional[DecodedShardCache] = None) -> MDSReader:
     """Reader for an index.json shard entry (format/__init__.py:29-42); MDS only."""
     assert obj['version'] == 2
     if obj['format'] != 'mds':
         raise ValueError(f'streaming_amd decodes MDS shards only, got format {obj["format"]!r}')
-    return MDSReader.from_json(dirname, split, obj, device=device)
+    return MDSReader.from_json(dirname, split, obj, device=device, cache=cache)
 
 
 def load_index(dirname: str, split: Optional[str] = None) -> dict[str, Any]:

@@ -76,7 +76,8 @@ def test_global_shards_independent_of_rank_split():
 
 
 def test_full_size_config_c_columns_are_64mib_shards():
-    cols, counts = var_c_columns_on_device([7])
+    parts, counts = var_c_columns_on_device([7])
+    cols = parts[0]
     names, encs, sizes = _schema(CONFIG_C)
     config = shard_config_bytes(names, encs, sizes, None, [], 1 << 26)
     b_len = torch.diff(cols['b'].offsets)
