@@ -112,6 +112,11 @@ int mdsx_plan_num_var(const mdsx_plan* plan);
  * Tile t of shard s covers rows
  * [(t - tile0) * tile_rows, ...) of that shard; a shard has ceil(samples / tile_rows) tiles. */
 int mdsx_plan_tile_rows(const mdsx_plan* plan);
+/* Rows per tile the decoder wants for a batch of `rows` samples in `shard_bytes` bytes of shard
+ * files (set as mdsx_batch.tile_rows and used to build its tile table). Ragged plans: sized so
+ * that a tile's samples fill about half of the LDS stage of the staged decode (a power of two
+ * in [1, 256]); all-fixed plans: mdsx_plan_tile_rows. */
+int mdsx_plan_tile_rows_for(const mdsx_plan* plan, uint64_t shard_bytes, uint64_t rows);
 /* Rows per tile of the encoder's batches (mdsx_encode_shards): its tile table is built with
  * this, not with mdsx_plan_tile_rows. */
 int mdsx_plan_encode_tile_rows(const mdsx_plan* plan);
@@ -136,6 +141,9 @@ typedef struct mdsx_batch {
   int32_t nshards;
   uint32_t ntiles;
   uint64_t rows;                  /* rows of the batch (sum of samples)                          */
+  uint32_t tile_rows;             /* rows per tile of this batch's tile table (a power of two
+                                     <= 256); 0 = mdsx_plan_tile_rows(plan)                       */
+  uint32_t reserved;
 } mdsx_batch;
 
 /* ---- workspace ----------------------------------------------------------------------------- */

@@ -20,22 +20,23 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from streaming_amd.decoder import BatchDecoder, DeviceBatch, Plan, _tables, output_bytes  # noqa
-from streaming_amd.synth import fixed_b_batch_on_device, var_c_shards  # noqa
+from streaming_amd.synth import fixed_b_batch_on_device, var_c_batch_on_device  # noqa
 
 
 def retile(batch: DeviceBatch, plan: Plan) -> DeviceBatch:
-    raw, tile_shard, row0, rows, tiles = _tables(batch.sizes, batch.samples, batch.offsets,
-                                                 plan.tile_rows)
+    tr = plan.tile_rows_for(batch.shard_bytes, batch.total_rows)
+    raw, tile_shard, row0, rows, tiles = _tables(batch.sizes, batch.samples, batch.offsets, tr)
     dev = batch.device
     return DeviceBatch(batch.buffer, torch.from_numpy(raw).to(dev),
                        torch.from_numpy(tile_shard).to(dev), batch.offsets, batch.sizes,
-                       batch.samples, row0, tiles, rows, plan.tile_rows)
+                       batch.samples, row0, tiles, rows, tr)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--config', default='B')
-    ap.add_argument('--samples', type=int, default=1_000_000)
+    ap.add_argument('--samples', type=int, default=1_000_000, help='config B samples')
+    ap.add_argument('--shards', type=int, default=64, help='config C: full 64 MiB shards')
     ap.add_argument('--rounds', type=int, default=5)
     ap.add_argument('--iters', type=int, default=10)
     ap.add_argument('--variants', nargs='+', default=['tile=256'])
@@ -49,12 +50,12 @@ def main():
                                            [4, 4096])
         src = synth.sources
     else:
-        from streaming_amd.decoder import stage_shards
         blob = tuple(int(x) for x in args.blob.split(','))
         chars = tuple(int(x) for x in args.chars.split(','))
-        shards, counts, src = var_c_shards(args.samples, seed=4, str_chars=chars, blob_bytes=blob)
+        synth = var_c_batch_on_device(list(range(args.shards)), seed=4, str_chars=chars,
+                                      blob_bytes=blob)
         names = (['b', 'n', 's'], ['bytes', 'int', 'str'], [None, 8, None])
-        base_batch = stage_shards(shards, counts, Plan(*names))
+        base_batch, src = synth.batch, synth.sources
     decs = {}
     for v in args.variants:
         # 'enc=a|b|c' overrides the column encodings (e.g. read a str column as bytes)
@@ -70,11 +71,12 @@ def main():
             assert torch.equal(out['x'].view(torch.int32), src['x'].view(torch.int32)), v
             assert torch.equal(out['id'], src['id']), v
         else:
-            assert np.array_equal(out['b'].values.cpu().numpy(), src['b_pool']), v
-            assert np.array_equal(out['s'].values.cpu().numpy(), src['s_pool']), v
+            for name in ('b', 's'):
+                assert torch.equal(out[name].values, src[name].values), (v, name)
+                assert torch.equal(out[name].offsets, src[name].offsets), (v, name)
             if out['s'].flags is not None:
                 assert int(out['s'].flags.sum()) == 0, v
-            assert np.array_equal(out['n'].cpu().numpy(), src['n']), v
+            assert torch.equal(out['n'], src['n']), v
         decs[v] = dec
     R = base_batch.shard_bytes
     W = output_bytes(decs[args.variants[0]].plan, decs[args.variants[0]].result())
@@ -112,7 +114,8 @@ def main():
         ms = float(np.median(ts))
         nbytes = 2 * base_batch.buffer.numel() if v in ('torch_copy', 'mdsx_copy_probe') else R + W
         res[v] = {'median_ms': ms, 'min_ms': float(np.min(ts)), 'GBps': nbytes / ms / 1e6}
-    print(json.dumps({'config': args.config, 'R': R, 'W': W, 'results': res}, indent=1))
+    print(json.dumps({'config': args.config, 'blob': args.blob, 'chars': args.chars, 'R': R,
+                      'W': W, 'rows': base_batch.total_rows, 'results': res}, indent=1))
 
 
 if __name__ == '__main__':

@@ -51,6 +51,7 @@ EXPORTED_SYMBOLS = (
     'mdsx_plan_num_columns',
     'mdsx_plan_num_var',
     'mdsx_plan_tile_rows',
+    'mdsx_plan_tile_rows_for',
     'mdsx_plan_column',
     'mdsx_plan_is_safe',
     'mdsx_workspace_bytes',
@@ -104,7 +105,8 @@ class Batch(ctypes.Structure):
     """``mdsx_batch``."""
     _fields_ = [('data', ctypes.c_void_p), ('bytes', ctypes.c_uint64), ('shards', ctypes.c_void_p),
                 ('tile_shard', ctypes.c_void_p), ('nshards', ctypes.c_int32),
-                ('ntiles', ctypes.c_uint32), ('rows', ctypes.c_uint64)]
+                ('ntiles', ctypes.c_uint32), ('rows', ctypes.c_uint64),
+                ('tile_rows', ctypes.c_uint32), ('reserved', ctypes.c_uint32)]
 
 
 class Status(ctypes.Structure):
@@ -120,7 +122,7 @@ class Segment(ctypes.Structure):
 
 assert ctypes.sizeof(ShardDesc) == 32
 assert ctypes.sizeof(ColumnOut) == 32
-assert ctypes.sizeof(Batch) == 48
+assert ctypes.sizeof(Batch) == 56
 
 _here = os.path.dirname(os.path.abspath(__file__))
 lib_path = os.path.join(_here, 'lib', 'libmdsx.so')
@@ -150,6 +152,8 @@ def _declare(handle: ctypes.CDLL) -> None:
         fn = getattr(handle, name)
         fn.restype = c_int
         fn.argtypes = [vp]
+    handle.mdsx_plan_tile_rows_for.restype = c_int
+    handle.mdsx_plan_tile_rows_for.argtypes = [vp, c_u64, c_u64]
     handle.mdsx_plan_column.restype = c_int
     handle.mdsx_plan_column.argtypes = [
         vp, c_int,

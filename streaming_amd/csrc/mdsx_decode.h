@@ -1,0 +1,133 @@
+// Decode-side structures shared by the decode kernels of libmdsx.so (mdsx_kernels.hip: scan,
+// register-copy decode, gather; mdsx_stage.hip: the LDS-staged decode of ragged plans): the
+// kernel argument block, the per-tile view of a shard and the block-wide scan.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "mdsx_device.h"
+#include "mdsx_internal.h"
+
+namespace mdsx_kernels {
+
+constexpr int kBlock = 256;                     // 4 waves
+constexpr int kSmallMax = 16;                   // fixed columns <= 16 B: one row per lane
+constexpr uint64_t kMapGrain = uint64_t(kBlock) * 16;  // 4 KiB: row-map granule of ragged outputs
+constexpr int kGatherRows = 1024;               // rows of a gather tile staged in LDS
+constexpr int kGroupUnroll = 2;                 // chunks per lane in flight in group_copy
+
+struct DevCol {
+  void* data;
+  int64_t* offsets;
+  uint8_t* flags;
+  uint64_t capacity;
+  uint32_t row_bytes;
+  int8_t kind;
+  int8_t var_index;
+  int8_t gather;  // ragged column copied by gather_ragged_kernel (short rows) instead of waves
+  int8_t group;   // ragged column of medium rows: four rows per wave (group_copy)
+};
+
+struct DevArgs {
+  const uint8_t* batch;
+  const mdsx_shard_desc* shards;
+  const uint32_t* tile_shard;
+  mdsx_status* status;
+  int64_t* tile_total;   // [nvar][nscan] ragged bytes of each scan block (scan_per tiles)
+  int64_t* tile_prefix;  // [nvar][nscan] their exclusive prefix
+  int64_t* totals;       // [nvar] or null
+  uint64_t* src_abs;     // [nvar][rows]  byte index into the batch of each row's ragged value
+  uint32_t* row_map;     // [nvar][map_len] first row of every gather tile
+  uint64_t* lookback;    // [nvar][ntiles] single-pass look-back status words
+  uint32_t* ticket;      // single-pass tile ticket counter
+  uint64_t map_len;
+  uint64_t rows;
+  uint32_t ntiles;
+  uint32_t nscan;     // scan blocks: ceil(ntiles / scan_per)
+  uint32_t scan_per;  // tiles per scan block (kBlock / tile_rows)
+  int32_t nshards;
+  int32_t ncols;
+  int32_t nvar;
+  int32_t tile_rows;
+  int16_t any_group;     // some ragged column uses group_copy
+  int16_t any_wave_str;  // some str column is copied by decode_kernel (validated there)
+  int16_t any_wave_ragged;  // some ragged column is copied one row per wave
+  int16_t str_cached;  // plan->str_cached
+  uint32_t stage_bytes;  // LDS stage of the staged decode (bytes, multiple of 1 KiB)
+  uint32_t gather_block0[MDSX_MAX_COLUMNS + 1];  // first gather workgroup of each ragged column
+  DevCol cols[MDSX_MAX_COLUMNS];
+};
+
+
+// Per-shard facts shared by the scan and decode kernels.
+struct TileView {
+  const uint8_t* shard;
+  const uint32_t* offs;  // offsets table (absolute file offsets), 4-byte aligned
+  mdsx_shard_desc d;
+  uint32_t shard_idx;
+  uint32_t r0;     // first row (inside the shard) of this tile
+  uint32_t nrows;  // rows of this tile
+  uint64_t hdr_end;
+  bool table_ok;   // the offsets table of `samples` rows fits in the file
+};
+
+__device__ __forceinline__ TileView tile_view(const DevArgs& a, uint32_t tile) {
+  TileView v;
+  v.shard_idx = a.tile_shard[tile];
+  v.d = a.shards[v.shard_idx];
+  v.shard = a.batch + v.d.offset;
+  v.offs = reinterpret_cast<const uint32_t*>(v.shard + 4);
+  v.r0 = (tile - v.d.tile0) * uint32_t(a.tile_rows);
+  v.nrows = v.d.samples > v.r0 ? min(uint32_t(a.tile_rows), v.d.samples - v.r0) : 0u;
+  v.hdr_end = 4ull + 4ull * (uint64_t(v.d.samples) + 1ull);
+  v.table_ok = v.hdr_end <= v.d.bytes;
+  return v;
+}
+
+// Range of sample i of the shard (mds/reader.py:137-142) and its validity. A sample with zero
+// bytes is the reference's IndexError (mds/reader.py:145-148).
+__device__ __forceinline__ int sample_range(const TileView& v, uint32_t i, uint32_t* b,
+                                            uint32_t* e) {
+  *b = v.offs[i];
+  *e = v.offs[i + 1];
+  if (!(v.hdr_end <= *b && *b <= *e && *e <= v.d.bytes)) return MDSX_E_BOUNDS;
+  if (*b == *e) return MDSX_E_EMPTY;
+  return MDSX_OK;
+}
+
+// Exclusive scan over the 256 threads of the block; *total gets the block sum.
+__device__ __forceinline__ int64_t block_exclusive_scan(int64_t x, int64_t* s_wsum,
+                                                        int64_t* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t incl = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) s_wsum[w] = incl;
+  __syncthreads();
+  int64_t base = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < kBlock / 64; ++k) {
+    const int64_t s = s_wsum[k];
+    base += (k < w) ? s : 0;
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + incl - x;
+}
+
+
+// Byte offset, inside the workspace's 256-byte status block, of the staged decode's count of
+// huge rows (listed in the src_abs region; mdsx_stage.hip).
+constexpr uint64_t kHugeCountOffset = 192;
+
+// The LDS-staged decode of a ragged plan (mdsx_stage.hip): every column of every row of a tile
+// from the tile's shard bytes staged once in LDS. Returns MDSX_OK or a launch error.
+int launch_stage_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s);
+
+}  // namespace mdsx_kernels

@@ -56,6 +56,46 @@ __device__ __forceinline__ void st16(uint64_t addr, const uint4 v) {
   }
 }
 
+// One global_load_lds_dwordx4: 16 bytes per lane from gsrc (per-lane address) into LDS at
+// lds + 16 * lane (lds wave-uniform). Issued from inline asm, so the compiler neither counts nor
+// waits for it: the issuing wave waits with an explicit s_waitcnt vmcnt (and a barrier orders
+// other waves' reads behind that wait).
+template <bool kNT>
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds) {
+  const uint32_t lds_dst = __builtin_amdgcn_readfirstlane(lds);  // wave-uniform by construction
+  uint32_t keep;
+  if constexpr (kNT)
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(lds_dst)
+        : "memory");
+  else
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(lds_dst)
+        : "memory");
+}
+
+// s_waitcnt vmcnt(m) for the largest listed m <= n (a smaller count only waits longer).
+__device__ __forceinline__ void wait_vm_at_most(uint32_t n) {
+  if (n >= 48) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+  else if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+  else if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (n >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if (n >= 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 __device__ __forceinline__ uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t r) {
   return __builtin_amdgcn_alignbyte(hi, lo, r);
 }

@@ -36,118 +36,11 @@
 #include <cstdint>
 #include <cstring>
 
+#include "mdsx_decode.h"
 #include "mdsx_device.h"
 #include "mdsx_internal.h"
 
 namespace mdsx_kernels {
-
-constexpr int kBlock = 256;                     // 4 waves
-constexpr int kSmallMax = 16;                   // fixed columns <= 16 B: one row per lane
-constexpr uint64_t kMapGrain = uint64_t(kBlock) * 16;  // 4 KiB: row-map granule of ragged outputs
-constexpr int kGatherRows = 1024;               // rows of a gather tile staged in LDS
-constexpr int kGroupUnroll = 2;                 // chunks per lane in flight in group_copy
-
-struct DevCol {
-  void* data;
-  int64_t* offsets;
-  uint8_t* flags;
-  uint64_t capacity;
-  uint32_t row_bytes;
-  int8_t kind;
-  int8_t var_index;
-  int8_t gather;  // ragged column copied by gather_ragged_kernel (short rows) instead of waves
-  int8_t group;   // ragged column of medium rows: four rows per wave (group_copy)
-};
-
-struct DevArgs {
-  const uint8_t* batch;
-  const mdsx_shard_desc* shards;
-  const uint32_t* tile_shard;
-  mdsx_status* status;
-  int64_t* tile_total;   // [nvar][nscan] ragged bytes of each scan block (scan_per tiles)
-  int64_t* tile_prefix;  // [nvar][nscan] their exclusive prefix
-  int64_t* totals;       // [nvar] or null
-  uint64_t* src_abs;     // [nvar][rows]  byte index into the batch of each row's ragged value
-  uint32_t* row_map;     // [nvar][map_len] first row of every gather tile
-  uint64_t* lookback;    // [nvar][ntiles] single-pass look-back status words
-  uint32_t* ticket;      // single-pass tile ticket counter
-  uint64_t map_len;
-  uint64_t rows;
-  uint32_t ntiles;
-  uint32_t nscan;     // scan blocks: ceil(ntiles / scan_per)
-  uint32_t scan_per;  // tiles per scan block (kBlock / tile_rows)
-  int32_t nshards;
-  int32_t ncols;
-  int32_t nvar;
-  int32_t tile_rows;
-  int16_t any_group;     // some ragged column uses group_copy
-  int16_t any_wave_str;  // some str column is copied by decode_kernel (validated there)
-  int16_t any_wave_ragged;  // some ragged column is copied one row per wave
-  int16_t str_cached;  // plan->str_cached
-  uint32_t gather_block0[MDSX_MAX_COLUMNS + 1];  // first gather workgroup of each ragged column
-  DevCol cols[MDSX_MAX_COLUMNS];
-};
-
-
-// Per-shard facts shared by the scan and decode kernels.
-struct TileView {
-  const uint8_t* shard;
-  const uint32_t* offs;  // offsets table (absolute file offsets), 4-byte aligned
-  mdsx_shard_desc d;
-  uint32_t shard_idx;
-  uint32_t r0;     // first row (inside the shard) of this tile
-  uint32_t nrows;  // rows of this tile
-  uint64_t hdr_end;
-  bool table_ok;   // the offsets table of `samples` rows fits in the file
-};
-
-__device__ __forceinline__ TileView tile_view(const DevArgs& a, uint32_t tile) {
-  TileView v;
-  v.shard_idx = a.tile_shard[tile];
-  v.d = a.shards[v.shard_idx];
-  v.shard = a.batch + v.d.offset;
-  v.offs = reinterpret_cast<const uint32_t*>(v.shard + 4);
-  v.r0 = (tile - v.d.tile0) * uint32_t(a.tile_rows);
-  v.nrows = v.d.samples > v.r0 ? min(uint32_t(a.tile_rows), v.d.samples - v.r0) : 0u;
-  v.hdr_end = 4ull + 4ull * (uint64_t(v.d.samples) + 1ull);
-  v.table_ok = v.hdr_end <= v.d.bytes;
-  return v;
-}
-
-// Range of sample i of the shard (mds/reader.py:137-142) and its validity. A sample with zero
-// bytes is the reference's IndexError (mds/reader.py:145-148).
-__device__ __forceinline__ int sample_range(const TileView& v, uint32_t i, uint32_t* b,
-                                            uint32_t* e) {
-  *b = v.offs[i];
-  *e = v.offs[i + 1];
-  if (!(v.hdr_end <= *b && *b <= *e && *e <= v.d.bytes)) return MDSX_E_BOUNDS;
-  if (*b == *e) return MDSX_E_EMPTY;
-  return MDSX_OK;
-}
-
-// Exclusive scan over the 256 threads of the block; *total gets the block sum.
-__device__ __forceinline__ int64_t block_exclusive_scan(int64_t x, int64_t* s_wsum,
-                                                        int64_t* total) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int64_t incl = x;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int64_t y = __shfl_up(incl, o);
-    if (lane >= o) incl += y;
-  }
-  if (lane == 63) s_wsum[w] = incl;
-  __syncthreads();
-  int64_t base = 0, tot = 0;
-#pragma unroll
-  for (int k = 0; k < kBlock / 64; ++k) {
-    const int64_t s = s_wsum[k];
-    base += (k < w) ? s : 0;
-    tot += s;
-  }
-  __syncthreads();
-  *total = tot;
-  return base + incl - x;
-}
 
 // ---------------------------------------------------------------------------------------------
 // Pass 1a: per-row ragged lengths -> block-local exclusive offsets + per-block totals.
@@ -251,42 +144,6 @@ __global__ __launch_bounds__(kBlock) void scan_totals_kernel(const DevArgs a) {
 // this wave issued after the slot's DMA (DMAs, and stores certain to issue; any other store
 // only makes the wait stricter). Only the issuing wave reads its slots, so its vmcnt orders the
 // reads (MI355X_MICROARCH.md: nothing else orders a ds_read behind a pending LDS-DMA).
-template <bool kNT>
-__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds) {
-  const uint32_t lds_dst = __builtin_amdgcn_readfirstlane(lds);  // wave-uniform by construction
-  uint32_t keep;
-  if constexpr (kNT)
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(gsrc), "s"(lds_dst)
-        : "memory");
-  else
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(gsrc), "s"(lds_dst)
-        : "memory");
-}
-
-// s_waitcnt vmcnt(m) for the largest listed m <= n (a smaller count only waits longer).
-__device__ __forceinline__ void wait_vm_at_most(uint32_t n) {
-  if (n >= 48) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
-  else if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-  else if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-  else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if (n >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-  else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else if (n >= 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
 // One long-row job of a wave: row r of ragged column c, as aligned 16-byte chunks.
 struct RingJob {
   const uint4* sal;  // first aligned source chunk
@@ -973,12 +830,16 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   a->totals = d_totals;
   a->rows = b->rows;
   a->ntiles = b->ntiles;
-  a->scan_per = plan->tile_rows > 0 && plan->tile_rows <= kBlock ? uint32_t(kBlock / plan->tile_rows) : 1u;
+  const int tr = b->tile_rows ? int(b->tile_rows) : plan->tile_rows;
+  if (tr < 1 || tr > kBlock || (tr & (tr - 1)))
+    return mdsx::fail(MDSX_E_ARG, "mdsx: batch tile_rows must be a power of two in [1, 256]");
+  a->scan_per = uint32_t(kBlock / tr);
   a->nscan = (b->ntiles + a->scan_per - 1) / a->scan_per;
   a->nshards = b->nshards;
   a->ncols = plan->ncols;
   a->nvar = plan->nvar;
-  a->tile_rows = plan->tile_rows;
+  a->tile_rows = tr;
+  a->stage_bytes = uint32_t(plan->stage_kb) * 1024u;
   uint32_t gblocks = 0;
   const uint64_t tile = kMapGrain * uint64_t(plan->gather_chunks);
   for (int c = 0; c < plan->ncols; ++c) {
@@ -1326,8 +1187,9 @@ int mdsx_scan_shards(const mdsx_plan* plan, const mdsx_batch* batch, const mdsx_
 static int launch_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s, bool single,
                          const uint64_t* mode_bytes) {
   int rc = MDSX_OK;
+  if (plan->nvar > 0 && !single && a.stage_bytes > 0) return launch_stage_decode(plan, a, s);
   const size_t lds =
-      size_t(plan->tile_rows) * (12 * size_t(plan->nvar) + 4 * size_t(plan->ncols) + 1) + 16;
+      size_t(a.tile_rows) * (12 * size_t(plan->nvar) + 4 * size_t(plan->ncols) + 1) + 16;
   const bool nt = plan->nontemporal != 0, ragged = plan->nvar > 0;
   // Edge (partial 16-byte chunk) stores are only needed for ragged columns and for large fixed
   // columns whose row size is not a multiple of 16 (outputs are 256-byte aligned).

@@ -5,6 +5,7 @@
 // _get_static_size (encodings.py:148-193) and the fixed/variable column split that
 // MDSReader.decode_sample does per sample (mds/reader.py:111-118). The reference re-parses the
 // encoding string for every column of every sample; here it is parsed once per schema.
+#include <algorithm>
 #include <cctype>
 #include <cstdint>
 #include <cstdlib>
@@ -200,6 +201,10 @@ void apply_tuning(mdsx_plan* p) {
       p->str_cached = v ? 1 : 0;
     } else if (key == "ring" && (v == 0 || v == 4 || v == 6 || v == 8)) {
       p->ring_slots = int(v);
+    } else if (key == "stage" && v >= 0 && v <= 96) {
+      p->stage_kb = int(v);
+    } else if (key == "fill" && v >= 10 && v <= 100) {
+      p->stage_fill = int(v);
     }
   }
 }
@@ -296,6 +301,9 @@ int mdsx_plan_create(const char* const* encodings, const int64_t* column_sizes, 
   // output hits L2 instead of HBM: config C 1.94-2.01 vs 2.06-2.10 ms; 1-3 KiB blobs + 200-400-
   // code-point strings 1.51 vs 1.56 ms (tune/strc_*.json).
   p->str_cached = 1;
+  // Ragged plans decode through the LDS stage (mdsx_stage.hip): each tile's shard bytes are read
+  // once, straight into LDS, and every column is written from there.
+  p->stage_kb = p->nvar > 0 ? 32 : 0;
   apply_tuning(p);
   *out = p;
   return MDSX_OK;
@@ -308,6 +316,16 @@ int mdsx_plan_num_columns(const mdsx_plan* plan) { return plan ? plan->ncols : M
 int mdsx_plan_num_var(const mdsx_plan* plan) { return plan ? plan->nvar : MDSX_E_ARG; }
 
 int mdsx_plan_tile_rows(const mdsx_plan* plan) { return plan ? plan->tile_rows : MDSX_E_ARG; }
+
+int mdsx_plan_tile_rows_for(const mdsx_plan* plan, uint64_t shard_bytes, uint64_t rows) {
+  if (!plan) return MDSX_E_ARG;
+  if (plan->nvar == 0 || plan->stage_kb == 0 || rows == 0) return plan->tile_rows;
+  const uint64_t target = uint64_t(plan->stage_kb) * 1024 * uint64_t(plan->stage_fill) / 100;
+  const uint64_t per_row = std::max<uint64_t>(1, shard_bytes / rows);
+  int tr = 1;
+  while (tr < 256 && uint64_t(tr) * 2 * per_row <= target) tr *= 2;
+  return tr;
+}
 
 int mdsx_plan_encode_tile_rows(const mdsx_plan* plan) {
   return plan ? plan->encode_tile_rows : MDSX_E_ARG;

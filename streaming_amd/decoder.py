@@ -133,6 +133,13 @@ class Plan:
     def names(self) -> list[str]:
         return [c.name for c in self.columns]
 
+    def tile_rows_for(self, shard_bytes: int, rows: int) -> int:
+        """Rows per tile of a decode batch of ``rows`` samples in ``shard_bytes`` bytes of shard
+        files (``mdsx_plan_tile_rows_for``: ragged plans size tiles to the LDS stage)."""
+        tr = int(self._lib.mdsx_plan_tile_rows_for(self._handle, int(shard_bytes), int(rows)))
+        _check(min(tr, 0), 'mdsx_plan_tile_rows_for')
+        return tr
+
     def workspace_bytes(self, batch: 'DeviceBatch') -> int:
         return int(self._lib.mdsx_workspace_bytes(self._handle, ctypes.byref(batch.abi())))
 
@@ -191,6 +198,7 @@ class DeviceBatch:
         b.nshards = self.nshards
         b.ntiles = self.ntiles
         b.rows = self.total_rows
+        b.tile_rows = self.tile_rows
         return b
 
 
@@ -234,12 +242,13 @@ def make_batch(plan: Plan,
     sizes = [int(x) for x in sizes]
     offsets, total = _layout(sizes)
     buffer = torch.zeros(total, dtype=torch.uint8, device=device)
-    raw, tile_shard, row0, rows, tiles = _tables(sizes, samples, offsets, plan.tile_rows)
+    tr = plan.tile_rows_for(sum(sizes), sum(int(n) for n in samples))
+    raw, tile_shard, row0, rows, tiles = _tables(sizes, samples, offsets, tr)
     descs = torch.from_numpy(raw).to(device)
     tiles_t = torch.from_numpy(tile_shard).to(device) if tiles else torch.zeros(
         1, dtype=torch.int32, device=device)
     return DeviceBatch(buffer, descs, tiles_t, offsets, sizes, [int(n) for n in samples], row0,
-                       tiles, rows, plan.tile_rows)
+                       tiles, rows, tr)
 
 
 def stage_shards(shards: Sequence[Union[bytes, bytearray, memoryview, np.ndarray, torch.Tensor]],
@@ -474,8 +483,6 @@ class BatchDecoder:
 
     def __init__(self, plan: Plan, batch: DeviceBatch,
                  capacities: Optional[dict[str, int]] = None, single: bool = False) -> None:
-        if plan.tile_rows != batch.tile_rows:
-            raise ValueError('batch was staged for a different tile size')
         _native.check_fork()
         self.plan = plan
         self.batch = batch

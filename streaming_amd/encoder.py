@@ -94,15 +94,15 @@ class EncodedBatch:
         """The encoded shards as a decode batch of ``plan`` (same buffer, the tile table rebuilt
         for the decoder's tile size)."""
         b = self.batch
-        if b.tile_rows == plan.tile_rows:
+        tr = plan.tile_rows_for(sum(b.sizes), sum(b.samples))
+        if b.tile_rows == tr:
             return b
-        raw, tile_shard, row0, rows, tiles = _tables(b.sizes, b.samples, b.offsets,
-                                                     plan.tile_rows)
+        raw, tile_shard, row0, rows, tiles = _tables(b.sizes, b.samples, b.offsets, tr)
         dev = b.device
         return DeviceBatch(b.buffer, torch.from_numpy(raw).to(dev),
                            torch.from_numpy(tile_shard).to(dev) if tiles else torch.zeros(
                                1, dtype=torch.int32, device=dev), b.offsets, b.sizes, b.samples,
-                           row0, tiles, rows, plan.tile_rows)
+                           row0, tiles, rows, tr)
 
 
 def _row_count(plan: Plan, columns: dict[str, Column]) -> int:

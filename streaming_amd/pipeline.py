@@ -176,15 +176,16 @@ class ShardPipeline:
         return futs, sizes, offsets, total
 
     def _batch(self, slot: _Slot, group, sizes, offsets, total) -> DeviceBatch:
-        raw, tile_shard, row0, rows, tiles = _tables(sizes, [s.samples for s in group], offsets,
-                                                     self.plan.tile_rows)
+        samples = [s.samples for s in group]
+        tr = self.plan.tile_rows_for(sum(sizes), sum(samples))
+        raw, tile_shard, row0, rows, tiles = _tables(sizes, samples, offsets, tr)
         dev = self.device
         # small tables: pinned + async on the compute stream (no host wait on the device)
         descs = torch.from_numpy(raw).pin_memory().to(dev, non_blocking=True)
         tiles_t = (torch.from_numpy(tile_shard).pin_memory().to(dev, non_blocking=True)
                    if tiles else torch.zeros(1, dtype=torch.int32, device=dev))
-        return DeviceBatch(slot.dev[:total], descs, tiles_t, offsets, sizes,
-                           [s.samples for s in group], row0, tiles, rows, self.plan.tile_rows)
+        return DeviceBatch(slot.dev[:total], descs, tiles_t, offsets, sizes, samples, row0, tiles,
+                           rows, tr)
 
     def __iter__(self) -> Iterator[DecodedBatch]:
         """Decoded batches in order (device tensors, valid until the slot is reused ``depth``

@@ -211,7 +211,9 @@ def var_c_columns_on_device(shard_ids: list[int],
 def var_c_batch_on_device(shard_ids: list[int],
                           seed: int = 2000,
                           size_limit: int = 1 << 26,
-                          device: Union[str, torch.device, None] = None) -> SynthShards:
+                          device: Union[str, torch.device, None] = None,
+                          str_chars: tuple[int, int] = (16, 256),
+                          blob_bytes: tuple[int, int] = (3072, 5120)) -> SynthShards:
     """Config C shards (``shard_ids`` of a dataset of full shards, see
     :func:`var_c_columns_on_device`) written by the device MDS encoder into one decode batch."""
     from streaming_amd.decoder import stage_shards
@@ -219,7 +221,8 @@ def var_c_batch_on_device(shard_ids: list[int],
     names, encs, sizes = _schema(CONFIG_C)
     plan = Plan(names, encs, sizes)
     config = shard_config_bytes(names, encs, sizes, None, [], size_limit)
-    parts, counts = var_c_columns_on_device(shard_ids, seed, size_limit, device)
+    parts, counts = var_c_columns_on_device(shard_ids, seed, size_limit, device, str_chars,
+                                            blob_bytes)
     files = []
     for cols, n in zip(parts, counts):
         enc, consumed = encode_batch(plan, cols, config, size_limit)

@@ -1,7 +1,13 @@
 """GPU parity of every ragged-column copy mode of the decoder, each forced through the
-measurement knobs (MDSX_TUNE, read at plan creation): destination-major gather kernel
-(short rows), four rows per wave in 16-lane groups (medium rows), one row per wave (long rows),
-the last either from registers or through the per-wave LDS-DMA ring (8 or 4 slots).
+measurement knobs (MDSX_TUNE, read at plan creation).
+
+* The LDS-staged decode (the default for ragged plans, mdsx_stage.hip) at its default stage, with
+  tiles overflowing a small stage (several row groups per tile), with a 1 KiB stage (most rows
+  larger than the stage: the huge-row kernel) and with a large stage (long tiles).
+* The register-copy decode (stage=0): destination-major gather kernel (short rows), four rows
+  per wave in 16-lane groups (medium rows), one row per wave (long rows), the last either from
+  registers or through the per-wave LDS-DMA ring (8 or 4 slots).
+
 Whatever mode a column gets, the bytes, offsets and UTF-8 flags must equal the reference's.
 """
 
@@ -23,12 +29,16 @@ from tests.test_device_decode import _device_digests
 pytestmark = pytest.mark.gpu
 
 MODES = {
-    'gather': 'gmin=1000000000',
-    'group': 'gmin=0,gmax=1000000000',
-    'group_nt': 'gmin=0,gmax=1000000000,strc=0',  # str rows streamed (non-temporal) too
-    'wave': 'gmin=0,gmax=0,ring=0',
-    'ring': 'gmin=0,gmax=0,ring=8',   # one row per wave through the LDS-DMA ring
-    'ring4': 'gmin=0,gmax=0,ring=4',
+    'stage': '',  # the default
+    'stage_overflow': 'stage=4,fill=100',  # tiles of ~2x the stage: several row groups each
+    'stage_tiny': 'stage=1',  # rows over 1 KiB go through the huge-row kernel
+    'stage_big': 'stage=64,fill=90',
+    'gather': 'stage=0,gmin=1000000000',
+    'group': 'stage=0,gmin=0,gmax=1000000000',
+    'group_nt': 'stage=0,gmin=0,gmax=1000000000,strc=0',  # str rows streamed (non-temporal) too
+    'wave': 'stage=0,gmin=0,gmax=0,ring=0',
+    'ring': 'stage=0,gmin=0,gmax=0,ring=8',   # one row per wave through the LDS-DMA ring
+    'ring4': 'stage=0,gmin=0,gmax=0,ring=4',
 }
 
 

@@ -36,7 +36,7 @@ def test_struct_layouts():
     assert ctypes.sizeof(_native.ShardDesc) == 32
     assert ctypes.sizeof(_native.ColumnOut) == 32
     assert ctypes.sizeof(_native.Status) == 16
-    assert ctypes.sizeof(_native.Batch) == 48
+    assert ctypes.sizeof(_native.Batch) == 56
 
 
 @pytest.mark.parametrize('name', gu.ALL_SETS)
@@ -105,3 +105,16 @@ def test_workspace_bytes():
 def test_too_many_columns():
     with pytest.raises(ValueError):
         Plan([f'c{i}' for i in range(65)], ['int'] * 65, [8] * 65)
+
+
+def test_tile_rows_for_sizes_ragged_tiles_to_the_stage():
+    """Ragged plans: tiles of about half the 32 KiB LDS stage (power of two rows, 1..256);
+    all-fixed plans: the plan's tile size whatever the batch."""
+    from streaming_amd.decoder import Plan
+    c = Plan(['b', 'n', 's'], ['bytes', 'int', 'str'], [None, 8, None])
+    assert c.tile_rows_for(1 << 26, 15_700) == 4  # ~4.3 KB rows: 4-row tiles (~17 KB)
+    assert c.tile_rows_for(1 << 26, (1 << 26) // 100) == 128  # 100-byte rows
+    assert c.tile_rows_for(1 << 26, 10) == 1  # 6.7 MB rows: one per tile (huge-row kernel)
+    assert c.tile_rows_for(1 << 26, 1 << 26) == 256  # 1-byte rows: capped
+    b = Plan(['id', 'x'], ['int32', 'ndarray:float32:1024'], [4, 4096])
+    assert b.tile_rows_for(1 << 26, 16_352) == b.tile_rows
