@@ -55,7 +55,8 @@ struct DevArgs {
   int16_t any_wave_str;  // some str column is copied by decode_kernel (validated there)
   int16_t any_wave_ragged;  // some ragged column is copied one row per wave
   int16_t str_cached;  // plan->str_cached
-  uint32_t stage_bytes;  // LDS stage of the staged decode (bytes, multiple of 1 KiB)
+  uint32_t stage_bytes;  // each of the two LDS stage buffers of the staged decode (bytes, 1 KiB multiple)
+  uint32_t stage_tiles;  // tiles per workgroup of the staged decode
   uint32_t gather_block0[MDSX_MAX_COLUMNS + 1];  // first gather workgroup of each ragged column
   DevCol cols[MDSX_MAX_COLUMNS];
 };
@@ -126,8 +127,11 @@ __device__ __forceinline__ int64_t block_exclusive_scan(int64_t x, int64_t* s_ws
 // huge rows (listed in the src_abs region; mdsx_stage.hip).
 constexpr uint64_t kHugeCountOffset = 192;
 
-// The LDS-staged decode of a ragged plan (mdsx_stage.hip): every column of every row of a tile
-// from the tile's shard bytes staged once in LDS. Returns MDSX_OK or a launch error.
+// The LDS-staged decode of ragged plans (mdsx_stage.hip). Pass 1: the ragged bytes of every tile
+// (then scan_totals_kernel, one entry per tile: a.scan_per == 1). Pass 2: every column of every
+// row from each tile's shard bytes staged once in LDS. Return MDSX_OK or a launch error.
+int launch_stage_totals(const DevArgs& a, hipStream_t s);
 int launch_stage_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s);
+uint32_t stage_tiles_per_wg(uint32_t ntiles);
 
 }  // namespace mdsx_kernels

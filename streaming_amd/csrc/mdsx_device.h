@@ -80,6 +80,18 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds) {
         : "memory");
 }
 
+// One global_load_lds_dword: 4 bytes per lane from gsrc into LDS at lds + 4 * lane.
+__device__ __forceinline__ void glds4(const void* gsrc, uint32_t lds) {
+  const uint32_t lds_dst = __builtin_amdgcn_readfirstlane(lds);
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_dst)
+      : "memory");
+}
+
 // s_waitcnt vmcnt(m) for the largest listed m <= n (a smaller count only waits longer).
 __device__ __forceinline__ void wait_vm_at_most(uint32_t n) {
   if (n >= 48) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");

@@ -833,13 +833,15 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   const int tr = b->tile_rows ? int(b->tile_rows) : plan->tile_rows;
   if (tr < 1 || tr > kBlock || (tr & (tr - 1)))
     return mdsx::fail(MDSX_E_ARG, "mdsx: batch tile_rows must be a power of two in [1, 256]");
-  a->scan_per = uint32_t(kBlock / tr);
+  a->stage_bytes = plan->nvar > 0 ? uint32_t(plan->stage_kb) * 1024u : 0u;
+  a->stage_tiles = stage_tiles_per_wg(b->ntiles);
+  // the staged decode scans one total per tile; the register-copy decode one per 256 rows
+  a->scan_per = a->stage_bytes ? 1u : uint32_t(kBlock / tr);
   a->nscan = (b->ntiles + a->scan_per - 1) / a->scan_per;
   a->nshards = b->nshards;
   a->ncols = plan->ncols;
   a->nvar = plan->nvar;
   a->tile_rows = tr;
-  a->stage_bytes = uint32_t(plan->stage_kb) * 1024u;
   uint32_t gblocks = 0;
   const uint64_t tile = kMapGrain * uint64_t(plan->gather_chunks);
   for (int c = 0; c < plan->ncols; ++c) {
@@ -1171,7 +1173,10 @@ int mdsx_scan_shards(const mdsx_plan* plan, const mdsx_batch* batch, const mdsx_
   hipStream_t s = static_cast<hipStream_t>(stream);
   rc = hip_check(hipMemsetAsync(d_workspace, 0, sizeof(mdsx_status), s), "hipMemsetAsync");
   if (rc != MDSX_OK || plan->nvar == 0) return rc;
-  if (a.ntiles > 0) {
+  if (a.ntiles > 0 && a.stage_bytes) {
+    rc = launch_stage_totals(a, s);
+    if (rc != MDSX_OK) return rc;
+  } else if (a.ntiles > 0) {
     hipLaunchKernelGGL(scan_tiles_kernel, dim3(a.nscan), dim3(kBlock), 0, s, a);
     rc = hip_check(hipGetLastError(), "scan_tiles_kernel launch");
     if (rc != MDSX_OK) return rc;

@@ -203,7 +203,7 @@ void apply_tuning(mdsx_plan* p) {
       p->ring_slots = int(v);
     } else if (key == "stage" && v >= 0 && v <= 96) {
       p->stage_kb = int(v);
-    } else if (key == "fill" && v >= 10 && v <= 100) {
+    } else if (key == "fill" && v >= 10 && v <= 400) {  // > 100: tiles overflow the stage
       p->stage_fill = int(v);
     }
   }
@@ -302,8 +302,10 @@ int mdsx_plan_create(const char* const* encodings, const int64_t* column_sizes, 
   // code-point strings 1.51 vs 1.56 ms (tune/strc_*.json).
   p->str_cached = 1;
   // Ragged plans decode through the LDS stage (mdsx_stage.hip): each tile's shard bytes are read
-  // once, straight into LDS, and every column is written from there.
-  p->stage_kb = p->nvar > 0 ? 32 : 0;
+  // once, straight into LDS, and every column is written from there. Two stage buffers per
+  // workgroup (one decoded, one in flight).
+  p->stage_kb = p->nvar > 0 ? 24 : 0;
+  p->stage_fill = 70;
   apply_tuning(p);
   *out = p;
   return MDSX_OK;

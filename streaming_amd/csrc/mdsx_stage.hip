@@ -1,31 +1,38 @@
-// LDS-staged decode of ragged plans (gfx950): one workgroup per tile of rows, the tile's shard
-// bytes read from HBM ONCE, straight into LDS, then every column written from LDS.
+// LDS-staged decode of ragged plans (gfx950): each tile's shard bytes are read from HBM ONCE,
+// straight into LDS, and every column is written from there.
 //
 // The reference decodes one sample per call: MDSReader.get_sample_data reads the sample's byte
 // range (streaming/base/format/mds/reader.py:128-149), decode_sample splits it at the u32 size
 // heads of the variable columns and mds_decode returns each column's value
-// (mds/reader.py:103-126, encodings.py:62-397,760-773). Here a tile's samples are contiguous in the
-// shard file, so their bytes [begin(first row), end(last row)) are one range:
+// (mds/reader.py:103-126, encodings.py:62-397,760-773). Here the samples of a tile (a few rows,
+// sized by the host to about half the LDS stage: mdsx_plan_tile_rows_for) are contiguous in the
+// shard file, so their bytes are one range.
 //
-//   1. offsets pairs of the tile's rows (mds/reader.py:137-142), checked against the file;
-//      final ragged output offsets = the scan pass's prefix + its tile-local offset;
-//   2. the rows are cut into groups whose byte range fits the LDS stage (normally one group per
-//      tile: the host sizes tiles to about half the stage, mdsx_plan_tile_rows_for); each group's
-//      range is fetched with global_load_lds_dwordx4 (1 KiB per wave-instruction, no VGPRs), so
-//      the column boundaries inside a sample, the heads and the str bytes re-read by the UTF-8
-//      check cost no second HBM read;
-//   3. size heads parsed from LDS (decode_sample's head loop), every column range checked;
-//   4. each column written destination-major: lane k of the workgroup owns 16-byte-aligned output
-//      chunk k of the group's contiguous output range of that column (fixed columns: rows x size;
-//      ragged: the packed values), assembled from the LDS bytes of the row(s) it covers (two
-//      aligned ds_read_b128 + v_alignbyte; binary search of the row), stored whole -- so every
-//      store is a full, coalesced 16-byte store except the two chunks a group shares with its
-//      neighbours (byte stores);
-//   5. str rows checked for strict UTF-8 from LDS (what bytes.decode('utf-8') accepts,
+// Pass 1 (stage_totals_kernel): the ragged bytes of every tile from the offsets table and the u32
+// size heads, then scan_totals_kernel (mdsx_kernels.hip) turns them into each tile's output base.
+//
+// Pass 2 (stage_decode_kernel): a workgroup runs a software pipeline over a run of consecutive
+// tiles. Wave 0 is the loader: while the four waves decode tile k from one LDS stage buffer, the
+// shard bytes of tile k + 1 are already in flight into the other (global_load_lds_dwordx4: 1 KiB
+// per wave-instruction, no VGPRs) and the offsets-table slice and output bases of tile k + 2 into
+// a third metadata slot (global_load_lds_dword). The loads are issued from inline asm, invisible
+// to the compiler, and retired by one explicit `s_waitcnt vmcnt(0)` + barrier per tile. For tile k:
+//
+//   1. each row's offsets pair (mds/reader.py:137-142) checked against the file, its size heads
+//      and column ranges parsed from LDS (decode_sample's head loop, mds/reader.py:111-125);
+//   2. ragged output offsets = the tile's base + an exclusive scan of the rows' lengths;
+//   3. every column written destination-major: lane k of the workgroup owns 16-byte-aligned output
+//      chunk k of the tile's contiguous output range of that column (fixed columns: rows x size;
+//      ragged: packed values), assembled from the LDS bytes of the row(s) it covers (two aligned
+//      ds_read_b128 + v_alignbyte; the row by binary search), stored whole -- every store is a
+//      full, coalesced 16-byte store except the two chunks a tile shares with its neighbours;
+//   4. str rows checked for strict UTF-8 from LDS (what bytes.decode('utf-8') accepts,
 //      encodings.py:80-81), four rows per wave, one per 16-lane group.
 //
-// A sample larger than the stage is copied straight from HBM (wave_copy, the 16-byte realigning
-// wave copy; the str check runs inside that copy).
+// So the heads, the column boundaries inside a sample and the str bytes the UTF-8 check reads cost
+// no second HBM read, and no row edge costs a partial store. A tile larger than a stage buffer is
+// decoded in row groups with synchronous loads; a sample larger than the stage is listed for
+// stage_huge_kernel, which copies it straight from HBM.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -38,14 +45,16 @@
 namespace mdsx_kernels {
 namespace {
 
-// 16 bytes of the stage at byte position p (any alignment, -16 < p < cap: the stage has 16 bytes
-// of slack on either side).
+constexpr int kMetaSlots = 3;
+
+// 16 bytes of a stage buffer at byte position p (any alignment, -16 < p < cap: a buffer has 16
+// bytes of slack on either side).
 __device__ __forceinline__ uint4 lds16(const uint8_t* stage, int32_t p) {
   const uint4* q = reinterpret_cast<const uint4*>(stage + (p & ~15));
   return funnel16_lane(q[0], q[1], uint32_t(p & 15));
 }
 
-// u32 of the stage at byte position p (any alignment).
+// u32 of a stage buffer at byte position p (any alignment).
 __device__ __forceinline__ uint32_t lds_u32(const uint8_t* stage, uint32_t p) {
   const uint32_t* q = reinterpret_cast<const uint32_t*>(stage + (p & ~3u));
   return alignbyte(q[1], q[0], p & 3u);
@@ -88,7 +97,7 @@ __device__ __forceinline__ bool lds_utf8_bad(const uint8_t* stage, uint32_t p0, 
 }
 
 // Store the bytes of `v` (chunk at column byte D) that lie in [lo, hi): a whole 16-byte store
-// when the chunk is inside, else one byte at a time (the group's two edge chunks).
+// when the chunk is inside, else one byte at a time (the two chunks a tile shares).
 template <bool kNT>
 __device__ __forceinline__ void store_chunk(uint8_t* out, uint64_t D, uint64_t lo, uint64_t hi,
                                             const uint4 v) {
@@ -100,40 +109,327 @@ __device__ __forceinline__ void store_chunk(uint8_t* out, uint64_t D, uint64_t l
     if (D + b >= lo && D + b < hi) *gp(out + D + b) = uint8_t(byte_of(v, b));
 }
 
-struct StageLds {
-  uint8_t* stage;    // [cap], 16 bytes of slack before and after
-  int64_t* dst;      // [nvar][TR]  final ragged output offset of each row
-  uint32_t* beg;     // [TR]        sample begin (file offset)
-  uint32_t* end;     // [TR]        sample end
-  uint32_t* src;     // [ncols][TR] stage position of each column of a row of the current group
-  uint32_t* len;     // [nvar][TR]  ragged length of a row (0 if the row failed a check)
-  uint8_t* ok;       // [TR]
+// A tile as the pipeline sees it (built once per workgroup from the tile and shard tables).
+struct TileDesc {
+  uint64_t shard_off;  // shard file offset inside the batch buffer
+  uint64_t row0;       // output row of the tile's first row
+  uint32_t bytes;      // shard file size (< 4 GiB: u32 offsets)
+  uint32_t r0;         // first row of the tile inside its shard
+  uint32_t nrows;
+  uint32_t samples;    // rows of the shard
+  int32_t shard;       // batch shard index
+  uint32_t table_ok;   // the shard's offsets table fits in its file
 };
 
-__host__ __device__ __forceinline__ size_t stage_meta_bytes(int TR, int ncols, int nvar) {
-  return size_t(TR) * (8 * size_t(nvar) + 8 + 4 * size_t(ncols) + 4 * size_t(nvar) + 1);
+// Per-tile metadata, loaded by LDS-DMA two tiles ahead: the tile's slice of the offsets table
+// (offs[r0 .. r0 + nrows]) and its output base in every ragged column (low / high dwords).
+struct MetaSlot {
+  uint32_t* offs;     // [TR + 1] (rounded up to 64 + 1 entries)
+  uint32_t* base_lo;  // [64]
+  uint32_t* base_hi;  // [64]
+};
+
+__host__ __device__ __forceinline__ uint32_t meta_slot_words(int TR) {
+  return uint32_t(((TR + 1 + 63) / 64) * 64) + 128;
 }
 
-// The heads and column layout of row t from its sample bytes at stage position `pos`
-// (MDSReader.decode_sample, mds/reader.py:111-125): the same rules as the scan pass, so a row's
-// lengths here are the ones its output offsets were scanned from.
+// Per-row layout of the tile being decoded.
+struct RowLds {
+  uint32_t* rel;  // [ncols][TR] byte offset of each column inside the row's sample
+  uint32_t* len;  // [nvar][TR]  ragged length (0 where the row failed a check)
+  int64_t* dst;   // [nvar][TR]  final ragged output offset
+  uint8_t* ok;    // [TR]
+};
+
+__host__ __device__ __forceinline__ size_t row_lds_bytes(int TR, int ncols, int nvar) {
+  return size_t(TR) * (4 * size_t(ncols) + 4 * size_t(nvar) + 8 * size_t(nvar) + 1);
+}
+
+// Column layout of a sample of `size` bytes from its size heads (MDSReader.decode_sample,
+// mds/reader.py:111-125): writes each column's offset inside the sample and each ragged column's
+// length; false where the heads or the columns do not fit in the sample. The same rule as
+// stage_totals_kernel, so a row's lengths here are the ones its tile base was summed from.
 template <class HeadAt>
-__device__ __forceinline__ bool row_layout(const DevArgs& a, const StageLds& L, int TR, int t,
-                                           uint64_t pos, uint64_t size, HeadAt head) {
+__device__ __forceinline__ bool row_layout(const DevArgs& a, const RowLds& R, int TR, int t,
+                                           uint64_t size, HeadAt head) {
   if (4ull * a.nvar > size) return false;
-  uint64_t p = pos + 4ull * a.nvar;
+  uint64_t p = 4ull * a.nvar;
   for (int c = 0; c < a.ncols; ++c) {
     const DevCol& col = a.cols[c];
     uint64_t n = col.row_bytes;
     if (col.var_index >= 0) {
       n = head(col.var_index);
-      L.len[col.var_index * TR + t] = uint32_t(n);
+      R.len[col.var_index * TR + t] = uint32_t(n);
     }
-    L.src[c * TR + t] = uint32_t(p);
+    R.rel[c * TR + t] = uint32_t(p);
     p += n;
   }
-  return p <= pos + size;
+  return p <= size;
 }
+
+// The rows of `td` from its metadata slot: sample range checks (mds/reader.py:137-148).
+__device__ __forceinline__ int row_range(const TileDesc& td, const MetaSlot& m, int t,
+                                         uint32_t* b, uint32_t* e) {
+  *b = m.offs[t];
+  *e = m.offs[t + 1];
+  const uint64_t hdr_end = 4ull + 4ull * (uint64_t(td.samples) + 1ull);
+  if (!(hdr_end <= *b && *b <= *e && *e <= td.bytes)) return MDSX_E_BOUNDS;
+  if (*b == *e) return MDSX_E_EMPTY;
+  return MDSX_OK;
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(
+      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const uint8_t*)p)));
+}
+
+// Loader (wave 0): the offsets-table slice and output bases of tile `td` into metadata slot m.
+__device__ __forceinline__ void load_meta(const DevArgs& a, const TileDesc& td, uint32_t tile,
+                                          const MetaSlot& m, int lane) {
+  if (!td.table_ok) return;
+  const uint32_t* offs = reinterpret_cast<const uint32_t*>(a.batch + td.shard_off + 4) + td.r0;
+  const uint32_t n = td.nrows + 1;
+  const uint32_t lds_offs = lds_addr(m.offs);
+  for (uint32_t i = 0; i < n; i += 64)
+    glds4(offs + min(i + uint32_t(lane), n - 1), lds_offs + 4 * i);
+  if (a.nvar) {
+    const int vi = lane < a.nvar ? lane : 0;
+    const uint32_t* base =
+        reinterpret_cast<const uint32_t*>(a.tile_prefix + uint64_t(vi) * a.nscan + tile);
+    glds4(base, lds_addr(m.base_lo));
+    glds4(base + 1, lds_addr(m.base_hi));
+  }
+}
+
+// Loader (wave 0): the byte range [lo, hi) of the tile's checked samples, and whether it fits a
+// stage buffer of `cap` bytes.
+__device__ __forceinline__ void tile_span(const TileDesc& td, const MetaSlot& m, uint32_t cap,
+                                          int lane, uint32_t* lo, uint32_t* hi, bool* fits) {
+  uint32_t mn = 0xffffffffu, mx = 0;
+  if (td.table_ok) {
+    for (uint32_t r = uint32_t(lane); r < td.nrows; r += 64) {
+      uint32_t b, e;
+      if (row_range(td, m, int(r), &b, &e) == MDSX_OK) {
+        mn = min(mn, b);
+        mx = max(mx, e);
+      }
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    mn = min(mn, uint32_t(__shfl_xor(int(mn), o)));
+    mx = max(mx, uint32_t(__shfl_xor(int(mx), o)));
+  }
+  if (mn > mx) {  // no checked row: nothing to load
+    *lo = *hi = 0;
+    *fits = true;
+    return;
+  }
+  *lo = mn & ~15u;
+  *hi = (mx + 15u) & ~15u;
+  *fits = *hi - *lo <= cap;
+}
+
+// Loader: bytes [lo, hi) of the shard into a stage buffer, 1 KiB per wave-instruction (waves
+// `w0`, `w0 + step`, ... issue pieces of it).
+template <bool kNT>
+__device__ __forceinline__ void load_bytes(const uint8_t* shard, uint32_t lo, uint32_t hi,
+                                           uint32_t stage_lds, int w0, int step, int lane) {
+  const uint32_t n = (hi - lo) >> 4;
+  const uint4* src = reinterpret_cast<const uint4*>(shard + lo);
+  for (uint32_t p = uint32_t(w0); p * 64 < n; p += uint32_t(step))
+    glds16<kNT>(src + min(p * 64 + uint32_t(lane), n - 1), stage_lds + p * 1024u);
+}
+
+// Every column of rows [ga, gb) of the tile from a stage buffer whose byte 0 is shard byte `lo`:
+// destination-major, one 16-byte output chunk per lane per step.
+template <bool kNT>
+__device__ __forceinline__ void write_columns(const DevArgs& a, const TileDesc& td,
+                                              const RowLds& R, const MetaSlot& m, int TR,
+                                              const uint8_t* stage, uint32_t lo, int ga, int gb) {
+  const int t = threadIdx.x;
+  const uint64_t grow0 = td.row0 + uint32_t(ga);
+  for (int c = 0; c < a.ncols; ++c) {
+    const DevCol& col = a.cols[c];
+    uint8_t* out = static_cast<uint8_t*>(col.data);
+    const int vi = col.var_index;
+    const uint32_t rb = col.row_bytes;
+    uint64_t d0, d1;  // the rows' output byte range of this column
+    if (vi < 0) {
+      d0 = grow0 * rb;
+      d1 = d0 + uint64_t(gb - ga) * rb;
+    } else {
+      d0 = uint64_t(R.dst[vi * TR + ga]);
+      d1 = uint64_t(R.dst[vi * TR + gb - 1]) + R.len[vi * TR + gb - 1];
+      if (d1 > col.capacity) {  // block-uniform
+        if (t == 0) report(a.status, MDSX_E_CAPACITY, td.shard, int(td.r0 + ga), c);
+        continue;
+      }
+    }
+    if (d1 <= d0) continue;
+    const bool wide = d1 - d0 >= (1ull << 32);
+    const uint64_t dbeg = d0 & ~uint64_t(15);
+    const uint32_t nout = uint32_t((((d1 + 15) & ~uint64_t(15)) - dbeg) >> 4);
+    for (uint32_t k = uint32_t(t); k < nout; k += kBlock) {
+      const uint64_t D = dbeg + 16ull * k;
+      const uint64_t x = D > d0 ? D : d0;  // first byte of the chunk these rows own
+      // row j holding byte x: fixed by division, ragged by binary search of the offsets
+      int j;
+      if (vi < 0) {
+        j = ga + int(wide ? (x - d0) / rb : uint64_t(uint32_t(x - d0) / rb));
+      } else {
+        int l = ga, h = gb - 1;
+        while (l < h) {
+          const int mid = (l + h + 1) >> 1;
+          if (uint64_t(R.dst[vi * TR + mid]) <= x) l = mid; else h = mid - 1;
+        }
+        j = l;
+      }
+      uint4 val = make_uint4(0, 0, 0, 0);
+      for (; j < gb; ++j) {
+        const uint64_t rd = vi < 0 ? grow0 * rb + uint64_t(j - ga) * rb
+                                   : uint64_t(R.dst[vi * TR + j]);
+        if (rd >= D + 16) break;
+        const uint32_t rl = vi < 0 ? rb : R.len[vi * TR + j];
+        const uint64_t pa = std::max(D, rd), pb = std::min(D + 16, rd + rl);
+        if (pb <= pa || !R.ok[j]) continue;
+        // the 16 stage bytes lined up with the chunk: row j's column starts at stage byte
+        // offs[j] - lo + rel, which is output byte rd
+        const int32_t sp = int32_t(m.offs[j] - lo + R.rel[c * TR + j]) - int32_t(rd - D);
+        const uint4 piece = lds16(stage, sp);
+        if (pa == D && pb == D + 16) {
+          val = piece;
+          break;
+        }
+        val = merge_bytes(val, piece, uint32_t(pa - D), uint32_t(pb - D));
+      }
+      store_chunk<kNT>(out, D, d0, d1, val);
+    }
+  }
+}
+
+// Strict UTF-8 of the str rows in [ga, gb) from a stage buffer whose byte 0 is shard byte lo.
+__device__ __forceinline__ void check_utf8(const DevArgs& a, const TileDesc& td, const RowLds& R,
+                                           const MetaSlot& m, int TR, const uint8_t* stage,
+                                           uint32_t lo, int ga, int gb) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int c = 0; c < a.ncols; ++c) {
+    const DevCol& col = a.cols[c];
+    if (col.kind != MDSX_KIND_STR || !col.flags) continue;
+    const int vi = col.var_index;
+    for (int r0 = ga + wave * 4; r0 < gb; r0 += kBlock / 16) {
+      const int r = min(r0 + (lane >> 4), gb - 1);
+      const bool live = r0 + (lane >> 4) < gb && R.ok[r];
+      const uint32_t n = live ? R.len[vi * TR + r] : 0u;
+      const uint32_t p0 = live ? m.offs[r] - lo + R.rel[c * TR + r] : 0u;
+      const bool bad = lds_utf8_bad(stage, p0, n, lane);
+      if ((lane & 15) == 0 && n && bad) col.flags[td.row0 + r] = 1;
+    }
+  }
+}
+
+// Exclusive scan of the rows' ragged lengths -> final offsets (tile base + scan), written out
+// with zeroed str flags. Block-uniform; ends with a barrier.
+__device__ __forceinline__ void tile_offsets(const DevArgs& a, const TileDesc& td,
+                                             const RowLds& R, const MetaSlot& m, int TR,
+                                             int64_t* s_wsum) {
+  const int t = threadIdx.x, lane = t & 63;
+  const int n = td.table_ok ? int(td.nrows) : 0;
+  for (int c = 0; c < a.ncols; ++c) {
+    const DevCol& col = a.cols[c];
+    if (col.var_index < 0) continue;
+    const int vi = col.var_index;
+    const int64_t base = int64_t((uint64_t(m.base_hi[vi]) << 32) | m.base_lo[vi]);
+    if (TR <= 64) {  // one wave: the rows are its lanes
+      if (t < 64) {
+        const int64_t x = lane < n ? int64_t(R.len[vi * TR + lane]) : 0;
+        int64_t incl = x;
+        for (int o = 1; o < TR; o <<= 1) {
+          const int64_t y = __shfl_up(incl, o);
+          if (lane >= o) incl += y;
+        }
+        if (lane < n) R.dst[vi * TR + lane] = base + incl - x;
+      }
+    } else {
+      const int64_t x = t < n ? int64_t(R.len[vi * TR + t]) : 0;
+      int64_t total;
+      const int64_t excl = block_exclusive_scan(x, s_wsum, &total);
+      if (t < n) R.dst[vi * TR + t] = base + excl;
+    }
+  }
+  __syncthreads();
+  if (t < n) {
+    const uint64_t row = td.row0 + t;
+    for (int c = 0; c < a.ncols; ++c) {
+      const DevCol& col = a.cols[c];
+      if (col.var_index < 0) continue;
+      col.offsets[row] = R.dst[col.var_index * TR + t];
+      if (col.flags) col.flags[row] = 0;
+    }
+  }
+}
+
+// A row that fails a check: no ragged bytes, its error reported.
+__device__ __forceinline__ void fail_row(const DevArgs& a, const TileDesc& td, const RowLds& R,
+                                         int TR, int t, int rc) {
+  R.ok[t] = 0;
+  for (int vi = 0; vi < a.nvar; ++vi) R.len[vi * TR + t] = 0;
+  report(a.status, rc, td.shard, int(td.r0 + t), -1);
+}
+
+}  // namespace
+
+// Pass 1 of the staged decode: the ragged bytes of every tile (one thread per row; 256 / TR tiles
+// per workgroup), with the staged kernel's row rule: a row whose range, heads or columns do not
+// fit counts zero.
+__global__ __launch_bounds__(kBlock) void stage_totals_kernel(const DevArgs a) {
+  __shared__ int64_t s_part[kBlock / 64][MDSX_MAX_COLUMNS];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int TR = a.tile_rows;
+  const uint32_t tile = blockIdx.x * uint32_t(kBlock / TR) + uint32_t(t / TR);
+  const bool tile_ok = tile < a.ntiles;
+  TileView v;
+  if (tile_ok) v = tile_view(a, tile);
+  const bool in_tile = tile_ok && v.table_ok && (t % TR) < int(v.nrows);
+  uint32_t b = 0, e = 0;
+  bool ok = false;
+  if (in_tile) ok = sample_range(v, v.r0 + t % TR, &b, &e) == MDSX_OK && 4ull * a.nvar <= e - b;
+  const bool few = a.nvar <= kHeadRegs;
+  Heads h;
+  if (ok && few) h.load(v.shard + b, a.nvar);
+  auto head = [&](int vi) -> uint32_t {
+    return few ? h.get(vi) : load_u32_any(v.shard + b + 4u * uint32_t(vi));
+  };
+  if (ok) {
+    uint64_t need = 4ull * a.nvar;
+    for (int c = 0; c < a.ncols; ++c) {
+      const DevCol& col = a.cols[c];
+      need += col.var_index >= 0 ? head(col.var_index) : col.row_bytes;
+    }
+    ok = uint64_t(b) + need <= e;
+  }
+  for (int vi = 0; vi < a.nvar; ++vi) {
+    int64_t x = ok ? int64_t(head(vi)) : 0;
+    if (TR <= 64) {  // segments of TR lanes inside the wave
+      for (int o = 1; o < TR; o <<= 1) x += __shfl_xor(x, o);
+      if (tile_ok && t % TR == 0) a.tile_total[uint64_t(vi) * a.nscan + tile] = x;
+    } else {  // a tile spans TR / 64 waves
+      for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+      if (lane == 0) s_part[wave][vi] = x;
+    }
+  }
+  if (TR > 64) {
+    __syncthreads();
+    if (tile_ok && t % TR == 0) {
+      for (int vi = 0; vi < a.nvar; ++vi) {
+        int64_t sum = 0;
+        for (int w = wave; w < wave + TR / 64; ++w) sum += s_part[w][vi];
+        a.tile_total[uint64_t(vi) * a.nscan + tile] = sum;
+      }
+    }
+  }
+}
+
+namespace {
 
 // Huge rows (a sample larger than the stage), listed by stage_decode_kernel: one workgroup per
 // row, straight from HBM (a separate launch, so the staged kernel keeps its registers for the
@@ -157,17 +453,6 @@ __global__ __launch_bounds__(kBlock) void stage_huge_kernel(const DevArgs a) {
     const uint8_t* sample = v.shard + b;
     auto head = [&](int vi) { return load_u32_any(sample + 4u * uint32_t(vi)); };
     uint64_t pos = 4ull * a.nvar;
-    bool ok = pos <= uint64_t(e - b);
-    for (int c = 0; ok && c < a.ncols; ++c) {
-      const DevCol& col = a.cols[c];
-      pos += col.var_index >= 0 ? head(col.var_index) : col.row_bytes;
-      ok = pos <= uint64_t(e - b);
-    }
-    if (!ok) {
-      if (threadIdx.x == 0) report(a.status, MDSX_E_BOUNDS, v.shard_idx, int(v.r0 + t), -1);
-      continue;
-    }
-    pos = 4ull * a.nvar;
     for (int c = 0; c < a.ncols; ++c) {
       const DevCol& col = a.cols[c];
       const uint64_t len = col.var_index >= 0 ? head(col.var_index) : col.row_bytes;
@@ -207,192 +492,190 @@ __global__ __launch_bounds__(kBlock) void stage_decode_kernel(const DevArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int TR = a.tile_rows;
   const uint32_t cap = a.stage_bytes;
-  StageLds L;
-  L.stage = smem + 16;
-  L.dst = reinterpret_cast<int64_t*>(smem + 16 + cap + 16);
-  L.beg = reinterpret_cast<uint32_t*>(L.dst + a.nvar * TR);
-  L.end = L.beg + TR;
-  L.src = L.end + TR;
-  L.len = L.src + a.ncols * TR;
-  L.ok = reinterpret_cast<uint8_t*>(L.len + a.nvar * TR);
-  __shared__ uint32_t s_first, s_gend, s_hi;
+  const uint32_t per_wg = a.stage_tiles;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const uint32_t tile0 = blockIdx.x * per_wg;
+  const uint32_t ntiles = min(per_wg, a.ntiles - tile0);
 
-  const int t = threadIdx.x;
-  const int lane = t & 63, wave = t >> 6;
-  const uint32_t tile = blockIdx.x;
-  const TileView v = tile_view(a, tile);
-  if (!v.table_ok) {
-    if (t == 0 && tile == v.d.tile0) report(a.status, MDSX_E_HEADER, v.shard_idx, -1, -1);
-    return;  // block-uniform
-  }
-  if (t == 0 && tile == v.d.tile0) {
+  // LDS: two stage buffers (16 bytes of slack around each), the run's tile table, three
+  // metadata slots, the decoded tile's row layout
+  uint8_t* const stage[2] = {smem + 16, smem + 16 + cap + 32};
+  TileDesc* s_td = reinterpret_cast<TileDesc*>(smem + 2 * (cap + 32));
+  uint32_t* meta_base = reinterpret_cast<uint32_t*>(s_td + per_wg);
+  const uint32_t mw = meta_slot_words(TR);
+  auto meta = [&](uint32_t k) {
+    uint32_t* p = meta_base + (k % kMetaSlots) * mw;
+    return MetaSlot{p, p + (mw - 128), p + (mw - 64)};
+  };
+  RowLds R;
+  R.dst = reinterpret_cast<int64_t*>(meta_base + kMetaSlots * mw);
+  R.rel = reinterpret_cast<uint32_t*>(R.dst + a.nvar * TR);
+  R.len = R.rel + a.ncols * TR;
+  R.ok = reinterpret_cast<uint8_t*>(R.len + a.nvar * TR);
+  __shared__ uint32_t s_lo[2], s_fits[2];
+  __shared__ uint32_t s_first, s_gend, s_ghi;
+  __shared__ int64_t s_wsum[kBlock / 64];
+
+  // ---- the run's tiles (plain loads, before any LDS-DMA is in flight)
+  for (uint32_t k = uint32_t(t); k < ntiles; k += kBlock) {
+    const uint32_t tile = tile0 + k;
+    const uint32_t si = a.tile_shard[tile];
+    const mdsx_shard_desc d = a.shards[si];
+    TileDesc td;
+    td.shard_off = d.offset;
+    td.r0 = (tile - d.tile0) * uint32_t(TR);
+    td.nrows = d.samples > td.r0 ? min(uint32_t(TR), d.samples - td.r0) : 0u;
+    td.row0 = d.row0 + td.r0;
+    td.bytes = uint32_t(min(d.bytes, uint64_t(0xffffffffu)));
+    td.samples = d.samples;
+    td.shard = int32_t(si);
+    td.table_ok = 4ull + 4ull * (uint64_t(d.samples) + 1ull) <= d.bytes ? 1u : 0u;
+    s_td[k] = td;
     // header written by encode_joint_shard (mds/writer.py:133-144): u32 N, then N+1 offsets
-    const uint32_t n = *reinterpret_cast<const uint32_t*>(v.shard);
-    if (n != v.d.samples || v.offs[0] < v.hdr_end || v.offs[v.d.samples] > v.d.bytes)
-      report(a.status, MDSX_E_HEADER, v.shard_idx, -1, -1);
-  }
-  const int nrows = int(v.nrows);
-
-  // ---- 1. sample ranges, final ragged offsets
-  if (t < nrows) {
-    uint32_t b = 0, e = 0;
-    const int rc = sample_range(v, v.r0 + t, &b, &e);
-    L.beg[t] = b;
-    L.end[t] = e;
-    L.ok[t] = rc == MDSX_OK;
-    if (rc != MDSX_OK) report(a.status, rc, v.shard_idx, int(v.r0 + t), -1);
-    const uint64_t row = v.d.row0 + v.r0 + t;
-    for (int c = 0; c < a.ncols; ++c) {
-      const DevCol& col = a.cols[c];
-      if (col.var_index < 0) continue;
-      const int vi = col.var_index;
-      // the scan pass left the scan-block-local offset in offsets[row]
-      const int64_t off = a.tile_prefix[uint64_t(vi) * a.nscan + tile / a.scan_per] +
-                          col.offsets[row];
-      col.offsets[row] = off;
-      L.dst[vi * TR + t] = off;
-      L.len[vi * TR + t] = 0;
-      if (col.flags) col.flags[row] = 0;
+    if (tile == d.tile0) {
+      const uint8_t* shard = a.batch + d.offset;
+      const uint32_t* offs = reinterpret_cast<const uint32_t*>(shard + 4);
+      if (!td.table_ok || *reinterpret_cast<const uint32_t*>(shard) != d.samples ||
+          offs[0] < 4ull + 4ull * (uint64_t(d.samples) + 1ull) || offs[d.samples] > d.bytes)
+        report(a.status, MDSX_E_HEADER, int(si), -1, -1);
     }
   }
   __syncthreads();
 
-  const uint32_t stage_lds = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(
-      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)L.stage)));
-  for (int ga = 0; ga < nrows;) {  // block-uniform loop over row groups
-    // ---- 2. the group: rows from ga while every checked row's bytes fit the stage window that
-    // starts at the first checked row
-    if (t == 0) {
-      s_first = uint32_t(nrows);
-      s_gend = uint32_t(nrows);
-      s_hi = 0;
-    }
-    __syncthreads();
-    if (t >= ga && t < nrows && L.ok[t]) atomicMin(&s_first, uint32_t(t));
-    __syncthreads();
-    const int first = int(s_first);
-    const uint32_t lo = first < nrows ? (L.beg[first] & ~15u) : 0u;
-    if (t >= ga && t < nrows && L.ok[t] && !(L.beg[t] >= lo && L.end[t] - lo <= cap))
-      atomicMin(&s_gend, uint32_t(t));
-    __syncthreads();
-    const int gb = int(s_gend);
-    if (gb == ga) {  // row ga is checked and larger than the stage: stage_huge_kernel's
-      if (t == 0) {
-        uint32_t* count = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(a.status) +
-                                                      kHugeCountOffset);
-        a.src_abs[atomicAdd(count, 1u)] = (uint64_t(tile) << 32) | uint32_t(ga);
-      }
-      ++ga;
-      __syncthreads();  // every thread has read s_first / s_gend before they are reset
-      continue;
-    }
-    if (t >= ga && t < gb && L.ok[t]) atomicMax(&s_hi, (L.end[t] + 15u) & ~15u);
-    __syncthreads();
-    const uint32_t hi = first < gb ? s_hi : lo;
+  const uint32_t stage_lds[2] = {lds_addr(stage[0]), lds_addr(stage[1])};
+  // ---- prologue (loader): metadata of tiles 0 and 1, the bytes of tile 0
+  if (wave == 0) {
+    load_meta(a, s_td[0], tile0, meta(0), lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t lo, hi;
+    bool fits;
+    tile_span(s_td[0], meta(0), cap, lane, &lo, &hi, &fits);
+    if (fits) load_bytes<kNT>(a.batch + s_td[0].shard_off, lo, hi, stage_lds[0], 0, 1, lane);
+    if (lane == 0) s_lo[0] = lo, s_fits[0] = fits;
+    if (ntiles > 1) load_meta(a, s_td[1], tile0 + 1, meta(1), lane);
+  }
 
-    // ---- the group's bytes [lo, hi) into the stage, 1 KiB per wave-instruction
-    const uint32_t nchunks = (hi - lo) >> 4;
-    const uint4* gsrc = reinterpret_cast<const uint4*>(v.shard + lo);
-    for (uint32_t p = uint32_t(wave); p * 64 < nchunks; p += kBlock / 64) {
-      const uint32_t k = min(p * 64 + uint32_t(lane), nchunks - 1);
-      glds16<kNT>(gsrc + k, stage_lds + p * 1024u);
-    }
+  for (uint32_t k = 0; k < ntiles; ++k) {
+    // the bytes of tile k and the metadata of tile k + 1 have landed; every wave's stores of
+    // tile k - 1 are done
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-
-    // ---- 3. heads and column ranges of the group's rows, from the stage
-    if (t >= ga && t < gb && L.ok[t]) {
-      const uint32_t pos = L.beg[t] - lo;
-      const bool fits = row_layout(a, L, TR, t, pos, uint64_t(L.end[t] - L.beg[t]),
-                                   [&](int vi) { return lds_u32(L.stage, pos + 4u * vi); });
-      if (!fits) {
-        L.ok[t] = 0;
-        for (int vi = 0; vi < a.nvar; ++vi) L.len[vi * TR + t] = 0;
-        report(a.status, MDSX_E_BOUNDS, v.shard_idx, int(v.r0 + t), -1);
+    const uint32_t sb = k & 1;
+    const TileDesc td = s_td[k];
+    const MetaSlot m = meta(k);
+    const int n = td.table_ok ? int(td.nrows) : 0;
+    const uint8_t* st = stage[sb];
+    const uint32_t lo = s_lo[sb];
+    const bool fits = s_fits[sb] != 0;
+    if (wave == 0) {  // loader: tile k + 1's bytes, tile k + 2's metadata
+      if (k + 1 < ntiles) {
+        uint32_t nlo, nhi;
+        bool nfits;
+        tile_span(s_td[k + 1], meta(k + 1), cap, lane, &nlo, &nhi, &nfits);
+        if (nfits)
+          load_bytes<kNT>(a.batch + s_td[k + 1].shard_off, nlo, nhi, stage_lds[sb ^ 1], 0, 1,
+                          lane);
+        if (lane == 0) s_lo[sb ^ 1] = nlo, s_fits[sb ^ 1] = nfits;
       }
+      if (k + 2 < ntiles) load_meta(a, s_td[k + 2], tile0 + k + 2, meta(k + 2), lane);
     }
-    __syncthreads();
 
-    // ---- 4. every column, destination-major from the stage
-    const uint64_t grow0 = v.d.row0 + v.r0 + ga;  // output row of the group's first row
-    for (int c = 0; c < a.ncols; ++c) {
-      const DevCol& col = a.cols[c];
-      uint8_t* out = static_cast<uint8_t*>(col.data);
-      const int vi = col.var_index;
-      const uint32_t rb = col.row_bytes;
-      uint64_t d0, d1;  // the group's output byte range of this column
-      if (vi < 0) {
-        d0 = grow0 * rb;
-        d1 = d0 + uint64_t(gb - ga) * rb;
-      } else {
-        d0 = uint64_t(L.dst[vi * TR + ga]);
-        d1 = uint64_t(L.dst[vi * TR + gb - 1]) + L.len[vi * TR + gb - 1];
-        if (d1 > col.capacity) {  // block-uniform
-          if (t == 0) report(a.status, MDSX_E_CAPACITY, v.shard_idx, int(v.r0 + ga), c);
+    if (fits) {
+      // ---- 1. ranges and column layout from the stage
+      if (t < n) {
+        uint32_t b, e;
+        const int rc = row_range(td, m, t, &b, &e);
+        R.ok[t] = 1;
+        if (rc != MDSX_OK) {
+          fail_row(a, td, R, TR, t, rc);
+        } else if (!row_layout(a, R, TR, t, uint64_t(e - b),
+                               [&](int vi) { return lds_u32(st, b - lo + 4u * uint32_t(vi)); })) {
+          fail_row(a, td, R, TR, t, MDSX_E_BOUNDS);
+        }
+      }
+      __syncthreads();
+      // ---- 2. ragged offsets; 3. columns; 4. UTF-8
+      tile_offsets(a, td, R, m, TR, s_wsum);
+      __syncthreads();
+      if (n) {
+        write_columns<kNT>(a, td, R, m, TR, st, lo, 0, n);
+        check_utf8(a, td, R, m, TR, st, lo, 0, n);
+      }
+    } else {
+      // ---- a tile larger than a stage buffer: layout from HBM, then row groups that fit,
+      // loaded synchronously into this tile's buffer (tile k + 1's stays in flight)
+      if (t < n) {
+        uint32_t b, e;
+        const int rc = row_range(td, m, t, &b, &e);
+        R.ok[t] = 1;
+        const uint8_t* sample = a.batch + td.shard_off + b;
+        if (rc != MDSX_OK) {
+          fail_row(a, td, R, TR, t, rc);
+        } else if (!row_layout(a, R, TR, t, uint64_t(e - b), [&](int vi) {
+                     return load_u32_any(sample + 4u * uint32_t(vi));
+                   })) {
+          fail_row(a, td, R, TR, t, MDSX_E_BOUNDS);
+        }
+      }
+      __syncthreads();
+      tile_offsets(a, td, R, m, TR, s_wsum);
+      for (int ga = 0; ga < n;) {  // block-uniform loop over row groups
+        if (t == 0) s_first = uint32_t(n), s_gend = uint32_t(n), s_ghi = 0;
+        __syncthreads();
+        if (t >= ga && t < n && R.ok[t]) atomicMin(&s_first, uint32_t(t));
+        __syncthreads();
+        const int first = int(s_first);
+        const uint32_t glo = first < n ? (m.offs[first] & ~15u) : 0u;
+        if (t >= ga && t < n && R.ok[t] && !(m.offs[t] >= glo && m.offs[t + 1] - glo <= cap))
+          atomicMin(&s_gend, uint32_t(t));
+        __syncthreads();
+        const int gb = int(s_gend);
+        if (gb == ga) {  // row ga alone is larger than the stage: stage_huge_kernel's
+          if (t == 0) {
+            uint32_t* count = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(a.status) +
+                                                          kHugeCountOffset);
+            a.src_abs[atomicAdd(count, 1u)] = (uint64_t(tile0 + k) << 32) | uint32_t(ga);
+          }
+          ++ga;
+          __syncthreads();  // every thread has read s_first / s_gend before they are reset
           continue;
         }
-      }
-      if (d1 <= d0) continue;
-      const uint64_t dbeg = d0 & ~uint64_t(15);
-      const uint32_t nout = uint32_t(((d1 + 15) & ~uint64_t(15)) - dbeg) >> 4;
-      for (uint32_t k = uint32_t(t); k < nout; k += kBlock) {
-        const uint64_t D = dbeg + 16ull * k;
-        const uint64_t x = D > d0 ? D : d0;  // first byte of the chunk this group owns
-        // row j holding byte x: fixed by division, ragged by binary search of the offsets
-        int j;
-        if (vi < 0) {
-          j = ga + int(d1 - d0 < (1ull << 32) ? uint64_t(uint32_t(x - d0) / rb) : (x - d0) / rb);
-        } else {
-          int l = ga, h = gb - 1;
-          while (l < h) {
-            const int m = (l + h + 1) >> 1;
-            if (uint64_t(L.dst[vi * TR + m]) <= x) l = m; else h = m - 1;
-          }
-          j = l;
-        }
-        uint4 val = make_uint4(0, 0, 0, 0);
-        for (; j < gb; ++j) {
-          const uint64_t rd = vi < 0 ? grow0 * rb + uint64_t(j - ga) * rb
-                                     : uint64_t(L.dst[vi * TR + j]);
-          if (rd >= D + 16) break;
-          const uint32_t rl = vi < 0 ? rb : L.len[vi * TR + j];
-          const uint64_t pa = std::max(D, rd), pb = std::min(D + 16, rd + rl);
-          if (pb <= pa || !L.ok[j]) continue;
-          // the 16 stage bytes that line up with the chunk: stage byte of D within row j
-          const uint4 piece = lds16(L.stage, int32_t(L.src[c * TR + j]) - int32_t(rd - D));
-          if (pa == D && pb == D + 16) {
-            val = piece;
-            break;
-          }
-          val = merge_bytes(val, piece, uint32_t(pa - D), uint32_t(pb - D));
-        }
-        store_chunk<kNT>(out, D, d0, d1, val);
+        if (t >= ga && t < gb && R.ok[t]) atomicMax(&s_ghi, (m.offs[t + 1] + 15u) & ~15u);
+        __syncthreads();
+        const uint32_t ghi = first < gb ? s_ghi : glo;
+        load_bytes<kNT>(a.batch + td.shard_off, glo, ghi, stage_lds[sb], wave, kBlock / 64, lane);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        write_columns<kNT>(a, td, R, m, TR, st, glo, ga, gb);
+        check_utf8(a, td, R, m, TR, st, glo, ga, gb);
+        __syncthreads();  // the buffer is refilled by the next group
+        ga = gb;
       }
     }
-
-    // ---- 5. strict UTF-8 of the group's str rows, from the stage
-    for (int c = 0; c < a.ncols; ++c) {
-      const DevCol& col = a.cols[c];
-      if (col.kind != MDSX_KIND_STR || !col.flags) continue;
-      const int vi = col.var_index;
-      for (int r0 = ga + wave * 4; r0 < gb; r0 += kBlock / 16) {
-        const int r = min(r0 + (lane >> 4), gb - 1);
-        const bool live = r0 + (lane >> 4) < gb && L.ok[r];
-        const uint32_t n = live ? L.len[vi * TR + r] : 0u;
-        const bool bad = lds_utf8_bad(L.stage, L.src[c * TR + r], n, lane);
-        if ((lane & 15) == 0 && n && bad) col.flags[v.d.row0 + v.r0 + r] = 1;
-      }
-    }
-    __syncthreads();  // the stage is refilled by the next group
-    ga = gb;
+    __syncthreads();  // stage buffer sb and metadata slot k are refilled from the next tile on
   }
 }
 
 }  // namespace
 
-size_t stage_lds_bytes(const mdsx_plan* plan, int tile_rows, uint32_t stage_bytes) {
-  return ((16 + size_t(stage_bytes) + 16 + stage_meta_bytes(tile_rows, plan->ncols, plan->nvar) +
-           15) & ~size_t(15));
+size_t stage_lds_bytes(const mdsx_plan* plan, int tile_rows, uint32_t stage_bytes,
+                       uint32_t tiles_per_wg) {
+  const size_t bytes = 2 * (size_t(stage_bytes) + 32) + sizeof(TileDesc) * tiles_per_wg +
+                       4 * size_t(kMetaSlots) * meta_slot_words(tile_rows) +
+                       row_lds_bytes(tile_rows, plan->ncols, plan->nvar);
+  return (bytes + 15) & ~size_t(15);
+}
+
+// Tiles per workgroup of the staged decode: runs long enough for the pipeline to fill, and
+// enough workgroups (>= ~16 per CU) to balance the tail.
+uint32_t stage_tiles_per_wg(uint32_t ntiles) {
+  return std::max<uint32_t>(1, std::min<uint32_t>(64, ntiles / 4096));
+}
+
+int launch_stage_totals(const DevArgs& a, hipStream_t s) {
+  const unsigned grid = unsigned((uint64_t(a.ntiles) * a.tile_rows + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(stage_totals_kernel, dim3(grid), dim3(kBlock), 0, s, a);
+  return hip_check(hipGetLastError(), "stage_totals_kernel launch");
 }
 
 int launch_stage_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
@@ -400,26 +683,26 @@ int launch_stage_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) 
                                     sizeof(uint32_t), s),
                      "hipMemsetAsync");
   if (rc != MDSX_OK) return rc;
-  const size_t lds = stage_lds_bytes(plan, a.tile_rows, a.stage_bytes);
+  const size_t lds = stage_lds_bytes(plan, a.tile_rows, a.stage_bytes, a.stage_tiles);
+  const void* fn = plan->nontemporal ? reinterpret_cast<const void*>(stage_decode_kernel<true>)
+                                     : reinterpret_cast<const void*>(stage_decode_kernel<false>);
   if (lds > 64 * 1024) {  // above the default dynamic-LDS limit of a launch
-    rc = hip_check(hipFuncSetAttribute(reinterpret_cast<const void*>(
-                                           plan->nontemporal ? stage_decode_kernel<true>
-                                                             : stage_decode_kernel<false>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)),
+    rc = hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)),
                    "hipFuncSetAttribute");
     if (rc != MDSX_OK) return rc;
   }
-  // huge rows: at most one per workgroup of the staged kernel's tiles (usually none)
+  const unsigned grid = (a.ntiles + a.stage_tiles - 1) / a.stage_tiles;
+  // huge rows: one workgroup each, 1024 at a time (usually none)
   const unsigned hgrid = unsigned(std::min<uint64_t>(a.ntiles, 1024));
   if (plan->nontemporal) {
     mdsx::set_last_kernel("stage_decode_kernel<true>");
-    hipLaunchKernelGGL((stage_decode_kernel<true>), dim3(a.ntiles), dim3(kBlock), lds, s, a);
+    hipLaunchKernelGGL((stage_decode_kernel<true>), dim3(grid), dim3(kBlock), lds, s, a);
     rc = hip_check(hipGetLastError(), "stage_decode_kernel launch");
     if (rc == MDSX_OK)
       hipLaunchKernelGGL((stage_huge_kernel<true>), dim3(hgrid), dim3(kBlock), 0, s, a);
   } else {
     mdsx::set_last_kernel("stage_decode_kernel<false>");
-    hipLaunchKernelGGL((stage_decode_kernel<false>), dim3(a.ntiles), dim3(kBlock), lds, s, a);
+    hipLaunchKernelGGL((stage_decode_kernel<false>), dim3(grid), dim3(kBlock), lds, s, a);
     rc = hip_check(hipGetLastError(), "stage_decode_kernel launch");
     if (rc == MDSX_OK)
       hipLaunchKernelGGL((stage_huge_kernel<false>), dim3(hgrid), dim3(kBlock), 0, s, a);

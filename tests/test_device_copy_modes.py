@@ -30,7 +30,7 @@ pytestmark = pytest.mark.gpu
 
 MODES = {
     'stage': '',  # the default
-    'stage_overflow': 'stage=4,fill=100',  # tiles of ~2x the stage: several row groups each
+    'stage_overflow': 'stage=4,fill=300',  # tiles of ~3x the stage: several row groups each
     'stage_tiny': 'stage=1',  # rows over 1 KiB go through the huge-row kernel
     'stage_big': 'stage=64,fill=90',
     'gather': 'stage=0,gmin=1000000000',

@@ -108,7 +108,7 @@ def test_too_many_columns():
 
 
 def test_tile_rows_for_sizes_ragged_tiles_to_the_stage():
-    """Ragged plans: tiles of about half the 32 KiB LDS stage (power of two rows, 1..256);
+    """Ragged plans: tiles of about 70 % of a 24 KiB LDS stage buffer (power of two rows, 1..256);
     all-fixed plans: the plan's tile size whatever the batch."""
     from streaming_amd.decoder import Plan
     c = Plan(['b', 'n', 's'], ['bytes', 'int', 'str'], [None, 8, None])
