@@ -37,6 +37,7 @@ struct DevArgs {
   mdsx_status* status;
   int64_t* tile_total;   // [nvar][nscan] ragged bytes of each scan block (scan_per tiles)
   int64_t* tile_prefix;  // [nvar][nscan] their exclusive prefix
+  int64_t* chunk_sum;    // [nvar][nchunk] scan of tile_total in chunks of kScanChunk entries
   int64_t* totals;       // [nvar] or null
   uint64_t* src_abs;     // [nvar][rows]  byte index into the batch of each row's ragged value
   uint32_t* row_map;     // [nvar][map_len] first row of every gather tile
@@ -46,6 +47,7 @@ struct DevArgs {
   uint64_t rows;
   uint32_t ntiles;
   uint32_t nscan;     // scan blocks: ceil(ntiles / scan_per)
+  uint32_t nchunk;    // chunks of the totals scan
   uint32_t scan_per;  // tiles per scan block (kBlock / tile_rows)
   int32_t nshards;
   int32_t ncols;

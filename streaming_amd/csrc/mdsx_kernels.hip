@@ -10,7 +10,8 @@
 //   scan_tiles_kernel    one workgroup per tile of rows: offsets-table scan + u32 size heads ->
 //                        per-row lengths of every ragged column, block exclusive scan (wave64
 //                        shuffles + LDS), per-tile totals.                      (ragged plans only)
-//   scan_totals_kernel   one workgroup per ragged column: exclusive scan of the tile totals.
+//   scan_chunks_kernel / scan_chunk_sums_kernel / scan_apply_kernel: exclusive scan of the
+//                        per-block totals of every ragged column (reduce-then-scan).
 //   decode_kernel        one workgroup per tile: per-row column boundaries into LDS; fixed columns
 //                        of <= 16 bytes gathered one row per lane; larger fixed columns and long
 //                        ragged rows copied one row per wave with 16-byte aligned loads and stores,
@@ -93,44 +94,71 @@ __global__ __launch_bounds__(kBlock) void scan_tiles_kernel(const DevArgs a) {
   }
 }
 
-// Pass 1b: exclusive scan of the scan-block totals of one ragged column (one workgroup per
-// column). Thread t owns the contiguous run [t * per, (t + 1) * per) of blocks: it sums its run, one block
-// scan of the 256 run sums gives every run its base, then each thread writes its run's prefixes
-// (one pass over the totals instead of ntiles / 256 dependent block scans).
-__global__ __launch_bounds__(kBlock) void scan_totals_kernel(const DevArgs a) {
+// Pass 1b: exclusive scan of the scan-block totals of every ragged column (nscan entries each),
+// reduce-then-scan over chunks of kScanChunk entries: scan_chunks_kernel sums each chunk,
+// scan_chunk_sums_kernel scans the chunk sums (one workgroup per column; the column totals land
+// in totals[] and offsets[rows]), scan_apply_kernel scans each chunk from its base.
+constexpr uint32_t kScanPer = 16;                   // entries per thread
+constexpr uint32_t kScanChunk = kBlock * kScanPer;  // entries per workgroup
+
+__global__ __launch_bounds__(kBlock) void scan_chunks_kernel(const DevArgs a) {
+  __shared__ int64_t s_wsum[kBlock / 64];
+  const int vi = blockIdx.y;
+  const int64_t* in = a.tile_total + uint64_t(vi) * a.nscan;
+  const uint64_t lo = uint64_t(blockIdx.x) * kScanChunk + uint64_t(threadIdx.x) * kScanPer;
+  int64_t x[kScanPer];
+#pragma unroll
+  for (uint32_t j = 0; j < kScanPer; ++j) x[j] = lo + j < a.nscan ? in[lo + j] : 0;
+  int64_t run = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kScanPer; ++j) run += x[j];
+  int64_t total;
+  block_exclusive_scan(run, s_wsum, &total);
+  if (threadIdx.x == 0) a.chunk_sum[uint64_t(vi) * a.nchunk + blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kBlock) void scan_chunk_sums_kernel(const DevArgs a) {
   __shared__ int64_t s_wsum[kBlock / 64];
   const int vi = blockIdx.x;
-  const int64_t* in = a.tile_total + uint64_t(vi) * a.nscan;
-  int64_t* out = a.tile_prefix + uint64_t(vi) * a.nscan;
-  const uint32_t per = (a.nscan + kBlock - 1) / kBlock;
-  const uint32_t lo = min(a.nscan, threadIdx.x * per), hi = min(a.nscan, lo + per);
-  constexpr uint32_t kBatch = 16;  // loads in flight per thread
-  int64_t run = 0;
-  for (uint32_t k0 = lo; k0 < hi; k0 += kBatch) {
-    int64_t x[kBatch];
-#pragma unroll
-    for (uint32_t j = 0; j < kBatch; ++j) x[j] = k0 + j < hi ? in[k0 + j] : 0;
-#pragma unroll
-    for (uint32_t j = 0; j < kBatch; ++j) run += x[j];
-  }
-  int64_t total;
-  int64_t base = block_exclusive_scan(run, s_wsum, &total);
-  for (uint32_t k0 = lo; k0 < hi; k0 += kBatch) {
-    int64_t x[kBatch];
-#pragma unroll
-    for (uint32_t j = 0; j < kBatch; ++j) x[j] = k0 + j < hi ? in[k0 + j] : 0;
-#pragma unroll
-    for (uint32_t j = 0; j < kBatch; ++j) {
-      if (k0 + j < hi) out[k0 + j] = base;
-      base += x[j];
-    }
+  int64_t* sums = a.chunk_sum + uint64_t(vi) * a.nchunk;
+  int64_t carry = 0;
+  for (uint32_t base = 0; base < a.nchunk; base += kBlock) {  // in place: sums -> prefixes
+    const uint32_t k = base + threadIdx.x;
+    const int64_t x = k < a.nchunk ? sums[k] : 0;
+    int64_t total;
+    const int64_t excl = block_exclusive_scan(x, s_wsum, &total);
+    if (k < a.nchunk) sums[k] = carry + excl;
+    carry += total;
   }
   if (threadIdx.x == 0) {
-    if (a.totals) a.totals[vi] = total;
+    if (a.totals) a.totals[vi] = carry;
     for (int c = 0; c < a.ncols; ++c)
-      if (a.cols[c].var_index == vi) a.cols[c].offsets[a.rows] = total;
+      if (a.cols[c].var_index == vi) a.cols[c].offsets[a.rows] = carry;
   }
 }
+
+__global__ __launch_bounds__(kBlock) void scan_apply_kernel(const DevArgs a) {
+  __shared__ int64_t s_wsum[kBlock / 64];
+  const int vi = blockIdx.y;
+  const int64_t* in = a.tile_total + uint64_t(vi) * a.nscan;
+  int64_t* out = a.tile_prefix + uint64_t(vi) * a.nscan;
+  const uint64_t lo = uint64_t(blockIdx.x) * kScanChunk + uint64_t(threadIdx.x) * kScanPer;
+  int64_t x[kScanPer];
+#pragma unroll
+  for (uint32_t j = 0; j < kScanPer; ++j) x[j] = lo + j < a.nscan ? in[lo + j] : 0;
+  int64_t run = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kScanPer; ++j) run += x[j];
+  int64_t total;
+  int64_t base = a.chunk_sum[uint64_t(vi) * a.nchunk + blockIdx.x] +
+                 block_exclusive_scan(run, s_wsum, &total);
+#pragma unroll
+  for (uint32_t j = 0; j < kScanPer; ++j) {
+    if (lo + j < a.nscan) out[lo + j] = base;
+    base += x[j];
+  }
+}
+
 
 
 // ---------------------------------------------------------------------------------------------
@@ -780,7 +808,7 @@ __global__ __launch_bounds__(kBlock) void gather_ragged_kernel(const DevArgs a) 
 
 // ---------------------------------------------------------------------------------------------
 struct Layout {
-  uint64_t tile_total, tile_prefix, src_abs, row_map, map_len, total;
+  uint64_t tile_total, tile_prefix, chunk_sum, src_abs, row_map, map_len, total;
 };
 
 __host__ uint64_t round256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
@@ -795,7 +823,8 @@ Layout workspace_layout(const mdsx_plan* plan, const mdsx_batch* b) {
   L.map_len = b->bytes / kMapGrain + 8;
   L.tile_total = 256;
   L.tile_prefix = L.tile_total + round256(nv * b->ntiles * 8);
-  L.src_abs = L.tile_prefix + round256(nv * b->ntiles * 8);
+  L.chunk_sum = L.tile_prefix + round256(nv * b->ntiles * 8);
+  L.src_abs = L.chunk_sum + round256(nv * (b->ntiles / kScanChunk + 1) * 8);
   L.row_map = L.src_abs + round256(nv * b->rows * 8);
   L.total = L.row_map + round256(nv * L.map_len * 4);
   return L;
@@ -822,6 +851,7 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   a->status = reinterpret_cast<mdsx_status*>(ws);
   a->tile_total = reinterpret_cast<int64_t*>(ws + L.tile_total);
   a->tile_prefix = reinterpret_cast<int64_t*>(ws + L.tile_prefix);
+  a->chunk_sum = reinterpret_cast<int64_t*>(ws + L.chunk_sum);
   a->src_abs = reinterpret_cast<uint64_t*>(ws + L.src_abs);
   a->row_map = reinterpret_cast<uint32_t*>(ws + L.row_map);
   a->lookback = reinterpret_cast<uint64_t*>(ws + L.tile_total);  // single pass: no tile totals
@@ -838,6 +868,7 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   // the staged decode scans one total per tile; the register-copy decode one per 256 rows
   a->scan_per = a->stage_bytes ? 1u : uint32_t(kBlock / tr);
   a->nscan = (b->ntiles + a->scan_per - 1) / a->scan_per;
+  a->nchunk = (a->nscan + kScanChunk - 1) / kScanChunk;
   a->nshards = b->nshards;
   a->ncols = plan->ncols;
   a->nvar = plan->nvar;
@@ -1181,8 +1212,16 @@ int mdsx_scan_shards(const mdsx_plan* plan, const mdsx_batch* batch, const mdsx_
     rc = hip_check(hipGetLastError(), "scan_tiles_kernel launch");
     if (rc != MDSX_OK) return rc;
   }
-  hipLaunchKernelGGL(scan_totals_kernel, dim3(plan->nvar), dim3(kBlock), 0, s, a);
-  return hip_check(hipGetLastError(), "scan_totals_kernel launch");
+  if (a.nchunk) {
+    hipLaunchKernelGGL(scan_chunks_kernel, dim3(a.nchunk, plan->nvar), dim3(kBlock), 0, s, a);
+    rc = hip_check(hipGetLastError(), "scan_chunks_kernel launch");
+    if (rc != MDSX_OK) return rc;
+  }
+  hipLaunchKernelGGL(scan_chunk_sums_kernel, dim3(plan->nvar), dim3(kBlock), 0, s, a);
+  rc = hip_check(hipGetLastError(), "scan_chunk_sums_kernel launch");
+  if (rc != MDSX_OK || !a.nchunk) return rc;
+  hipLaunchKernelGGL(scan_apply_kernel, dim3(a.nchunk, plan->nvar), dim3(kBlock), 0, s, a);
+  return hip_check(hipGetLastError(), "scan_apply_kernel launch");
 }
 
 }  // extern "C"

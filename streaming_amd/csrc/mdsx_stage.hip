@@ -12,11 +12,12 @@
 // size heads, then scan_totals_kernel (mdsx_kernels.hip) turns them into each tile's output base.
 //
 // Pass 2 (stage_decode_kernel): a workgroup runs a software pipeline over a run of consecutive
-// tiles. Wave 0 is the loader: while the four waves decode tile k from one LDS stage buffer, the
-// shard bytes of tile k + 1 are already in flight into the other (global_load_lds_dwordx4: 1 KiB
-// per wave-instruction, no VGPRs) and the offsets-table slice and output bases of tile k + 2 into
-// a third metadata slot (global_load_lds_dword). The loads are issued from inline asm, invisible
-// to the compiler, and retired by one explicit `s_waitcnt vmcnt(0)` + barrier per tile. For tile k:
+// tiles. Wave 0 is the loader: while waves 1-3 decode tile k from one LDS stage buffer, the shard
+// bytes of tile k + 1 are in flight into the other (global_load_lds_dwordx4: 1 KiB per
+// wave-instruction, no VGPRs) and the offsets-table slice and output bases of tile k + 2 into a
+// third metadata slot (global_load_lds_dword). The loads are issued from inline asm, invisible to
+// the compiler; the loader, which stores nothing, retires them with one `s_waitcnt vmcnt(0)` per
+// tile and a barrier publishes them, while the consumers' stores stay in flight. For tile k:
 //
 //   1. each row's offsets pair (mds/reader.py:137-142) checked against the file, its size heads
 //      and column ranges parsed from LDS (decode_sample's head loop, mds/reader.py:111-125);
@@ -46,6 +47,11 @@ namespace mdsx_kernels {
 namespace {
 
 constexpr int kMetaSlots = 3;
+// Wave 0 of a stage_decode_kernel workgroup is the loader: it issues every LDS-DMA and no global
+// store, so it can wait for its loads with vmcnt(0) without waiting for stores; waves 1..3 (the
+// consumers, consumer thread ct = threadIdx.x - 64) decode and store, and never wait for their
+// stores inside the loop.
+constexpr int kConsumers = kBlock - 64;
 
 // 16 bytes of a stage buffer at byte position p (any alignment, -16 < p < cap: a buffer has 16
 // bytes of slack on either side).
@@ -241,12 +247,12 @@ __device__ __forceinline__ void load_bytes(const uint8_t* shard, uint32_t lo, ui
 }
 
 // Every column of rows [ga, gb) of the tile from a stage buffer whose byte 0 is shard byte `lo`:
-// destination-major, one 16-byte output chunk per lane per step.
+// destination-major, one 16-byte output chunk per consumer lane per step (consumer waves only).
 template <bool kNT>
 __device__ __forceinline__ void write_columns(const DevArgs& a, const TileDesc& td,
                                               const RowLds& R, const MetaSlot& m, int TR,
                                               const uint8_t* stage, uint32_t lo, int ga, int gb) {
-  const int t = threadIdx.x;
+  const int ct = int(threadIdx.x) - 64;
   const uint64_t grow0 = td.row0 + uint32_t(ga);
   for (int c = 0; c < a.ncols; ++c) {
     const DevCol& col = a.cols[c];
@@ -261,7 +267,7 @@ __device__ __forceinline__ void write_columns(const DevArgs& a, const TileDesc& 
       d0 = uint64_t(R.dst[vi * TR + ga]);
       d1 = uint64_t(R.dst[vi * TR + gb - 1]) + R.len[vi * TR + gb - 1];
       if (d1 > col.capacity) {  // block-uniform
-        if (t == 0) report(a.status, MDSX_E_CAPACITY, td.shard, int(td.r0 + ga), c);
+        if (ct == 0) report(a.status, MDSX_E_CAPACITY, td.shard, int(td.r0 + ga), c);
         continue;
       }
     }
@@ -269,7 +275,7 @@ __device__ __forceinline__ void write_columns(const DevArgs& a, const TileDesc& 
     const bool wide = d1 - d0 >= (1ull << 32);
     const uint64_t dbeg = d0 & ~uint64_t(15);
     const uint32_t nout = uint32_t((((d1 + 15) & ~uint64_t(15)) - dbeg) >> 4);
-    for (uint32_t k = uint32_t(t); k < nout; k += kBlock) {
+    for (uint32_t k = uint32_t(ct); k < nout; k += kConsumers) {
       const uint64_t D = dbeg + 16ull * k;
       const uint64_t x = D > d0 ? D : d0;  // first byte of the chunk these rows own
       // row j holding byte x: fixed by division, ragged by binary search of the offsets
@@ -307,16 +313,17 @@ __device__ __forceinline__ void write_columns(const DevArgs& a, const TileDesc& 
   }
 }
 
-// Strict UTF-8 of the str rows in [ga, gb) from a stage buffer whose byte 0 is shard byte lo.
+// Strict UTF-8 of the str rows in [ga, gb) from a stage buffer whose byte 0 is shard byte lo
+// (consumer waves only: four rows per wave).
 __device__ __forceinline__ void check_utf8(const DevArgs& a, const TileDesc& td, const RowLds& R,
                                            const MetaSlot& m, int TR, const uint8_t* stage,
                                            uint32_t lo, int ga, int gb) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, cw = int(threadIdx.x >> 6) - 1;
   for (int c = 0; c < a.ncols; ++c) {
     const DevCol& col = a.cols[c];
     if (col.kind != MDSX_KIND_STR || !col.flags) continue;
     const int vi = col.var_index;
-    for (int r0 = ga + wave * 4; r0 < gb; r0 += kBlock / 16) {
+    for (int r0 = ga + cw * 4; r0 < gb; r0 += kConsumers / 16) {
       const int r = min(r0 + (lane >> 4), gb - 1);
       const bool live = r0 + (lane >> 4) < gb && R.ok[r];
       const uint32_t n = live ? R.len[vi * TR + r] : 0u;
@@ -328,7 +335,7 @@ __device__ __forceinline__ void check_utf8(const DevArgs& a, const TileDesc& td,
 }
 
 // Exclusive scan of the rows' ragged lengths -> final offsets (tile base + scan), written out
-// with zeroed str flags. Block-uniform; ends with a barrier.
+// by the consumers with zeroed str flags. Block-uniform (every wave: the scan is LDS-only).
 __device__ __forceinline__ void tile_offsets(const DevArgs& a, const TileDesc& td,
                                              const RowLds& R, const MetaSlot& m, int TR,
                                              int64_t* s_wsum) {
@@ -340,7 +347,7 @@ __device__ __forceinline__ void tile_offsets(const DevArgs& a, const TileDesc& t
     const int vi = col.var_index;
     const int64_t base = int64_t((uint64_t(m.base_hi[vi]) << 32) | m.base_lo[vi]);
     if (TR <= 64) {  // one wave: the rows are its lanes
-      if (t < 64) {
+      if (t >= 64 && t < 128) {
         const int64_t x = lane < n ? int64_t(R.len[vi * TR + lane]) : 0;
         int64_t incl = x;
         for (int o = 1; o < TR; o <<= 1) {
@@ -357,12 +364,12 @@ __device__ __forceinline__ void tile_offsets(const DevArgs& a, const TileDesc& t
     }
   }
   __syncthreads();
-  if (t < n) {
-    const uint64_t row = td.row0 + t;
+  for (int r = t - 64; r >= 0 && r < n; r += kConsumers) {
+    const uint64_t row = td.row0 + r;
     for (int c = 0; c < a.ncols; ++c) {
       const DevCol& col = a.cols[c];
       if (col.var_index < 0) continue;
-      col.offsets[row] = R.dst[col.var_index * TR + t];
+      col.offsets[row] = R.dst[col.var_index * TR + r];
       if (col.flags) col.flags[row] = 0;
     }
   }
@@ -556,9 +563,9 @@ __global__ __launch_bounds__(kBlock) void stage_decode_kernel(const DevArgs a) {
   }
 
   for (uint32_t k = 0; k < ntiles; ++k) {
-    // the bytes of tile k and the metadata of tile k + 1 have landed; every wave's stores of
-    // tile k - 1 are done
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // the bytes of tile k and the metadata of tile k + 1 have landed (the loader's loads; the
+    // consumers' stores stay in flight)
+    if (wave == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const uint32_t sb = k & 1;
     const TileDesc td = s_td[k];
@@ -582,39 +589,39 @@ __global__ __launch_bounds__(kBlock) void stage_decode_kernel(const DevArgs a) {
 
     if (fits) {
       // ---- 1. ranges and column layout from the stage
-      if (t < n) {
+      for (int r = t - 64; r >= 0 && r < n; r += kConsumers) {
         uint32_t b, e;
-        const int rc = row_range(td, m, t, &b, &e);
-        R.ok[t] = 1;
+        const int rc = row_range(td, m, r, &b, &e);
+        R.ok[r] = 1;
         if (rc != MDSX_OK) {
-          fail_row(a, td, R, TR, t, rc);
-        } else if (!row_layout(a, R, TR, t, uint64_t(e - b),
+          fail_row(a, td, R, TR, r, rc);
+        } else if (!row_layout(a, R, TR, r, uint64_t(e - b),
                                [&](int vi) { return lds_u32(st, b - lo + 4u * uint32_t(vi)); })) {
-          fail_row(a, td, R, TR, t, MDSX_E_BOUNDS);
+          fail_row(a, td, R, TR, r, MDSX_E_BOUNDS);
         }
       }
       __syncthreads();
       // ---- 2. ragged offsets; 3. columns; 4. UTF-8
       tile_offsets(a, td, R, m, TR, s_wsum);
       __syncthreads();
-      if (n) {
+      if (n && wave > 0) {
         write_columns<kNT>(a, td, R, m, TR, st, lo, 0, n);
         check_utf8(a, td, R, m, TR, st, lo, 0, n);
       }
     } else {
       // ---- a tile larger than a stage buffer: layout from HBM, then row groups that fit,
       // loaded synchronously into this tile's buffer (tile k + 1's stays in flight)
-      if (t < n) {
+      for (int r = t - 64; r >= 0 && r < n; r += kConsumers) {
         uint32_t b, e;
-        const int rc = row_range(td, m, t, &b, &e);
-        R.ok[t] = 1;
+        const int rc = row_range(td, m, r, &b, &e);
+        R.ok[r] = 1;
         const uint8_t* sample = a.batch + td.shard_off + b;
         if (rc != MDSX_OK) {
-          fail_row(a, td, R, TR, t, rc);
-        } else if (!row_layout(a, R, TR, t, uint64_t(e - b), [&](int vi) {
+          fail_row(a, td, R, TR, r, rc);
+        } else if (!row_layout(a, R, TR, r, uint64_t(e - b), [&](int vi) {
                      return load_u32_any(sample + 4u * uint32_t(vi));
                    })) {
-          fail_row(a, td, R, TR, t, MDSX_E_BOUNDS);
+          fail_row(a, td, R, TR, r, MDSX_E_BOUNDS);
         }
       }
       __syncthreads();
@@ -622,16 +629,18 @@ __global__ __launch_bounds__(kBlock) void stage_decode_kernel(const DevArgs a) {
       for (int ga = 0; ga < n;) {  // block-uniform loop over row groups
         if (t == 0) s_first = uint32_t(n), s_gend = uint32_t(n), s_ghi = 0;
         __syncthreads();
-        if (t >= ga && t < n && R.ok[t]) atomicMin(&s_first, uint32_t(t));
+        for (int r = t; r < n; r += kBlock)
+          if (r >= ga && R.ok[r]) atomicMin(&s_first, uint32_t(r));
         __syncthreads();
         const int first = int(s_first);
         const uint32_t glo = first < n ? (m.offs[first] & ~15u) : 0u;
-        if (t >= ga && t < n && R.ok[t] && !(m.offs[t] >= glo && m.offs[t + 1] - glo <= cap))
-          atomicMin(&s_gend, uint32_t(t));
+        for (int r = t; r < n; r += kBlock)
+          if (r >= ga && R.ok[r] && !(m.offs[r] >= glo && m.offs[r + 1] - glo <= cap))
+            atomicMin(&s_gend, uint32_t(r));
         __syncthreads();
         const int gb = int(s_gend);
         if (gb == ga) {  // row ga alone is larger than the stage: stage_huge_kernel's
-          if (t == 0) {
+          if (t == 64) {  // a consumer: the loader wave stores nothing
             uint32_t* count = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(a.status) +
                                                           kHugeCountOffset);
             a.src_abs[atomicAdd(count, 1u)] = (uint64_t(tile0 + k) << 32) | uint32_t(ga);
@@ -640,14 +649,19 @@ __global__ __launch_bounds__(kBlock) void stage_decode_kernel(const DevArgs a) {
           __syncthreads();  // every thread has read s_first / s_gend before they are reset
           continue;
         }
-        if (t >= ga && t < gb && R.ok[t]) atomicMax(&s_ghi, (m.offs[t + 1] + 15u) & ~15u);
+        for (int r = t; r < gb; r += kBlock)
+          if (r >= ga && R.ok[r]) atomicMax(&s_ghi, (m.offs[r + 1] + 15u) & ~15u);
         __syncthreads();
         const uint32_t ghi = first < gb ? s_ghi : glo;
-        load_bytes<kNT>(a.batch + td.shard_off, glo, ghi, stage_lds[sb], wave, kBlock / 64, lane);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (wave == 0) {
+          load_bytes<kNT>(a.batch + td.shard_off, glo, ghi, stage_lds[sb], 0, 1, lane);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         __syncthreads();
-        write_columns<kNT>(a, td, R, m, TR, st, glo, ga, gb);
-        check_utf8(a, td, R, m, TR, st, glo, ga, gb);
+        if (wave > 0) {
+          write_columns<kNT>(a, td, R, m, TR, st, glo, ga, gb);
+          check_utf8(a, td, R, m, TR, st, glo, ga, gb);
+        }
         __syncthreads();  // the buffer is refilled by the next group
         ga = gb;
       }

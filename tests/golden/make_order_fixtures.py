@@ -43,7 +43,7 @@ SETTINGS = [
     ('py1e_w1', dict(shuffle=True, shuffle_algo='py1e', shuffle_seed=17, num_canonical_nodes=2,
                      batch_size=16, shuffle_block_size=1000), (1, 1, 1), 336),
     ('py1s_n1r2w2', dict(shuffle=True, shuffle_algo='py1s', shuffle_seed=5, num_canonical_nodes=4,
-                         batch_size=8), (1, 2, 2), 800),
+                         batch_size=8, shuffle_block_size=2048), (1, 2, 2), 800),
     ('py1br_n2r2w1', dict(shuffle=True, shuffle_algo='py1br', shuffle_seed=3,
                           num_canonical_nodes=2, batch_size=32, shuffle_block_size=2000),
      (2, 2, 1), 1024),
