@@ -59,6 +59,7 @@ struct DevArgs {
   int16_t str_cached;  // plan->str_cached
   uint32_t stage_bytes;  // each of the two LDS stage buffers of the staged decode (bytes, 1 KiB multiple)
   uint32_t stage_tiles;  // tiles per workgroup of the staged decode
+  uint32_t stage_debug;  // measurement only (MDSX_TUNE sdbg): parts of the staged decode skipped
   uint32_t gather_block0[MDSX_MAX_COLUMNS + 1];  // first gather workgroup of each ragged column
   DevCol cols[MDSX_MAX_COLUMNS];
 };

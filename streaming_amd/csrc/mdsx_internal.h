@@ -45,6 +45,8 @@ struct mdsx_plan {
   int str_cached = 0;   // medium str rows stored temporally (the UTF-8 re-read then hits L2)
   int ring_slots = 0;   // long ragged rows through a per-wave LDS-DMA ring of this many KiB (0: off)
   int stage_kb = 0;     // ragged plans: LDS stage of the staged decode in KiB (0: register copy)
+  int stage_tiles = 0;  // tiles per workgroup of the staged decode (0: per launch)
+  int stage_debug = 0;  // measurement only: parts of the staged decode skipped (bits)
   int stage_fill = 70;  // percent of a stage buffer a tile's samples fill on average (tile sizing)
   int gather_chunks = 2;  // 16-byte chunks per lane in the ragged gather (tile = 4 KiB x this)
   int gather_min = 256;   // ragged columns averaging fewer bytes per row use the gather kernel

@@ -864,7 +864,8 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   if (tr < 1 || tr > kBlock || (tr & (tr - 1)))
     return mdsx::fail(MDSX_E_ARG, "mdsx: batch tile_rows must be a power of two in [1, 256]");
   a->stage_bytes = plan->nvar > 0 ? uint32_t(plan->stage_kb) * 1024u : 0u;
-  a->stage_tiles = stage_tiles_per_wg(b->ntiles);
+  a->stage_tiles = plan->stage_tiles ? uint32_t(plan->stage_tiles) : stage_tiles_per_wg(b->ntiles);
+  a->stage_debug = uint32_t(plan->stage_debug);
   // the staged decode scans one total per tile; the register-copy decode one per 256 rows
   a->scan_per = a->stage_bytes ? 1u : uint32_t(kBlock / tr);
   a->nscan = (b->ntiles + a->scan_per - 1) / a->scan_per;

@@ -201,6 +201,10 @@ void apply_tuning(mdsx_plan* p) {
       p->str_cached = v ? 1 : 0;
     } else if (key == "ring" && (v == 0 || v == 4 || v == 6 || v == 8)) {
       p->ring_slots = int(v);
+    } else if (key == "stiles" && v >= 0 && v <= 1024) {
+      p->stage_tiles = int(v);
+    } else if (key == "sdbg" && v >= 0) {
+      p->stage_debug = int(v);
     } else if (key == "stage" && v >= 0 && v <= 96) {
       p->stage_kb = int(v);
     } else if (key == "fill" && v >= 10 && v <= 400) {  // > 100: tiles overflow the stage

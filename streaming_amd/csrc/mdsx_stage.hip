@@ -579,7 +579,7 @@ __global__ __launch_bounds__(kBlock) void stage_decode_kernel(const DevArgs a) {
         uint32_t nlo, nhi;
         bool nfits;
         tile_span(s_td[k + 1], meta(k + 1), cap, lane, &nlo, &nhi, &nfits);
-        if (nfits)
+        if (nfits && !(a.stage_debug & 1))
           load_bytes<kNT>(a.batch + s_td[k + 1].shard_off, nlo, nhi, stage_lds[sb ^ 1], 0, 1,
                           lane);
         if (lane == 0) s_lo[sb ^ 1] = nlo, s_fits[sb ^ 1] = nfits;
@@ -587,6 +587,10 @@ __global__ __launch_bounds__(kBlock) void stage_decode_kernel(const DevArgs a) {
       if (k + 2 < ntiles) load_meta(a, s_td[k + 2], tile0 + k + 2, meta(k + 2), lane);
     }
 
+    if (a.stage_debug & 8) {  // measurement only: skip the tile's decode
+      __syncthreads();
+      continue;
+    }
     if (fits) {
       // ---- 1. ranges and column layout from the stage
       for (int r = t - 64; r >= 0 && r < n; r += kConsumers) {
@@ -605,8 +609,8 @@ __global__ __launch_bounds__(kBlock) void stage_decode_kernel(const DevArgs a) {
       tile_offsets(a, td, R, m, TR, s_wsum);
       __syncthreads();
       if (n && wave > 0) {
-        write_columns<kNT>(a, td, R, m, TR, st, lo, 0, n);
-        check_utf8(a, td, R, m, TR, st, lo, 0, n);
+        if (!(a.stage_debug & 2)) write_columns<kNT>(a, td, R, m, TR, st, lo, 0, n);
+        if (!(a.stage_debug & 4)) check_utf8(a, td, R, m, TR, st, lo, 0, n);
       }
     } else {
       // ---- a tile larger than a stage buffer: layout from HBM, then row groups that fit,
