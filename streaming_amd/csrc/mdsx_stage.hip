@@ -47,11 +47,12 @@ namespace mdsx_kernels {
 namespace {
 
 constexpr int kMetaSlots = 3;
-// Wave 0 of a stage_decode_kernel workgroup is the loader: it issues every LDS-DMA and no global
-// store, so it can wait for its loads with vmcnt(0) without waiting for stores; waves 1..3 (the
-// consumers, consumer thread ct = threadIdx.x - 64) decode and store, and never wait for their
-// stores inside the loop.
-constexpr int kConsumers = kBlock - 64;
+// A stage_decode_kernel workgroup: 8 waves. Wave 0 is the loader: it issues every LDS-DMA and
+// no global store, so it waits for its loads with vmcnt(0) without waiting for stores; waves 1-7
+// (the consumers, consumer thread ct = threadIdx.x - 64) decode and store, and never wait for
+// their stores inside the loop.
+constexpr int kStageBlock = 512;
+constexpr int kConsumers = kStageBlock - 64;
 
 // 16 bytes of a stage buffer at byte position p (any alignment, -16 < p < cap: a buffer has 16
 // bytes of slack on either side).
@@ -141,14 +142,17 @@ __host__ __device__ __forceinline__ uint32_t meta_slot_words(int TR) {
 
 // Per-row layout of the tile being decoded.
 struct RowLds {
-  uint32_t* rel;  // [ncols][TR] byte offset of each column inside the row's sample
-  uint32_t* len;  // [nvar][TR]  ragged length (0 where the row failed a check)
-  int64_t* dst;   // [nvar][TR]  final ragged output offset
-  uint8_t* ok;    // [TR]
+  uint32_t* rel;   // [ncols][TR] byte offset of each column inside the row's sample
+  uint32_t* len;   // [nvar][TR]  ragged length (0 where the row failed a check)
+  int64_t* dst;    // [nvar][TR]  final ragged output offset
+  int32_t* src;    // [ncols][TR] stage position of the column's first byte (-1: the row failed)
+  uint32_t* rdst;  // [ncols][TR] output position of the column's first byte, relative to the
+                   //             first 16-byte-aligned output chunk of the rows being written
+  uint8_t* ok;     // [TR]
 };
 
 __host__ __device__ __forceinline__ size_t row_lds_bytes(int TR, int ncols, int nvar) {
-  return size_t(TR) * (4 * size_t(ncols) + 4 * size_t(nvar) + 8 * size_t(nvar) + 1);
+  return size_t(TR) * (12 * size_t(ncols) + 4 * size_t(nvar) + 8 * size_t(nvar) + 1);
 }
 
 // Column layout of a sample of `size` bytes from its size heads (MDSReader.decode_sample,
@@ -235,89 +239,121 @@ __device__ __forceinline__ void tile_span(const TileDesc& td, const MetaSlot& m,
   *fits = *hi - *lo <= cap;
 }
 
-// Loader: bytes [lo, hi) of the shard into a stage buffer, 1 KiB per wave-instruction (waves
-// `w0`, `w0 + step`, ... issue pieces of it).
+// Loader: bytes [lo, hi) of the shard into a stage buffer, 1 KiB per wave-instruction.
 template <bool kNT>
 __device__ __forceinline__ void load_bytes(const uint8_t* shard, uint32_t lo, uint32_t hi,
-                                           uint32_t stage_lds, int w0, int step, int lane) {
+                                           uint32_t stage_lds, int lane) {
   const uint32_t n = (hi - lo) >> 4;
   const uint4* src = reinterpret_cast<const uint4*>(shard + lo);
-  for (uint32_t p = uint32_t(w0); p * 64 < n; p += uint32_t(step))
+  for (uint32_t p = 0; p * 64 < n; ++p)
     glds16<kNT>(src + min(p * 64 + uint32_t(lane), n - 1), stage_lds + p * 1024u);
 }
 
-// Every column of rows [ga, gb) of the tile from a stage buffer whose byte 0 is shard byte `lo`:
-// destination-major, one 16-byte output chunk per consumer lane per step (consumer waves only).
-template <bool kNT>
-__device__ __forceinline__ void write_columns(const DevArgs& a, const TileDesc& td,
-                                              const RowLds& R, const MetaSlot& m, int TR,
-                                              const uint8_t* stage, uint32_t lo, int ga, int gb) {
-  const int ct = int(threadIdx.x) - 64;
-  const uint64_t grow0 = td.row0 + uint32_t(ga);
-  for (int c = 0; c < a.ncols; ++c) {
-    const DevCol& col = a.cols[c];
-    uint8_t* out = static_cast<uint8_t*>(col.data);
-    const int vi = col.var_index;
-    const uint32_t rb = col.row_bytes;
-    uint64_t d0, d1;  // the rows' output byte range of this column
-    if (vi < 0) {
-      d0 = grow0 * rb;
-      d1 = d0 + uint64_t(gb - ga) * rb;
-    } else {
-      d0 = uint64_t(R.dst[vi * TR + ga]);
-      d1 = uint64_t(R.dst[vi * TR + gb - 1]) + R.len[vi * TR + gb - 1];
-      if (d1 > col.capacity) {  // block-uniform
-        if (ct == 0) report(a.status, MDSX_E_CAPACITY, td.shard, int(td.r0 + ga), c);
-        continue;
-      }
-    }
-    if (d1 <= d0) continue;
-    const bool wide = d1 - d0 >= (1ull << 32);
-    const uint64_t dbeg = d0 & ~uint64_t(15);
-    const uint32_t nout = uint32_t((((d1 + 15) & ~uint64_t(15)) - dbeg) >> 4);
-    for (uint32_t k = uint32_t(ct); k < nout; k += kConsumers) {
-      const uint64_t D = dbeg + 16ull * k;
-      const uint64_t x = D > d0 ? D : d0;  // first byte of the chunk these rows own
-      // row j holding byte x: fixed by division, ragged by binary search of the offsets
-      int j;
-      if (vi < 0) {
-        j = ga + int(wide ? (x - d0) / rb : uint64_t(uint32_t(x - d0) / rb));
-      } else {
-        int l = ga, h = gb - 1;
-        while (l < h) {
-          const int mid = (l + h + 1) >> 1;
-          if (uint64_t(R.dst[vi * TR + mid]) <= x) l = mid; else h = mid - 1;
-        }
-        j = l;
-      }
-      uint4 val = make_uint4(0, 0, 0, 0);
-      for (; j < gb; ++j) {
-        const uint64_t rd = vi < 0 ? grow0 * rb + uint64_t(j - ga) * rb
-                                   : uint64_t(R.dst[vi * TR + j]);
-        if (rd >= D + 16) break;
-        const uint32_t rl = vi < 0 ? rb : R.len[vi * TR + j];
-        const uint64_t pa = std::max(D, rd), pb = std::min(D + 16, rd + rl);
-        if (pb <= pa || !R.ok[j]) continue;
-        // the 16 stage bytes lined up with the chunk: row j's column starts at stage byte
-        // offs[j] - lo + rel, which is output byte rd
-        const int32_t sp = int32_t(m.offs[j] - lo + R.rel[c * TR + j]) - int32_t(rd - D);
-        const uint4 piece = lds16(stage, sp);
-        if (pa == D && pb == D + 16) {
-          val = piece;
-          break;
-        }
-        val = merge_bytes(val, piece, uint32_t(pa - D), uint32_t(pb - D));
-      }
-      store_chunk<kNT>(out, D, d0, d1, val);
+// The output byte range [d0, d1) of column c for rows [ga, gb) of the tile.
+__device__ __forceinline__ void column_range(const DevCol& col, const TileDesc& td,
+                                             const RowLds& R, int TR, int ga, int gb,
+                                             uint64_t* d0, uint64_t* d1) {
+  const int vi = col.var_index;
+  if (vi < 0) {
+    *d0 = (td.row0 + uint32_t(ga)) * col.row_bytes;
+    *d1 = *d0 + uint64_t(gb - ga) * col.row_bytes;
+  } else {
+    *d0 = uint64_t(R.dst[vi * TR + ga]);
+    *d1 = uint64_t(R.dst[vi * TR + gb - 1]) + R.len[vi * TR + gb - 1];
+  }
+}
+
+// Consumers: where each column of rows [ga, gb) sits in the stage (whose byte 0 is shard byte
+// `lo`) and in the output (relative to the rows' first aligned output chunk of the column).
+__device__ __forceinline__ void place_rows(const DevArgs& a, const TileDesc& td, const RowLds& R,
+                                           const MetaSlot& m, int TR, uint32_t lo, int ga,
+                                           int gb) {
+  for (int r = ga + int(threadIdx.x) - 64; r >= ga && r < gb; r += kConsumers) {
+    for (int c = 0; c < a.ncols; ++c) {
+      const DevCol& col = a.cols[c];
+      uint64_t d0, d1;
+      column_range(col, td, R, TR, ga, gb, &d0, &d1);
+      const uint64_t rd = col.var_index < 0 ? d0 + uint64_t(r - ga) * col.row_bytes
+                                            : uint64_t(R.dst[col.var_index * TR + r]);
+      R.rdst[c * TR + r] = uint32_t(rd - (d0 & ~uint64_t(15)));
+      R.src[c * TR + r] = R.ok[r] ? int32_t(m.offs[r] - lo + R.rel[c * TR + r]) : -1;
     }
   }
 }
 
-// Strict UTF-8 of the str rows in [ga, gb) from a stage buffer whose byte 0 is shard byte lo
-// (consumer waves only: four rows per wave).
+// Consumers: every column of rows [ga, gb) from the stage, destination-major: consumer lane k
+// assembles 16-byte-aligned output chunk k of the rows' contiguous output range of the column
+// from the stage bytes of the row(s) it covers (the row: division for fixed columns, binary
+// search for ragged ones) and stores it whole; only the range's two edge chunks, shared with
+// the neighbouring rows of other tiles, are stored a byte at a time.
+template <bool kNT>
+__device__ __forceinline__ void write_columns(const DevArgs& a, const TileDesc& td,
+                                              const RowLds& R, int TR, const uint8_t* stage,
+                                              int ga, int gb) {
+  const int ct = int(threadIdx.x) - 64;
+  for (int c = 0; c < a.ncols; ++c) {
+    const DevCol& col = a.cols[c];
+    const int vi = col.var_index;
+    const uint32_t rb = col.row_bytes;
+    uint64_t d0, d1;
+    column_range(col, td, R, TR, ga, gb, &d0, &d1);
+    if (vi >= 0 && d1 > col.capacity) {  // block-uniform
+      if (ct == 0) report(a.status, MDSX_E_CAPACITY, td.shard, int(td.r0 + ga), c);
+      continue;
+    }
+    if (d1 <= d0) continue;
+    const uint64_t dbeg = d0 & ~uint64_t(15);
+    uint8_t* out = static_cast<uint8_t*>(col.data) + dbeg;
+    const uint32_t lo = uint32_t(d0 - dbeg), hi = uint32_t(d1 - dbeg);  // owned bytes
+    const uint32_t nout = (hi + 15) >> 4;
+    const uint32_t* rdst = R.rdst + c * TR;
+    const int32_t* src = R.src + c * TR;
+    for (uint32_t k = uint32_t(ct); k < nout; k += kConsumers) {
+      const uint32_t D = 16u * k;
+      const uint32_t x = max(D, lo);  // first byte of the chunk these rows own
+      int j;
+      if (vi < 0) {
+        j = ga + int((x - lo) / rb);
+      } else {
+        int l = ga, h = gb - 1;
+        while (l < h) {
+          const int mid = (l + h + 1) >> 1;
+          if (rdst[mid] <= x) l = mid; else h = mid - 1;
+        }
+        j = l;
+      }
+      uint32_t rd = rdst[j];
+      uint32_t rl = vi < 0 ? rb : R.len[vi * TR + j];
+      int32_t sp = src[j];
+      uint4 val;
+      if (sp >= 0 && D >= rd && D + 16 <= rd + rl) {  // inside one row: the common case
+        val = lds16(stage, sp + int32_t(D - rd));
+      } else {
+        val = make_uint4(0, 0, 0, 0);
+        for (;;) {
+          const uint32_t pa = max(D, rd), pb = min(D + 16, rd + rl);
+          if (pb > pa && sp >= 0)
+            val = merge_bytes(val, lds16(stage, sp - int32_t(rd - D)), pa - D, pb - D);
+          if (++j >= gb) break;
+          rd = rdst[j];
+          if (rd >= D + 16) break;
+          rl = vi < 0 ? rb : R.len[vi * TR + j];
+          sp = src[j];
+        }
+      }
+      if (D >= lo && D + 16 <= hi) {
+        st16<kNT>(reinterpret_cast<uint64_t>(out) + D, val);
+      } else {
+        for (uint32_t b = 0; b < 16; ++b)
+          if (D + b >= lo && D + b < hi) *gp(out + D + b) = uint8_t(byte_of(val, int(b)));
+      }
+    }
+  }
+}
+
+// Consumers: strict UTF-8 of the str rows in [ga, gb), from the stage (four rows per wave).
 __device__ __forceinline__ void check_utf8(const DevArgs& a, const TileDesc& td, const RowLds& R,
-                                           const MetaSlot& m, int TR, const uint8_t* stage,
-                                           uint32_t lo, int ga, int gb) {
+                                           int TR, const uint8_t* stage, int ga, int gb) {
   const int lane = threadIdx.x & 63, cw = int(threadIdx.x >> 6) - 1;
   for (int c = 0; c < a.ncols; ++c) {
     const DevCol& col = a.cols[c];
@@ -325,42 +361,37 @@ __device__ __forceinline__ void check_utf8(const DevArgs& a, const TileDesc& td,
     const int vi = col.var_index;
     for (int r0 = ga + cw * 4; r0 < gb; r0 += kConsumers / 16) {
       const int r = min(r0 + (lane >> 4), gb - 1);
-      const bool live = r0 + (lane >> 4) < gb && R.ok[r];
+      const bool live = r0 + (lane >> 4) < gb && R.src[c * TR + r] >= 0;
       const uint32_t n = live ? R.len[vi * TR + r] : 0u;
-      const uint32_t p0 = live ? m.offs[r] - lo + R.rel[c * TR + r] : 0u;
-      const bool bad = lds_utf8_bad(stage, p0, n, lane);
+      const bool bad = lds_utf8_bad(stage, live ? uint32_t(R.src[c * TR + r]) : 0u, n, lane);
       if ((lane & 15) == 0 && n && bad) col.flags[td.row0 + r] = 1;
     }
   }
 }
 
-// Exclusive scan of the rows' ragged lengths -> final offsets (tile base + scan), written out
-// by the consumers with zeroed str flags. Block-uniform (every wave: the scan is LDS-only).
+// Exclusive scan of the rows' ragged lengths -> final offsets (tile base + scan) by wave 1 (up to
+// four rows per lane), written out by the consumers with zeroed str flags. Block-uniform.
 __device__ __forceinline__ void tile_offsets(const DevArgs& a, const TileDesc& td,
-                                             const RowLds& R, const MetaSlot& m, int TR,
-                                             int64_t* s_wsum) {
+                                             const RowLds& R, const MetaSlot& m, int TR) {
   const int t = threadIdx.x, lane = t & 63;
   const int n = td.table_ok ? int(td.nrows) : 0;
-  for (int c = 0; c < a.ncols; ++c) {
-    const DevCol& col = a.cols[c];
-    if (col.var_index < 0) continue;
-    const int vi = col.var_index;
-    const int64_t base = int64_t((uint64_t(m.base_hi[vi]) << 32) | m.base_lo[vi]);
-    if (TR <= 64) {  // one wave: the rows are its lanes
-      if (t >= 64 && t < 128) {
-        const int64_t x = lane < n ? int64_t(R.len[vi * TR + lane]) : 0;
-        int64_t incl = x;
-        for (int o = 1; o < TR; o <<= 1) {
-          const int64_t y = __shfl_up(incl, o);
-          if (lane >= o) incl += y;
-        }
-        if (lane < n) R.dst[vi * TR + lane] = base + incl - x;
+  if ((t >> 6) == 1) {
+    const int per = (n + 63) / 64;
+    const int r0 = lane * per, r1 = min(r0 + per, n);
+    for (int vi = 0; vi < a.nvar; ++vi) {
+      const uint32_t* len = R.len + vi * TR;
+      int64_t sum = 0;
+      for (int r = r0; r < r1; ++r) sum += len[r];
+      int64_t incl = sum;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
       }
-    } else {
-      const int64_t x = t < n ? int64_t(R.len[vi * TR + t]) : 0;
-      int64_t total;
-      const int64_t excl = block_exclusive_scan(x, s_wsum, &total);
-      if (t < n) R.dst[vi * TR + t] = base + excl;
+      int64_t run = int64_t((uint64_t(m.base_hi[vi]) << 32) | m.base_lo[vi]) + incl - sum;
+      for (int r = r0; r < r1; ++r) {
+        R.dst[vi * TR + r] = run;
+        run += len[r];
+      }
     }
   }
   __syncthreads();
@@ -495,7 +526,7 @@ __global__ __launch_bounds__(kBlock) void stage_huge_kernel(const DevArgs a) {
 }
 
 template <bool kNT>
-__global__ __launch_bounds__(kBlock) void stage_decode_kernel(const DevArgs a) {
+__global__ __launch_bounds__(kStageBlock) void stage_decode_kernel(const DevArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int TR = a.tile_rows;
   const uint32_t cap = a.stage_bytes;
@@ -518,13 +549,14 @@ __global__ __launch_bounds__(kBlock) void stage_decode_kernel(const DevArgs a) {
   R.dst = reinterpret_cast<int64_t*>(meta_base + kMetaSlots * mw);
   R.rel = reinterpret_cast<uint32_t*>(R.dst + a.nvar * TR);
   R.len = R.rel + a.ncols * TR;
-  R.ok = reinterpret_cast<uint8_t*>(R.len + a.nvar * TR);
+  R.src = reinterpret_cast<int32_t*>(R.len + a.nvar * TR);
+  R.rdst = reinterpret_cast<uint32_t*>(R.src + a.ncols * TR);
+  R.ok = reinterpret_cast<uint8_t*>(R.rdst + a.ncols * TR);
   __shared__ uint32_t s_lo[2], s_fits[2];
   __shared__ uint32_t s_first, s_gend, s_ghi;
-  __shared__ int64_t s_wsum[kBlock / 64];
 
   // ---- the run's tiles (plain loads, before any LDS-DMA is in flight)
-  for (uint32_t k = uint32_t(t); k < ntiles; k += kBlock) {
+  for (uint32_t k = uint32_t(t); k < ntiles; k += kStageBlock) {
     const uint32_t tile = tile0 + k;
     const uint32_t si = a.tile_shard[tile];
     const mdsx_shard_desc d = a.shards[si];
@@ -557,7 +589,7 @@ __global__ __launch_bounds__(kBlock) void stage_decode_kernel(const DevArgs a) {
     uint32_t lo, hi;
     bool fits;
     tile_span(s_td[0], meta(0), cap, lane, &lo, &hi, &fits);
-    if (fits) load_bytes<kNT>(a.batch + s_td[0].shard_off, lo, hi, stage_lds[0], 0, 1, lane);
+    if (fits) load_bytes<kNT>(a.batch + s_td[0].shard_off, lo, hi, stage_lds[0], lane);
     if (lane == 0) s_lo[0] = lo, s_fits[0] = fits;
     if (ntiles > 1) load_meta(a, s_td[1], tile0 + 1, meta(1), lane);
   }
@@ -580,65 +612,56 @@ __global__ __launch_bounds__(kBlock) void stage_decode_kernel(const DevArgs a) {
         bool nfits;
         tile_span(s_td[k + 1], meta(k + 1), cap, lane, &nlo, &nhi, &nfits);
         if (nfits && !(a.stage_debug & 1))
-          load_bytes<kNT>(a.batch + s_td[k + 1].shard_off, nlo, nhi, stage_lds[sb ^ 1], 0, 1,
-                          lane);
+          load_bytes<kNT>(a.batch + s_td[k + 1].shard_off, nlo, nhi, stage_lds[sb ^ 1], lane);
         if (lane == 0) s_lo[sb ^ 1] = nlo, s_fits[sb ^ 1] = nfits;
       }
       if (k + 2 < ntiles) load_meta(a, s_td[k + 2], tile0 + k + 2, meta(k + 2), lane);
     }
-
     if (a.stage_debug & 8) {  // measurement only: skip the tile's decode
       __syncthreads();
       continue;
     }
-    if (fits) {
-      // ---- 1. ranges and column layout from the stage
-      for (int r = t - 64; r >= 0 && r < n; r += kConsumers) {
-        uint32_t b, e;
-        const int rc = row_range(td, m, r, &b, &e);
-        R.ok[r] = 1;
-        if (rc != MDSX_OK) {
-          fail_row(a, td, R, TR, r, rc);
-        } else if (!row_layout(a, R, TR, r, uint64_t(e - b),
-                               [&](int vi) { return lds_u32(st, b - lo + 4u * uint32_t(vi)); })) {
-          fail_row(a, td, R, TR, r, MDSX_E_BOUNDS);
-        }
+
+    // ---- 1. ranges and column layout: from the stage, or (a tile larger than a stage buffer)
+    // from HBM
+    for (int r = t - 64; r >= 0 && r < n; r += kConsumers) {
+      uint32_t b, e;
+      const int rc = row_range(td, m, r, &b, &e);
+      R.ok[r] = 1;
+      const uint8_t* sample = a.batch + td.shard_off + b;
+      if (rc != MDSX_OK) {
+        fail_row(a, td, R, TR, r, rc);
+      } else if (fits ? !row_layout(a, R, TR, r, uint64_t(e - b),
+                                    [&](int vi) { return lds_u32(st, b - lo + 4u * vi); })
+                      : !row_layout(a, R, TR, r, uint64_t(e - b), [&](int vi) {
+                          return load_u32_any(sample + 4u * uint32_t(vi));
+                        })) {
+        fail_row(a, td, R, TR, r, MDSX_E_BOUNDS);
       }
+    }
+    __syncthreads();
+    // ---- 2. ragged offsets
+    tile_offsets(a, td, R, m, TR);
+    if (fits) {
+      place_rows(a, td, R, m, TR, lo, 0, n);
       __syncthreads();
-      // ---- 2. ragged offsets; 3. columns; 4. UTF-8
-      tile_offsets(a, td, R, m, TR, s_wsum);
-      __syncthreads();
+      // ---- 3. columns; 4. UTF-8
       if (n && wave > 0) {
-        if (!(a.stage_debug & 2)) write_columns<kNT>(a, td, R, m, TR, st, lo, 0, n);
-        if (!(a.stage_debug & 4)) check_utf8(a, td, R, m, TR, st, lo, 0, n);
+        if (!(a.stage_debug & 2)) write_columns<kNT>(a, td, R, TR, st, 0, n);
+        if (!(a.stage_debug & 4)) check_utf8(a, td, R, TR, st, 0, n);
       }
     } else {
-      // ---- a tile larger than a stage buffer: layout from HBM, then row groups that fit,
-      // loaded synchronously into this tile's buffer (tile k + 1's stays in flight)
-      for (int r = t - 64; r >= 0 && r < n; r += kConsumers) {
-        uint32_t b, e;
-        const int rc = row_range(td, m, r, &b, &e);
-        R.ok[r] = 1;
-        const uint8_t* sample = a.batch + td.shard_off + b;
-        if (rc != MDSX_OK) {
-          fail_row(a, td, R, TR, r, rc);
-        } else if (!row_layout(a, R, TR, r, uint64_t(e - b), [&](int vi) {
-                     return load_u32_any(sample + 4u * uint32_t(vi));
-                   })) {
-          fail_row(a, td, R, TR, r, MDSX_E_BOUNDS);
-        }
-      }
-      __syncthreads();
-      tile_offsets(a, td, R, m, TR, s_wsum);
+      // ---- a tile larger than a stage buffer: row groups that fit, loaded synchronously into
+      // this tile's buffer (tile k + 1's stays in flight)
       for (int ga = 0; ga < n;) {  // block-uniform loop over row groups
         if (t == 0) s_first = uint32_t(n), s_gend = uint32_t(n), s_ghi = 0;
         __syncthreads();
-        for (int r = t; r < n; r += kBlock)
+        for (int r = t; r < n; r += kStageBlock)
           if (r >= ga && R.ok[r]) atomicMin(&s_first, uint32_t(r));
         __syncthreads();
         const int first = int(s_first);
         const uint32_t glo = first < n ? (m.offs[first] & ~15u) : 0u;
-        for (int r = t; r < n; r += kBlock)
+        for (int r = t; r < n; r += kStageBlock)
           if (r >= ga && R.ok[r] && !(m.offs[r] >= glo && m.offs[r + 1] - glo <= cap))
             atomicMin(&s_gend, uint32_t(r));
         __syncthreads();
@@ -653,18 +676,19 @@ __global__ __launch_bounds__(kBlock) void stage_decode_kernel(const DevArgs a) {
           __syncthreads();  // every thread has read s_first / s_gend before they are reset
           continue;
         }
-        for (int r = t; r < gb; r += kBlock)
+        for (int r = t; r < gb; r += kStageBlock)
           if (r >= ga && R.ok[r]) atomicMax(&s_ghi, (m.offs[r + 1] + 15u) & ~15u);
         __syncthreads();
         const uint32_t ghi = first < gb ? s_ghi : glo;
         if (wave == 0) {
-          load_bytes<kNT>(a.batch + td.shard_off, glo, ghi, stage_lds[sb], 0, 1, lane);
+          load_bytes<kNT>(a.batch + td.shard_off + glo, 0, ghi - glo, stage_lds[sb], lane);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
+        place_rows(a, td, R, m, TR, glo, ga, gb);
         __syncthreads();
         if (wave > 0) {
-          write_columns<kNT>(a, td, R, m, TR, st, glo, ga, gb);
-          check_utf8(a, td, R, m, TR, st, glo, ga, gb);
+          write_columns<kNT>(a, td, R, TR, st, ga, gb);
+          check_utf8(a, td, R, TR, st, ga, gb);
         }
         __syncthreads();  // the buffer is refilled by the next group
         ga = gb;
@@ -714,13 +738,13 @@ int launch_stage_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) 
   const unsigned hgrid = unsigned(std::min<uint64_t>(a.ntiles, 1024));
   if (plan->nontemporal) {
     mdsx::set_last_kernel("stage_decode_kernel<true>");
-    hipLaunchKernelGGL((stage_decode_kernel<true>), dim3(grid), dim3(kBlock), lds, s, a);
+    hipLaunchKernelGGL((stage_decode_kernel<true>), dim3(grid), dim3(kStageBlock), lds, s, a);
     rc = hip_check(hipGetLastError(), "stage_decode_kernel launch");
     if (rc == MDSX_OK)
       hipLaunchKernelGGL((stage_huge_kernel<true>), dim3(hgrid), dim3(kBlock), 0, s, a);
   } else {
     mdsx::set_last_kernel("stage_decode_kernel<false>");
-    hipLaunchKernelGGL((stage_decode_kernel<false>), dim3(grid), dim3(kBlock), lds, s, a);
+    hipLaunchKernelGGL((stage_decode_kernel<false>), dim3(grid), dim3(kStageBlock), lds, s, a);
     rc = hip_check(hipGetLastError(), "stage_decode_kernel launch");
     if (rc == MDSX_OK)
       hipLaunchKernelGGL((stage_huge_kernel<false>), dim3(hgrid), dim3(kBlock), 0, s, a);
