@@ -54,16 +54,27 @@ constexpr int kMetaSlots = 3;
 constexpr int kStageBlock = 512;
 constexpr int kConsumers = kStageBlock - 64;
 
+// LDS pointers carry their address space, so every stage access compiles to ds_read (a generic
+// pointer compiles to flat_load, which counts in vmcnt too: every wait for it would also wait for
+// the consumers' stores in flight). The host pass only parses these device functions: it gets no
+// address space (its vector types do not bind LDS references).
+#ifdef __HIP_DEVICE_COMPILE__
+#define MDSX_L __attribute__((address_space(3)))
+#else
+#define MDSX_L
+#endif
+typedef MDSX_L uint8_t lds_u8;
+
 // 16 bytes of a stage buffer at byte position p (any alignment, -16 < p < cap: a buffer has 16
 // bytes of slack on either side).
-__device__ __forceinline__ uint4 lds16(const uint8_t* stage, int32_t p) {
-  const uint4* q = reinterpret_cast<const uint4*>(stage + (p & ~15));
+__device__ __forceinline__ uint4 lds16(const lds_u8* stage, int32_t p) {
+  const MDSX_L uint4* q = reinterpret_cast<const MDSX_L uint4*>(stage + (p & ~15));
   return funnel16_lane(q[0], q[1], uint32_t(p & 15));
 }
 
 // u32 of a stage buffer at byte position p (any alignment).
-__device__ __forceinline__ uint32_t lds_u32(const uint8_t* stage, uint32_t p) {
-  const uint32_t* q = reinterpret_cast<const uint32_t*>(stage + (p & ~3u));
+__device__ __forceinline__ uint32_t lds_u32(const lds_u8* stage, uint32_t p) {
+  const MDSX_L uint32_t* q = reinterpret_cast<const MDSX_L uint32_t*>(stage + (p & ~3u));
   return alignbyte(q[1], q[0], p & 3u);
 }
 
@@ -78,7 +89,7 @@ __device__ __forceinline__ uint4 merge_bytes(uint4 acc, const uint4 val, uint32_
 // aligned 16-byte chunks gl, gl + 16, ... of its row [p0, p0 + len) of the stage (bytes outside
 // the row zeroed), the dword before each chunk passed along the group. Returns the group's
 // verdict (uniform within the group).
-__device__ __forceinline__ bool lds_utf8_bad(const uint8_t* stage, uint32_t p0, uint32_t len,
+__device__ __forceinline__ bool lds_utf8_bad(const lds_u8* stage, uint32_t p0, uint32_t len,
                                              int lane) {
   const int gl = lane & 15;
   const uint32_t d0 = p0, dend = p0 + len, dbeg = p0 & ~15u;
@@ -92,7 +103,7 @@ __device__ __forceinline__ bool lds_utf8_bad(const uint8_t* stage, uint32_t p0, 
     const uint32_t k = base + uint32_t(gl);
     const uint32_t D = dbeg + 16u * k;
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (k < nchunks) v = *reinterpret_cast<const uint4*>(stage + D);
+    if (k < nchunks) v = *reinterpret_cast<const MDSX_L uint4*>(stage + D);
     const uint4 vout = keep_range(v, D, d0, dend);
     uint32_t pw = __shfl_up(vout.w, 1, 16);
     if (gl == 0) pw = carry;
@@ -160,12 +171,13 @@ __host__ __device__ __forceinline__ size_t row_lds_bytes(int TR, int ncols, int 
 // length; false where the heads or the columns do not fit in the sample. The same rule as
 // stage_totals_kernel, so a row's lengths here are the ones its tile base was summed from.
 template <class HeadAt>
-__device__ __forceinline__ bool row_layout(const DevArgs& a, const RowLds& R, int TR, int t,
-                                           uint64_t size, HeadAt head) {
+__device__ __forceinline__ bool row_layout(const DevArgs& a, const MDSX_L DevCol* cols,
+                                           const RowLds& R, int TR, int t, uint64_t size,
+                                           HeadAt head) {
   if (4ull * a.nvar > size) return false;
   uint64_t p = 4ull * a.nvar;
   for (int c = 0; c < a.ncols; ++c) {
-    const DevCol& col = a.cols[c];
+    const MDSX_L DevCol& col = cols[c];
     uint64_t n = col.row_bytes;
     if (col.var_index >= 0) {
       n = head(col.var_index);
@@ -250,7 +262,7 @@ __device__ __forceinline__ void load_bytes(const uint8_t* shard, uint32_t lo, ui
 }
 
 // The output byte range [d0, d1) of column c for rows [ga, gb) of the tile.
-__device__ __forceinline__ void column_range(const DevCol& col, const TileDesc& td,
+__device__ __forceinline__ void column_range(const MDSX_L DevCol& col, const TileDesc& td,
                                              const RowLds& R, int TR, int ga, int gb,
                                              uint64_t* d0, uint64_t* d1) {
   const int vi = col.var_index;
@@ -265,12 +277,12 @@ __device__ __forceinline__ void column_range(const DevCol& col, const TileDesc& 
 
 // Consumers: where each column of rows [ga, gb) sits in the stage (whose byte 0 is shard byte
 // `lo`) and in the output (relative to the rows' first aligned output chunk of the column).
-__device__ __forceinline__ void place_rows(const DevArgs& a, const TileDesc& td, const RowLds& R,
-                                           const MetaSlot& m, int TR, uint32_t lo, int ga,
-                                           int gb) {
+__device__ __forceinline__ void place_rows(const DevArgs& a, const MDSX_L DevCol* cols,
+                                           const TileDesc& td, const RowLds& R, const MetaSlot& m,
+                                           int TR, uint32_t lo, int ga, int gb) {
   for (int r = ga + int(threadIdx.x) - 64; r >= ga && r < gb; r += kConsumers) {
     for (int c = 0; c < a.ncols; ++c) {
-      const DevCol& col = a.cols[c];
+      const MDSX_L DevCol& col = cols[c];
       uint64_t d0, d1;
       column_range(col, td, R, TR, ga, gb, &d0, &d1);
       const uint64_t rd = col.var_index < 0 ? d0 + uint64_t(r - ga) * col.row_bytes
@@ -287,12 +299,12 @@ __device__ __forceinline__ void place_rows(const DevArgs& a, const TileDesc& td,
 // search for ragged ones) and stores it whole; only the range's two edge chunks, shared with
 // the neighbouring rows of other tiles, are stored a byte at a time.
 template <bool kNT>
-__device__ __forceinline__ void write_columns(const DevArgs& a, const TileDesc& td,
-                                              const RowLds& R, int TR, const uint8_t* stage,
-                                              int ga, int gb) {
+__device__ __forceinline__ void write_columns(const DevArgs& a, const MDSX_L DevCol* cols,
+                                              const TileDesc& td, const RowLds& R, int TR,
+                                              const lds_u8* stage, int ga, int gb) {
   const int ct = int(threadIdx.x) - 64;
   for (int c = 0; c < a.ncols; ++c) {
-    const DevCol& col = a.cols[c];
+    const MDSX_L DevCol& col = cols[c];
     const int vi = col.var_index;
     const uint32_t rb = col.row_bytes;
     uint64_t d0, d1;
@@ -352,11 +364,12 @@ __device__ __forceinline__ void write_columns(const DevArgs& a, const TileDesc& 
 }
 
 // Consumers: strict UTF-8 of the str rows in [ga, gb), from the stage (four rows per wave).
-__device__ __forceinline__ void check_utf8(const DevArgs& a, const TileDesc& td, const RowLds& R,
-                                           int TR, const uint8_t* stage, int ga, int gb) {
+__device__ __forceinline__ void check_utf8(const DevArgs& a, const MDSX_L DevCol* cols,
+                                           const TileDesc& td, const RowLds& R, int TR,
+                                           const lds_u8* stage, int ga, int gb) {
   const int lane = threadIdx.x & 63, cw = int(threadIdx.x >> 6) - 1;
   for (int c = 0; c < a.ncols; ++c) {
-    const DevCol& col = a.cols[c];
+    const MDSX_L DevCol& col = cols[c];
     if (col.kind != MDSX_KIND_STR || !col.flags) continue;
     const int vi = col.var_index;
     for (int r0 = ga + cw * 4; r0 < gb; r0 += kConsumers / 16) {
@@ -371,8 +384,9 @@ __device__ __forceinline__ void check_utf8(const DevArgs& a, const TileDesc& td,
 
 // Exclusive scan of the rows' ragged lengths -> final offsets (tile base + scan) by wave 1 (up to
 // four rows per lane), written out by the consumers with zeroed str flags. Block-uniform.
-__device__ __forceinline__ void tile_offsets(const DevArgs& a, const TileDesc& td,
-                                             const RowLds& R, const MetaSlot& m, int TR) {
+__device__ __forceinline__ void tile_offsets(const DevArgs& a, const MDSX_L DevCol* cols,
+                                             const TileDesc& td, const RowLds& R,
+                                             const MetaSlot& m, int TR) {
   const int t = threadIdx.x, lane = t & 63;
   const int n = td.table_ok ? int(td.nrows) : 0;
   if ((t >> 6) == 1) {
@@ -398,7 +412,7 @@ __device__ __forceinline__ void tile_offsets(const DevArgs& a, const TileDesc& t
   for (int r = t - 64; r >= 0 && r < n; r += kConsumers) {
     const uint64_t row = td.row0 + r;
     for (int c = 0; c < a.ncols; ++c) {
-      const DevCol& col = a.cols[c];
+      const MDSX_L DevCol& col = cols[c];
       if (col.var_index < 0) continue;
       col.offsets[row] = R.dst[col.var_index * TR + r];
       if (col.flags) col.flags[row] = 0;
@@ -554,6 +568,11 @@ __global__ __launch_bounds__(kStageBlock) void stage_decode_kernel(const DevArgs
   R.ok = reinterpret_cast<uint8_t*>(R.rdst + a.ncols * TR);
   __shared__ uint32_t s_lo[2], s_fits[2];
   __shared__ uint32_t s_first, s_gend, s_ghi;
+  // the column table in LDS: kernel-argument fields indexed by a loop variable compile to vector
+  // loads, whose waits (vmcnt) would also wait for the consumers' stores in flight
+  __shared__ DevCol s_cols[MDSX_MAX_COLUMNS];
+  const MDSX_L DevCol* cols = (const MDSX_L DevCol*)s_cols;
+  for (int c = t; c < a.ncols; c += kStageBlock) s_cols[c] = a.cols[c];
 
   // ---- the run's tiles (plain loads, before any LDS-DMA is in flight)
   for (uint32_t k = uint32_t(t); k < ntiles; k += kStageBlock) {
@@ -603,7 +622,7 @@ __global__ __launch_bounds__(kStageBlock) void stage_decode_kernel(const DevArgs
     const TileDesc td = s_td[k];
     const MetaSlot m = meta(k);
     const int n = td.table_ok ? int(td.nrows) : 0;
-    const uint8_t* st = stage[sb];
+    const lds_u8* st = (const lds_u8*)(stage[sb]);
     const uint32_t lo = s_lo[sb];
     const bool fits = s_fits[sb] != 0;
     if (wave == 0) {  // loader: tile k + 1's bytes, tile k + 2's metadata
@@ -631,9 +650,9 @@ __global__ __launch_bounds__(kStageBlock) void stage_decode_kernel(const DevArgs
       const uint8_t* sample = a.batch + td.shard_off + b;
       if (rc != MDSX_OK) {
         fail_row(a, td, R, TR, r, rc);
-      } else if (fits ? !row_layout(a, R, TR, r, uint64_t(e - b),
+      } else if (fits ? !row_layout(a, cols, R, TR, r, uint64_t(e - b),
                                     [&](int vi) { return lds_u32(st, b - lo + 4u * vi); })
-                      : !row_layout(a, R, TR, r, uint64_t(e - b), [&](int vi) {
+                      : !row_layout(a, cols, R, TR, r, uint64_t(e - b), [&](int vi) {
                           return load_u32_any(sample + 4u * uint32_t(vi));
                         })) {
         fail_row(a, td, R, TR, r, MDSX_E_BOUNDS);
@@ -641,14 +660,14 @@ __global__ __launch_bounds__(kStageBlock) void stage_decode_kernel(const DevArgs
     }
     __syncthreads();
     // ---- 2. ragged offsets
-    tile_offsets(a, td, R, m, TR);
+    tile_offsets(a, cols, td, R, m, TR);
     if (fits) {
-      place_rows(a, td, R, m, TR, lo, 0, n);
+      place_rows(a, cols, td, R, m, TR, lo, 0, n);
       __syncthreads();
       // ---- 3. columns; 4. UTF-8
       if (n && wave > 0) {
-        if (!(a.stage_debug & 2)) write_columns<kNT>(a, td, R, TR, st, 0, n);
-        if (!(a.stage_debug & 4)) check_utf8(a, td, R, TR, st, 0, n);
+        if (!(a.stage_debug & 2)) write_columns<kNT>(a, cols, td, R, TR, st, 0, n);
+        if (!(a.stage_debug & 4)) check_utf8(a, cols, td, R, TR, st, 0, n);
       }
     } else {
       // ---- a tile larger than a stage buffer: row groups that fit, loaded synchronously into
@@ -684,11 +703,11 @@ __global__ __launch_bounds__(kStageBlock) void stage_decode_kernel(const DevArgs
           load_bytes<kNT>(a.batch + td.shard_off + glo, 0, ghi - glo, stage_lds[sb], lane);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        place_rows(a, td, R, m, TR, glo, ga, gb);
+        place_rows(a, cols, td, R, m, TR, glo, ga, gb);
         __syncthreads();
         if (wave > 0) {
-          write_columns<kNT>(a, td, R, TR, st, ga, gb);
-          check_utf8(a, td, R, TR, st, ga, gb);
+          write_columns<kNT>(a, cols, td, R, TR, st, ga, gb);
+          check_utf8(a, cols, td, R, TR, st, ga, gb);
         }
         __syncthreads();  // the buffer is refilled by the next group
         ga = gb;
