@@ -113,13 +113,24 @@ def main():
         e.record()
         torch.cuda.synchronize()
         times['mdsx_copy_probe'].append(s.elapsed_time(e) / args.iters)
+    phases = {}
+    for v, dec in decs.items():  # sdbg bit 16: the staged decode's cycles per phase, per tile
+        dbg = [int(kv[5:], 0) for kv in v.split(',') if kv.startswith('sdbg=')]
+        if dbg and dbg[0] & 16:
+            dec.run()
+            torch.cuda.synchronize()
+            raw = dec.workspace[200:256].cpu().view(torch.int64).tolist()
+            nt = int(dec.batch.tile_shard.numel())
+            phases[v] = dict(zip(['loader_wait', 'rows', 'offsets', 'place', 'write', 'utf8',
+                                  'end_barrier'], [round(x / nt) for x in raw]))
     res = {}
     for v, ts in times.items():
         ms = float(np.median(ts))
         nbytes = 2 * base_batch.buffer.numel() if v in ('torch_copy', 'mdsx_copy_probe') else R + W
         res[v] = {'median_ms': ms, 'min_ms': float(np.min(ts)), 'GBps': nbytes / ms / 1e6}
     print(json.dumps({'config': args.config, 'blob': args.blob, 'chars': args.chars, 'R': R,
-                      'W': W, 'rows': base_batch.total_rows, 'results': res}, indent=1))
+                      'W': W, 'rows': base_batch.total_rows, 'results': res,
+                      'phase_cycles_per_tile': phases}, indent=1))
 
 
 if __name__ == '__main__':

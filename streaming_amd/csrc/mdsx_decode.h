@@ -129,6 +129,9 @@ __device__ __forceinline__ int64_t block_exclusive_scan(int64_t x, int64_t* s_ws
 // Byte offset, inside the workspace's 256-byte status block, of the staged decode's count of
 // huge rows (listed in the src_abs region; mdsx_stage.hip).
 constexpr uint64_t kHugeCountOffset = 192;
+// measurement only (stage_debug & 16): 7 u64 cycle sums of the staged decode's phases
+constexpr uint64_t kStageTimeOffset = 200;
+constexpr uint64_t kStatusBlock = 256;
 
 // The LDS-staged decode of ragged plans (mdsx_stage.hip). Pass 1: the ragged bytes of every tile
 // (then scan_totals_kernel, one entry per tile: a.scan_per == 1). Pass 2: every column of every

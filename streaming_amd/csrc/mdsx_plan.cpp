@@ -305,10 +305,12 @@ int mdsx_plan_create(const char* const* encodings, const int64_t* column_sizes, 
   // output hits L2 instead of HBM: config C 1.94-2.01 vs 2.06-2.10 ms; 1-3 KiB blobs + 200-400-
   // code-point strings 1.51 vs 1.56 ms (tune/strc_*.json).
   p->str_cached = 1;
-  // Ragged plans decode through the LDS stage (mdsx_stage.hip): each tile's shard bytes are read
-  // once, straight into LDS, and every column is written from there. Two stage buffers per
-  // workgroup (one decoded, one in flight).
-  p->stage_kb = p->nvar > 0 ? 24 : 0;
+  // The staged decode (mdsx_stage.hip: each tile's shard bytes read once into LDS, every column
+  // written from there) is opt-in (MDSX_TUNE=stage=24): its per-tile phases are chains of
+  // dependent LDS round trips behind block barriers, measured at 0.6-0.9 TB/s on config C against
+  // 4.3 TB/s for the register/ring decode, and 0.56-0.71 vs 0.89 TB/s on short rows
+  // (scripts/gpu_stage_dbg.sh, profiles/r02/stage_phases.txt).
+  p->stage_kb = 0;
   p->stage_fill = 70;
   apply_tuning(p);
   *out = p;

@@ -613,11 +613,25 @@ __global__ __launch_bounds__(kStageBlock) void stage_decode_kernel(const DevArgs
     if (ntiles > 1) load_meta(a, s_td[1], tile0 + 1, meta(1), lane);
   }
 
+  // measurement only (stage_debug & 16): cycles per phase, summed over the workgroups by the
+  // loader's lane 0 (slot 0: its wait for the DMA) and the first consumer (slots 1-6)
+  const bool timed = (a.stage_debug & 16) != 0;
+  uint64_t ph[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t last = timed ? __builtin_readcyclecounter() : 0;
+  auto stamp = [&](int i) {
+    if (timed) {
+      const uint64_t now = __builtin_readcyclecounter();
+      ph[i] += now - last;
+      last = now;
+    }
+  };
   for (uint32_t k = 0; k < ntiles; ++k) {
     // the bytes of tile k and the metadata of tile k + 1 have landed (the loader's loads; the
     // consumers' stores stay in flight)
     if (wave == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (wave == 0) stamp(0);
     __syncthreads();
+    if (wave > 0) stamp(6);
     const uint32_t sb = k & 1;
     const TileDesc td = s_td[k];
     const MetaSlot m = meta(k);
@@ -659,15 +673,20 @@ __global__ __launch_bounds__(kStageBlock) void stage_decode_kernel(const DevArgs
       }
     }
     __syncthreads();
+    stamp(1);
     // ---- 2. ragged offsets
     tile_offsets(a, cols, td, R, m, TR);
+    stamp(2);
     if (fits) {
       place_rows(a, cols, td, R, m, TR, lo, 0, n);
       __syncthreads();
+      stamp(3);
       // ---- 3. columns; 4. UTF-8
       if (n && wave > 0) {
         if (!(a.stage_debug & 2)) write_columns<kNT>(a, cols, td, R, TR, st, 0, n);
+        stamp(4);
         if (!(a.stage_debug & 4)) check_utf8(a, cols, td, R, TR, st, 0, n);
+        stamp(5);
       }
     } else {
       // ---- a tile larger than a stage buffer: row groups that fit, loaded synchronously into
@@ -715,6 +734,11 @@ __global__ __launch_bounds__(kStageBlock) void stage_decode_kernel(const DevArgs
     }
     __syncthreads();  // stage buffer sb and metadata slot k are refilled from the next tile on
   }
+  if (timed && (t == 0 || t == 64)) {
+    unsigned long long* acc = reinterpret_cast<unsigned long long*>(
+        reinterpret_cast<uint8_t*>(a.status) + kStageTimeOffset);
+    for (int i = t == 0 ? 0 : 1; i < (t == 0 ? 1 : 7); ++i) atomicAdd(acc + i, ph[i]);
+  }
 }
 
 }  // namespace
@@ -740,8 +764,9 @@ int launch_stage_totals(const DevArgs& a, hipStream_t s) {
 }
 
 int launch_stage_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
+  // the huge-row count and (measurement only) the phase cycle sums
   int rc = hip_check(hipMemsetAsync(reinterpret_cast<uint8_t*>(a.status) + kHugeCountOffset, 0,
-                                    sizeof(uint32_t), s),
+                                    kStatusBlock - kHugeCountOffset, s),
                      "hipMemsetAsync");
   if (rc != MDSX_OK) return rc;
   const size_t lds = stage_lds_bytes(plan, a.tile_rows, a.stage_bytes, a.stage_tiles);

@@ -29,7 +29,8 @@ from tests.test_device_decode import _device_digests
 pytestmark = pytest.mark.gpu
 
 MODES = {
-    'stage': '',  # the default
+    'default': '',
+    'stage': 'stage=24',  # the staged decode (opt-in; measured slower)
     'stage_overflow': 'stage=4,fill=300',  # tiles of ~3x the stage: several row groups each
     'stage_tiny': 'stage=1',  # rows over 1 KiB go through the huge-row kernel
     'stage_big': 'stage=64,fill=90',
