@@ -33,6 +33,17 @@ __device__ __forceinline__ MDSX_G T* gp_at(uint64_t a) {
   return (MDSX_G T*)a;
 }
 
+// LDS pointers carry their address space, so every stage access compiles to ds_read (a generic
+// pointer compiles to flat_load, which counts in vmcnt too: every wait for it would also wait for
+// the consumers' stores in flight). The host pass only parses these device functions: it gets no
+// address space (its vector types do not bind LDS references).
+#ifdef __HIP_DEVICE_COMPILE__
+#define MDSX_L __attribute__((address_space(3)))
+#else
+#define MDSX_L
+#endif
+typedef MDSX_L uint8_t lds_u8;
+
 // 16-byte global load / store, optionally non-temporal (streamed once: no reuse in L2/MALL).
 template <bool kNT>
 __device__ __forceinline__ uint4 ld16(const uint4* p) {
@@ -215,6 +226,13 @@ __device__ __forceinline__ uint4 byte_mask(uint32_t a, uint32_t b) {
     m[j] = uint32_t(mh & ~ml);
   }
   return make_uint4(m[0], m[1], m[2], m[3]);
+}
+
+// Bytes [a, b) (0 <= a <= b <= 16) of `val` merged into `acc`.
+__device__ __forceinline__ uint4 merge_bytes(uint4 acc, const uint4 val, uint32_t a, uint32_t b) {
+  const uint4 m = byte_mask(a, b);
+  return make_uint4((acc.x & ~m.x) | (val.x & m.x), (acc.y & ~m.y) | (val.y & m.y),
+                    (acc.z & ~m.z) | (val.z & m.z), (acc.w & ~m.w) | (val.w & m.w));
 }
 
 // ---- strict UTF-8 well-formedness, 4 bytes per dword op (SWAR) ------------------------------

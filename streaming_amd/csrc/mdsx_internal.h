@@ -48,6 +48,8 @@ struct mdsx_plan {
   int stage_tiles = 0;  // tiles per workgroup of the staged decode (0: per launch)
   int stage_debug = 0;  // measurement only: parts of the staged decode skipped (bits)
   int stage_fill = 70;  // percent of a stage buffer a tile's samples fill on average (tile sizing)
+  int run_slots = 0;    // ragged plans: KiB of the streaming decode's per-wave LDS ring (0: off)
+  int run_kb = 64;      // streaming decode: about this many KiB of samples per tile (tile sizing)
   int gather_chunks = 2;  // 16-byte chunks per lane in the ragged gather (tile = 4 KiB x this)
   int gather_min = 256;   // ragged columns averaging fewer bytes per row use the gather kernel
   int group_max = 1024;   // ... fewer than this (and >= gather_min): four rows per wave

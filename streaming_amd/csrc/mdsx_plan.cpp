@@ -209,6 +209,10 @@ void apply_tuning(mdsx_plan* p) {
       p->stage_kb = int(v);
     } else if (key == "fill" && v >= 10 && v <= 400) {  // > 100: tiles overflow the stage
       p->stage_fill = int(v);
+    } else if (key == "run" && (v == 0 || v == 4 || v == 8 || v == 16)) {
+      p->run_slots = int(v);
+    } else if (key == "rkb" && v >= 1 && v <= 4096) {
+      p->run_kb = int(v);
     }
   }
 }
@@ -327,6 +331,13 @@ int mdsx_plan_tile_rows(const mdsx_plan* plan) { return plan ? plan->tile_rows :
 
 int mdsx_plan_tile_rows_for(const mdsx_plan* plan, uint64_t shard_bytes, uint64_t rows) {
   if (!plan) return MDSX_E_ARG;
+  if (plan->nvar > 0 && plan->run_slots > 0 && rows > 0) {
+    // streaming decode: about run_kb KiB of samples per tile (one wave's run), 1..32 rows
+    const uint64_t per_row = std::max<uint64_t>(1, shard_bytes / rows);
+    int tr = 1;
+    while (tr < 32 && uint64_t(tr) * 2 * per_row <= uint64_t(plan->run_kb) * 1024) tr *= 2;
+    return tr;
+  }
   if (plan->nvar == 0 || plan->stage_kb == 0 || rows == 0) return plan->tile_rows;
   const uint64_t target = uint64_t(plan->stage_kb) * 1024 * uint64_t(plan->stage_fill) / 100;
   const uint64_t per_row = std::max<uint64_t>(1, shard_bytes / rows);

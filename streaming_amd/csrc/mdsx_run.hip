@@ -1,0 +1,372 @@
+// Streaming decode of ragged plans (gfx950): every wave decodes one tile -- a run of consecutive
+// samples of one shard -- by streaming the run's bytes through a private LDS ring ONCE, in file
+// order, and writing every column from there.
+//
+// The reference decodes one sample per call: MDSReader.get_sample_data reads the sample's byte
+// range (streaming/base/format/mds/reader.py:128-149), decode_sample splits it at the u32 size
+// heads of the variable columns (mds/reader.py:103-126) and each column's decoder returns its
+// value (encodings.py:62-397, 760-773). In an MDS shard the samples of a run are contiguous --
+// sample i ends where sample i + 1 starts (offsets[i + 1]) -- so a run is one byte range.
+//
+// Pass 1 (stage_totals_kernel + the reduce-then-scan kernels, mdsx_stage.hip / mdsx_kernels.hip):
+// each tile's ragged bytes from the offsets table and the heads, scanned into each tile's output
+// base per ragged column.
+//
+// Pass 2 (run_decode_kernel): a wave keeps up to S KiB of its run in flight into its LDS ring
+// (global_load_lds_dwordx4: 1 KiB per wave-instruction, no VGPR destination) and walks the run's
+// samples in order, all control wave-uniform:
+//   * the sample's size heads are read from the ring (decode_sample's head loop) and its column
+//     boundaries checked against its size (mds/reader.py:111-125);
+//   * each column's bytes are written destination-major: lane k of a group owns 16-byte-aligned
+//     output chunk k of the column, realigned from two aligned ring chunks (v_alignbyte). The
+//     outputs of a column are contiguous over the run, so the chunk a sample leaves partly filled
+//     is carried (in the column's lane of a lane-distributed register) into the next sample's
+//     first chunk: every store is a whole 16-byte chunk except the two a run shares with its
+//     neighbours;
+//   * str values are checked for strict UTF-8 on the same registers (what bytes.decode('utf-8')
+//     accepts, encodings.py:80-81), no second read;
+//   * ragged offsets and UTF-8 flags are collected in LDS and written once per run, coalesced.
+// So every byte of the shard range is read from HBM once (the heads, the column boundaries and
+// the str bytes the check reads come from the ring) and the outputs are written once in whole
+// chunks. The ring waits are explicit `s_waitcnt vmcnt(n)`, n = the vector-memory operations this
+// wave issued after the slot's load (its loads, and stores certain to have issued), as in the
+// ring of mdsx_kernels.hip.
+//
+// A run with a sample whose offsets fail the file checks is decoded sample by sample straight
+// from HBM (wave_copy), every bad sample reported: the stream order no longer holds there.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+
+#include "mdsx_decode.h"
+#include "mdsx_device.h"
+#include "mdsx_internal.h"
+
+namespace mdsx_kernels {
+namespace {
+
+constexpr int kRunBlock = 256;  // 4 waves, one tile each
+constexpr int kRunWaves = kRunBlock / 64;
+constexpr int kRunMaxRows = 32;  // rows of a tile: one offsets-table entry per lane (+1)
+
+__host__ __device__ __forceinline__ uint32_t run_wave_lds(int S, int TR, int nvar) {
+  return (uint32_t(S) * 1024u + uint32_t(nvar) * uint32_t(TR) * 9u + 15u) & ~15u;
+}
+
+// Stream chunk q (16 bytes) of the ring: slot (q / 64) % S, position q % 64.
+template <int S>
+__device__ __forceinline__ uint4 ring_chunk(const lds_u8* ring, uint32_t q) {
+  const u32x4 v = *(const MDSX_L u32x4*)(ring + ((((q >> 6) & (S - 1)) << 10) | ((q & 63u) << 4)));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// 16 stream bytes at stream byte p (any alignment; bytes before the stream start read as zero).
+template <int S>
+__device__ __forceinline__ uint4 ring16(const lds_u8* ring, int64_t p) {
+  const int64_t q = p >> 4;  // floor
+  const uint4 lo = q >= 0 ? ring_chunk<S>(ring, uint32_t(q)) : make_uint4(0, 0, 0, 0);
+  return funnel16_lane(lo, ring_chunk<S>(ring, uint32_t(q + 1)), uint32_t(p) & 15u);
+}
+
+// u32 at stream byte p (any alignment).
+template <int S>
+__device__ __forceinline__ uint32_t ring_u32(const lds_u8* ring, uint32_t p) {
+  auto dw = [&](uint32_t w) {  // stream dword w
+    const uint32_t q = w >> 2;
+    return *(const MDSX_L uint32_t*)(ring + ((((q >> 6) & (S - 1)) << 10) | ((q & 63u) << 4) |
+                                             ((w & 3u) << 2)));
+  };
+  const uint32_t w = p >> 2;
+  return alignbyte(dw(w + 1), dw(w), p & 3u);
+}
+
+// The wave's stream: chunks [0, nq) from base, in slots of 64 chunks.
+struct Stream {
+  const uint4* base;
+  uint32_t nq, nslots;
+  uint32_t issued;  // slots issued
+  uint32_t ops;     // vector-memory operations issued by this wave (loads; stores certain to issue)
+  uint32_t op_at;   // lane r: `ops` when the slot now in ring position r was issued
+};
+
+// Issue slots while they fit in the ring above slot `low`: the stream bytes still to be read
+// all lie in slots >= low (callers pass a non-decreasing low).
+template <int S, bool kNT>
+__device__ __forceinline__ void pump(Stream& st, uint32_t ring_lds, uint32_t low, int lane) {
+  while (st.issued < st.nslots && st.issued < low + S) {
+    const uint32_t k = st.issued * 64u + uint32_t(lane);
+    glds16<kNT>(st.base + min(k, st.nq - 1), ring_lds + ((st.issued & (S - 1)) << 10));
+    if (lane == int(st.issued & (S - 1))) st.op_at = st.ops;
+    ++st.ops;
+    ++st.issued;
+  }
+}
+
+// pump, then wait until stream bytes [lo, hi] (hi - lo < (S - 1) KiB) have landed.
+template <int S, bool kNT>
+__device__ __forceinline__ void ensure(Stream& st, uint32_t ring_lds, uint32_t lo, uint32_t hi,
+                                       int lane) {
+  pump<S, kNT>(st, ring_lds, lo >> 10, lane);
+  const uint32_t upto = min(hi >> 10, st.nslots - 1);
+  wait_vm_at_most(st.ops - uint32_t(__builtin_amdgcn_readlane(int(st.op_at), int(upto & (S - 1)))) -
+                  1u);
+}
+
+__device__ __forceinline__ uint4 readlane4(const uint4 v, int l) {
+  return make_uint4(__builtin_amdgcn_readlane(v.x, l), __builtin_amdgcn_readlane(v.y, l),
+                    __builtin_amdgcn_readlane(v.z, l), __builtin_amdgcn_readlane(v.w, l));
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+  return uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v)), l))) |
+         (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v >> 32)), l))) << 32);
+}
+
+// The per-column state of a wave, lane-distributed (lane c: column c).
+struct Cursors {
+  uint64_t cur;  // next output byte address of the column
+  uint64_t cst;  // first output byte of the column's current contiguous stretch (bytes below it
+                 // belong to another run)
+  uint4 carry;   // the partly filled chunk at cur & ~15 (bytes below cur valid from cst on)
+};
+
+// Write out the partly filled chunk of column c (the bytes [max(cst, chunk), cur)).
+__device__ __forceinline__ void flush(const Cursors& k, int c, int lane) {
+  const uint64_t cur = readlane64(k.cur, c), cst = readlane64(k.cst, c);
+  if ((cur & 15) == 0) return;
+  const uint64_t C = cur & ~uint64_t(15);
+  const uint64_t lo = max(cst, C);
+  if (lo >= cur) return;
+  wave_edge_store(k.carry, c, C, lo, cur, lane);
+}
+
+// Column c of one sample: output bytes [d, d + len) from stream bytes [sp, sp + len).
+// Returns (str columns, kUtf8) whether the value is not well-formed UTF-8 (wave-uniform).
+template <int S, bool kNT>
+__device__ __forceinline__ bool copy_segment(Stream& st, const lds_u8* ring, uint32_t ring_lds,
+                                             Cursors& k, int c, uint64_t d, uint32_t len,
+                                             uint32_t sp, bool utf8, int lane) {
+  if (len == 0) return false;
+  if (readlane64(k.cur, c) != d) {  // a gap (a skipped sample's fixed bytes): a new stretch
+    flush(k, c, lane);
+    if (lane == c) k.cst = d;
+  }
+  const uint64_t cst = readlane64(k.cst, c);
+  const uint4 carry = readlane4(k.carry, c);
+  const uint64_t dbeg = d & ~uint64_t(15), dend = d + len;
+  const uint32_t head = uint32_t(d - dbeg);                 // carried bytes in the first chunk
+  const uint32_t nch = uint32_t((dend + 15 - dbeg) >> 4);   // chunks touched
+  const uint32_t nfull = uint32_t((dend - dbeg) >> 4);      // chunks completed by this value
+  const uint64_t cchunk = cst & ~uint64_t(15);              // the stretch's shared first chunk
+  const bool cpart = (cst & 15) != 0;
+  bool bad = false;
+  uint32_t prev_w = 0;
+  uint4 last = make_uint4(0, 0, 0, 0);
+  // the stretch's first chunk, when another run owns its leading bytes: index inside this value
+  const uint32_t kc = cpart && cchunk >= dbeg ? uint32_t((cchunk - dbeg) >> 4) : 0xffffffffu;
+  for (uint32_t g0 = 0; g0 < nch; g0 += 64) {
+    // stream bytes lane l reads: 16 from s0 + 16 l, s0 = sp + 16 g0 - head (the bytes before sp
+    // are the carried ones, masked below); live bytes from max(sp, s0) on
+    const int64_t s0 = int64_t(sp) + 16 * int64_t(g0) - int64_t(head);
+    ensure<S, kNT>(st, ring_lds, g0 ? uint32_t(s0) : sp, uint32_t(s0 + 64 * 16 + 15), lane);
+    const uint32_t kk = g0 + uint32_t(lane);
+    const uint64_t D = dbeg + 16ull * kk;
+    uint4 val = ring16<S>(ring, s0 + 16 * int64_t(lane));
+    if (kk == 0 && head) val = merge_bytes(val, carry, 0, head);
+    // whole chunks are stored whole, except the stretch's shared first chunk (its own bytes only)
+    if (kk < nfull && kk != kc) st16<kNT>(D, val);
+    const uint32_t f1 = min(nfull, g0 + 64);
+    if (f1 > g0 + ((kc >= g0 && kc < f1) ? 1u : 0u)) ++st.ops;  // a store certain to have issued
+    if (kc >= g0 && kc < f1) wave_edge_store(val, int(kc - g0), cchunk, cst, cchunk + 16, lane);
+    if (utf8) {
+      const uint4 vout = keep_range(val, D, d, dend);
+      uint32_t pw = __shfl_up(vout.w, 1);
+      if (lane == 0) pw = prev_w;
+      prev_w = __builtin_amdgcn_readlane(vout.w, 63);
+      if (kk < nch) bad |= utf8_chunk_bad(vout, pw, kk == nch - 1);
+    }
+    if (nch - 1 >= g0 && nch - 1 < g0 + 64) last = readlane4(val, int(nch - 1 - g0));
+  }
+  if (lane == c) {
+    k.cur = dend;
+    k.carry = last;  // the chunk at dend & ~15 (meaningful when dend is not aligned)
+  }
+  return utf8 ? __any(bad) : false;
+}
+
+template <int S, bool kNT>
+__global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  __shared__ DevCol s_cols[MDSX_MAX_COLUMNS];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  // the column table in LDS: kernel-argument fields indexed by a loop variable compile to vector
+  // loads, whose waits would also wait for the ring's loads and the stores in flight
+  for (int c = t; c < a.ncols; c += kRunBlock) s_cols[c] = a.cols[c];
+  __syncthreads();
+  const MDSX_L DevCol* cols = (const MDSX_L DevCol*)s_cols;
+  const uint32_t tile = blockIdx.x * kRunWaves + uint32_t(wave);
+  if (tile >= a.ntiles) return;  // wave-uniform; no barrier below
+  const int TR = a.tile_rows;
+  const int ncols = a.ncols, nvar = a.nvar;
+  uint8_t* wl = smem + size_t(wave) * run_wave_lds(S, TR, nvar);
+  const lds_u8* ring = (const lds_u8*)wl;
+  MDSX_L int64_t* obuf = (MDSX_L int64_t*)(wl + S * 1024);         // [nvar][TR]
+  MDSX_L uint8_t* fbuf = (MDSX_L uint8_t*)(wl + S * 1024 + nvar * TR * 8);  // [nvar][TR]
+  const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((const MDSX_L uint8_t*)wl)));
+
+  const TileView v = tile_view(a, tile);
+  if (lane == 0 && tile == v.d.tile0) {
+    // header written by encode_joint_shard (mds/writer.py:133-144): u32 N, then N + 1 offsets
+    if (!v.table_ok || *reinterpret_cast<const uint32_t*>(v.shard) != v.d.samples ||
+        v.offs[0] < v.hdr_end || v.offs[v.d.samples] > v.d.bytes)
+      report(a.status, MDSX_E_HEADER, v.shard_idx, -1, -1);
+  }
+  if (!v.table_ok) return;
+  const int n = int(v.nrows);
+  if (n == 0) return;
+  const uint64_t row0 = v.d.row0 + v.r0;
+
+  // this run's offsets-table slice: lane j holds offsets[r0 + j] (j <= n)
+  const uint32_t ob = lane <= n ? v.offs[v.r0 + lane] : 0u;
+  const uint32_t oe = __shfl_down(ob, 1);
+  const bool range_ok = lane >= n || (v.hdr_end <= ob && ob < oe && oe <= v.d.bytes);
+  const bool fast = __all(range_ok);
+
+  // column cursors at the run's first output byte
+  Cursors k;
+  k.carry = make_uint4(0, 0, 0, 0);
+  k.cur = 0;
+  if (lane < ncols) {
+    const MDSX_L DevCol& col = cols[lane];
+    const uint64_t data = reinterpret_cast<uint64_t>(col.data);
+    k.cur = col.var_index < 0
+                ? data + row0 * col.row_bytes
+                : data + uint64_t(a.tile_prefix[uint64_t(col.var_index) * a.nscan + tile]);
+  }
+  k.cst = k.cur;
+
+  Stream st;
+  const uint64_t first = reinterpret_cast<uint64_t>(v.shard) + __builtin_amdgcn_readfirstlane(ob);
+  const uint64_t sbase = first & ~uint64_t(15);
+  st.base = reinterpret_cast<const uint4*>(sbase);
+  st.nq = 0;
+  st.nslots = 0;
+  st.issued = 0;
+  st.ops = 0;
+  st.op_at = 0;
+  if (fast) {
+    const uint64_t last =
+        reinterpret_cast<uint64_t>(v.shard) + uint32_t(__builtin_amdgcn_readlane(int(ob), n));
+    st.nq = uint32_t((last - sbase + 15) >> 4);
+    st.nslots = (st.nq + 63) >> 6;
+    pump<S, kNT>(st, ring_lds, 0, lane);  // the first S KiB in flight
+  }
+
+  for (int j = 0; j < n; ++j) {  // wave-uniform
+    const uint32_t b = uint32_t(__builtin_amdgcn_readlane(int(ob), j));
+    const uint32_t e = uint32_t(__builtin_amdgcn_readlane(int(ob), j + 1));
+    const uint64_t srow = reinterpret_cast<uint64_t>(v.shard) + b;  // the sample's first byte
+    const uint32_t size = e - b;
+    int rc = MDSX_OK;
+    if (!fast) {
+      if (!(v.hdr_end <= b && b <= e && e <= v.d.bytes)) rc = MDSX_E_BOUNDS;
+      else if (b == e) rc = MDSX_E_EMPTY;
+    }
+    const uint32_t sp = uint32_t(srow - sbase);  // stream position (fast path)
+    // size heads: lane vi holds head vi
+    uint32_t h = 0;
+    if (rc == MDSX_OK && 4u * uint32_t(nvar) <= size && nvar > 0) {
+      if (fast) {
+        ensure<S, kNT>(st, ring_lds, sp, sp + 4u * uint32_t(nvar) + 3u, lane);
+        if (lane < nvar) h = ring_u32<S>(ring, sp + 4u * uint32_t(lane));
+      } else if (lane < nvar) {
+        h = load_u32_any(reinterpret_cast<const uint8_t*>(srow) + 4u * uint32_t(lane));
+      }
+    }
+    if (rc == MDSX_OK) {
+      if (4u * uint32_t(nvar) > size) {
+        rc = MDSX_E_BOUNDS;
+      } else {
+        uint64_t need = 4ull * uint32_t(nvar);
+        for (int c = 0; c < ncols; ++c) {
+          const int vi = cols[c].var_index;
+          need += vi >= 0 ? uint32_t(__builtin_amdgcn_readlane(int(h), vi)) : cols[c].row_bytes;
+        }
+        if (need > size) rc = MDSX_E_BOUNDS;
+      }
+    }
+    if (rc != MDSX_OK && lane == 0) report(a.status, rc, v.shard_idx, int(v.r0 + j), -1);
+    uint32_t rel = 4u * uint32_t(nvar);
+    for (int c = 0; c < ncols; ++c) {
+      const MDSX_L DevCol& col = cols[c];
+      const int vi = col.var_index;
+      const uint32_t len = rc != MDSX_OK ? 0u
+                           : vi >= 0     ? uint32_t(__builtin_amdgcn_readlane(int(h), vi))
+                                         : col.row_bytes;
+      const bool utf8 = col.kind == MDSX_KIND_STR && col.flags != nullptr;
+      uint64_t d = readlane64(k.cur, c);
+      if (vi < 0) d = reinterpret_cast<uint64_t>(col.data) + (row0 + j) * col.row_bytes;
+      if (vi >= 0 && lane == 0) obuf[vi * TR + j] = int64_t(d - reinterpret_cast<uint64_t>(col.data));
+      bool bad = false;
+      if (len && vi >= 0 && d - reinterpret_cast<uint64_t>(col.data) + len > col.capacity) {
+        if (lane == 0) report(a.status, MDSX_E_CAPACITY, v.shard_idx, int(v.r0 + j), c);
+      } else if (len && fast) {
+        bad = copy_segment<S, kNT>(st, ring, ring_lds, k, c, d, len, sp + rel, utf8, lane);
+      } else if (len) {
+        const uint8_t* src = reinterpret_cast<const uint8_t*>(srow) + rel;
+        uint8_t* dst = reinterpret_cast<uint8_t*>(d);
+        bad = utf8 ? wave_copy<true, 2, kNT>(src, dst, len, lane)
+                   : wave_copy<false, 2, kNT>(src, dst, len, lane);
+        if (lane == c) k.cur = d + len, k.cst = d + len;
+      }
+      if (utf8 && lane == 0) fbuf[vi * TR + j] = bad ? 1 : 0;
+      rel += len;
+    }
+  }
+  // the partly filled last chunk of every column; the run's offsets and flags
+  if (fast)
+    for (int c = 0; c < ncols; ++c) flush(k, c, lane);
+  for (int c = 0; c < ncols; ++c) {
+    const MDSX_L DevCol& col = cols[c];
+    const int vi = col.var_index;
+    if (vi < 0) continue;
+    if (lane < n) *gp(col.offsets + row0 + lane) = obuf[vi * TR + lane];
+    if (col.kind == MDSX_KIND_STR && col.flags && lane < n)
+      *gp(col.flags + row0 + lane) = fbuf[vi * TR + lane];
+  }
+}
+
+}  // namespace
+
+int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
+  const unsigned grid = (a.ntiles + kRunWaves - 1) / kRunWaves;
+  const size_t lds = size_t(kRunWaves) * run_wave_lds(a.run_slots, a.tile_rows, a.nvar);
+  if (a.tile_rows > kRunMaxRows)
+    return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode tiles hold at most 32 rows");
+#define MDSX_RUN_CASE(S, NT)                                                              \
+  if (a.run_slots == S && bool(plan->nontemporal) == NT) {                                \
+    if (lds > 64 * 1024) {                                                                \
+      const int rc = hip_check(                                                           \
+          hipFuncSetAttribute(reinterpret_cast<const void*>(run_decode_kernel<S, NT>),    \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)),      \
+          "hipFuncSetAttribute");                                                         \
+      if (rc != MDSX_OK) return rc;                                                       \
+    }                                                                                     \
+    mdsx::set_last_kernel("run_decode_kernel<" #S ", " #NT ">");                         \
+    hipLaunchKernelGGL((run_decode_kernel<S, NT>), dim3(grid), dim3(kRunBlock), lds, s, a); \
+    return hip_check(hipGetLastError(), "run_decode_kernel launch");                      \
+  }
+  MDSX_RUN_CASE(4, true)
+  MDSX_RUN_CASE(4, false)
+  MDSX_RUN_CASE(8, true)
+  MDSX_RUN_CASE(8, false)
+  MDSX_RUN_CASE(16, true)
+  MDSX_RUN_CASE(16, false)
+#undef MDSX_RUN_CASE
+  return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode ring of 4, 8 or 16 KiB");
+}
+
+}  // namespace mdsx_kernels

@@ -54,16 +54,6 @@ constexpr int kMetaSlots = 3;
 constexpr int kStageBlock = 512;
 constexpr int kConsumers = kStageBlock - 64;
 
-// LDS pointers carry their address space, so every stage access compiles to ds_read (a generic
-// pointer compiles to flat_load, which counts in vmcnt too: every wait for it would also wait for
-// the consumers' stores in flight). The host pass only parses these device functions: it gets no
-// address space (its vector types do not bind LDS references).
-#ifdef __HIP_DEVICE_COMPILE__
-#define MDSX_L __attribute__((address_space(3)))
-#else
-#define MDSX_L
-#endif
-typedef MDSX_L uint8_t lds_u8;
 
 // 16 bytes of a stage buffer at byte position p (any alignment, -16 < p < cap: a buffer has 16
 // bytes of slack on either side).
@@ -76,13 +66,6 @@ __device__ __forceinline__ uint4 lds16(const lds_u8* stage, int32_t p) {
 __device__ __forceinline__ uint32_t lds_u32(const lds_u8* stage, uint32_t p) {
   const MDSX_L uint32_t* q = reinterpret_cast<const MDSX_L uint32_t*>(stage + (p & ~3u));
   return alignbyte(q[1], q[0], p & 3u);
-}
-
-// Bytes [a, b) (0 <= a <= b <= 16) of `val` merged into `acc`.
-__device__ __forceinline__ uint4 merge_bytes(uint4 acc, const uint4 val, uint32_t a, uint32_t b) {
-  const uint4 m = byte_mask(a, b);
-  return make_uint4((acc.x & ~m.x) | (val.x & m.x), (acc.y & ~m.y) | (val.y & m.y),
-                    (acc.z & ~m.z) | (val.z & m.z), (acc.w & ~m.w) | (val.w & m.w));
 }
 
 // Strict UTF-8 of four staged rows per wave, one per 16-lane group: lane gl of a group checks

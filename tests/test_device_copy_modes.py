@@ -30,6 +30,9 @@ pytestmark = pytest.mark.gpu
 
 MODES = {
     'default': '',
+    'run': 'run=8',  # the streaming decode (mdsx_run.hip)
+    'run4': 'run=4,rkb=4',  # small ring, 1-2-row tiles
+    'run16': 'run=16,rkb=1024',  # 32-row tiles
     'stage': 'stage=24',  # the staged decode (opt-in; measured slower)
     'stage_overflow': 'stage=4,fill=300',  # tiles of ~3x the stage: several row groups each
     'stage_tiny': 'stage=1',  # rows over 1 KiB go through the huge-row kernel
