@@ -121,8 +121,13 @@ def main():
             torch.cuda.synchronize()
             raw = dec.workspace[200:256].cpu().view(torch.int64).tolist()
             nt = int(dec.batch.tile_shard.numel())
-            phases[v] = dict(zip(['loader_wait', 'rows', 'offsets', 'place', 'write', 'utf8',
-                                  'end_barrier'], [round(x / nt) for x in raw]))
+            if 'run=' in v:  # streaming decode: per-wave (tile) ring-wait and total cycles
+                phases[v] = {'ring_wait': round(raw[0] / max(raw[2], 1)),
+                             'total': round(raw[1] / max(raw[2], 1)), 'waves': raw[2],
+                             'rows_per_tile': dec.batch.tile_rows}
+            else:
+                phases[v] = dict(zip(['loader_wait', 'rows', 'offsets', 'place', 'write', 'utf8',
+                                      'end_barrier'], [round(x / nt) for x in raw]))
     res = {}
     for v, ts in times.items():
         ms = float(np.median(ts))

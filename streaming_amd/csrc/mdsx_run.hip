@@ -32,8 +32,8 @@
 // wave issued after the slot's load (its loads, and stores certain to have issued), as in the
 // ring of mdsx_kernels.hip.
 //
-// A run with a sample whose offsets fail the file checks is decoded sample by sample straight
-// from HBM (wave_copy), every bad sample reported: the stream order no longer holds there.
+// A run with a sample whose offsets fail the file checks streams each good sample on its own
+// (every bad one reported): the file order of the run no longer holds there.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -88,6 +88,9 @@ struct Stream {
   uint32_t issued;  // slots issued
   uint32_t ops;     // vector-memory operations issued by this wave (loads; stores certain to issue)
   uint32_t op_at;   // lane r: `ops` when the slot now in ring position r was issued
+  uint32_t dbg;     // measurement only (MDSX_TUNE sdbg): 1 no stores, 2 no UTF-8, 4 no copies,
+                    // 8 no ring waits, 16 cycle sums
+  uint64_t wait_cycles;
 };
 
 // Issue slots while they fit in the ring above slot `low`: the stream bytes still to be read
@@ -109,8 +112,11 @@ __device__ __forceinline__ void ensure(Stream& st, uint32_t ring_lds, uint32_t l
                                        int lane) {
   pump<S, kNT>(st, ring_lds, lo >> 10, lane);
   const uint32_t upto = min(hi >> 10, st.nslots - 1);
+  if (st.dbg & 8) return;
+  const uint64_t t0 = (st.dbg & 16) ? __builtin_readcyclecounter() : 0;
   wait_vm_at_most(st.ops - uint32_t(__builtin_amdgcn_readlane(int(st.op_at), int(upto & (S - 1)))) -
                   1u);
+  if (st.dbg & 16) st.wait_cycles += __builtin_readcyclecounter() - t0;
 }
 
 __device__ __forceinline__ uint4 readlane4(const uint4 v, int l) {
@@ -141,52 +147,74 @@ __device__ __forceinline__ void flush(const Cursors& k, int c, int lane) {
   wave_edge_store(k.carry, c, C, lo, cur, lane);
 }
 
+// Bytes [0, n) of `v` zeroed (n uniform, 0 <= n <= 16).
+__device__ __forceinline__ uint4 zero_below(const uint4 v, uint32_t n) {
+  const uint4 m = byte_mask(0, n);
+  return make_uint4(v.x & ~m.x, v.y & ~m.y, v.z & ~m.z, v.w & ~m.w);
+}
+
 // Column c of one sample: output bytes [d, d + len) from stream bytes [sp, sp + len).
-// Returns (str columns, kUtf8) whether the value is not well-formed UTF-8 (wave-uniform).
+// Returns (utf8: a str column) whether the value is not well-formed UTF-8 (wave-uniform).
+// Everything but the per-lane chunk is wave-uniform: the source shift of a value is one shift
+// for all its chunks (funnel16, four v_alignbyte), the carried bytes and the value's last
+// partial chunk are handled under uniform branches.
 template <int S, bool kNT>
 __device__ __forceinline__ bool copy_segment(Stream& st, const lds_u8* ring, uint32_t ring_lds,
                                              Cursors& k, int c, uint64_t d, uint32_t len,
                                              uint32_t sp, bool utf8, int lane) {
-  if (len == 0) return false;
   if (readlane64(k.cur, c) != d) {  // a gap (a skipped sample's fixed bytes): a new stretch
     flush(k, c, lane);
     if (lane == c) k.cst = d;
   }
   const uint64_t cst = readlane64(k.cst, c);
-  const uint4 carry = readlane4(k.carry, c);
   const uint64_t dbeg = d & ~uint64_t(15), dend = d + len;
   const uint32_t head = uint32_t(d - dbeg);                 // carried bytes in the first chunk
+  const uint32_t tail = uint32_t(dend & 15);                // bytes of the last chunk, if partial
   const uint32_t nch = uint32_t((dend + 15 - dbeg) >> 4);   // chunks touched
   const uint32_t nfull = uint32_t((dend - dbeg) >> 4);      // chunks completed by this value
-  const uint64_t cchunk = cst & ~uint64_t(15);              // the stretch's shared first chunk
-  const bool cpart = (cst & 15) != 0;
+  // the stretch's first chunk, when another run owns its leading bytes: index inside this value
+  const uint64_t cchunk = cst & ~uint64_t(15);
+  const uint32_t kc =
+      (cst & 15) && cchunk >= dbeg ? uint32_t((cchunk - dbeg) >> 4) : 0xffffffffu;
+  // chunk kk of the value holds stream bytes from sp - head + 16 kk: stream chunk q0 + kk, shift sh
+  const uint32_t s0 = sp - head;  // wraps below 0 only on the first value of the stream
+  const uint32_t q0 = uint32_t(int32_t(s0) >> 4), sh = s0 & 15u;
   bool bad = false;
   uint32_t prev_w = 0;
   uint4 last = make_uint4(0, 0, 0, 0);
-  // the stretch's first chunk, when another run owns its leading bytes: index inside this value
-  const uint32_t kc = cpart && cchunk >= dbeg ? uint32_t((cchunk - dbeg) >> 4) : 0xffffffffu;
   for (uint32_t g0 = 0; g0 < nch; g0 += 64) {
-    // stream bytes lane l reads: 16 from s0 + 16 l, s0 = sp + 16 g0 - head (the bytes before sp
-    // are the carried ones, masked below); live bytes from max(sp, s0) on
-    const int64_t s0 = int64_t(sp) + 16 * int64_t(g0) - int64_t(head);
-    ensure<S, kNT>(st, ring_lds, g0 ? uint32_t(s0) : sp, uint32_t(s0 + 64 * 16 + 15), lane);
+    ensure<S, kNT>(st, ring_lds, g0 ? s0 + 16u * g0 : sp, s0 + 16u * g0 + 64u * 16u + 15u, lane);
     const uint32_t kk = g0 + uint32_t(lane);
-    const uint64_t D = dbeg + 16ull * kk;
-    uint4 val = ring16<S>(ring, s0 + 16 * int64_t(lane));
-    if (kk == 0 && head) val = merge_bytes(val, carry, 0, head);
-    // whole chunks are stored whole, except the stretch's shared first chunk (its own bytes only)
-    if (kk < nfull && kk != kc) st16<kNT>(D, val);
-    const uint32_t f1 = min(nfull, g0 + 64);
-    if (f1 > g0 + ((kc >= g0 && kc < f1) ? 1u : 0u)) ++st.ops;  // a store certain to have issued
-    if (kc >= g0 && kc < f1) wave_edge_store(val, int(kc - g0), cchunk, cst, cchunk + 16, lane);
-    if (utf8) {
-      const uint4 vout = keep_range(val, D, d, dend);
-      uint32_t pw = __shfl_up(vout.w, 1);
-      if (lane == 0) pw = prev_w;
-      prev_w = __builtin_amdgcn_readlane(vout.w, 63);
-      if (kk < nch) bad |= utf8_chunk_bad(vout, pw, kk == nch - 1);
+    const uint32_t q = q0 + kk;
+    uint4 val = ring_chunk<S>(ring, q);
+    if (sh) val = funnel16(val, ring_chunk<S>(ring, q + 1), sh);
+    if (g0 == 0 && head) {  // the bytes carried from the column's previous value
+      const uint4 carry = readlane4(k.carry, c);
+      if (lane == 0) val = merge_bytes(val, carry, 0, head);
     }
-    if (nch - 1 >= g0 && nch - 1 < g0 + 64) last = readlane4(val, int(nch - 1 - g0));
+    // whole chunks are stored whole, except the stretch's shared first chunk (its own bytes only)
+    const uint32_t f1 = min(nfull, g0 + 64);
+    const bool kc_here = kc >= g0 && kc < f1;
+    if (!(st.dbg & 1)) {
+      if (kk < nfull && kk != kc) st16<kNT>(dbeg + 16ull * kk, val);
+      if (f1 > g0 + (kc_here ? 1u : 0u)) ++st.ops;  // a store certain to have issued
+    }
+    if (kc_here) wave_edge_store(val, int(kc - g0), cchunk, cst, cchunk + 16, lane);
+    const bool last_here = nch - 1 < g0 + 64;
+    if (utf8 && !(st.dbg & 2)) {
+      // this value's bytes only: the carried ones and those past its end zeroed
+      uint4 vout = kk < nch ? val : make_uint4(0, 0, 0, 0);
+      if (g0 == 0 && head && lane == 0) vout = zero_below(vout, head);
+      if (last_here && tail && kk == nch - 1) vout = keep_range(vout, 0, 0, tail);
+      const uint32_t any8 = (vout.x | vout.y | vout.z | vout.w) & 0x80808080u;
+      if (__any(any8 != 0) || hi_c0(prev_w)) {  // some byte >= 0x80 (or a sequence open before)
+        uint32_t pw = __shfl_up(vout.w, 1);
+        if (lane == 0) pw = prev_w;
+        if (kk < nch) bad |= utf8_chunk_bad(vout, pw, kk == nch - 1);
+      }
+      prev_w = __builtin_amdgcn_readlane(vout.w, 63);
+    }
+    if (last_here && tail) last = readlane4(val, int(nch - 1 - g0));
   }
   if (lane == c) {
     k.cur = dend;
@@ -194,6 +222,15 @@ __device__ __forceinline__ bool copy_segment(Stream& st, const lds_u8* ring, uin
   }
   return utf8 ? __any(bad) : false;
 }
+
+// Column facts, lane-distributed (lane c: column c), read with v_readlane in the sample loop.
+struct ColRegs {
+  uint64_t data;
+  uint64_t capacity;
+  uint32_t row_bytes;
+  int32_t var_index;
+  uint32_t utf8;  // a str column with UTF-8 flags
+};
 
 template <int S, bool kNT>
 __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) {
@@ -235,28 +272,36 @@ __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) 
   const bool range_ok = lane >= n || (v.hdr_end <= ob && ob < oe && oe <= v.d.bytes);
   const bool fast = __all(range_ok);
 
-  // column cursors at the run's first output byte
+  // column facts and cursors (at the run's first output byte), lane-distributed
+  ColRegs cr = {0, 0, 0, -1, 0};
   Cursors k;
   k.carry = make_uint4(0, 0, 0, 0);
   k.cur = 0;
   if (lane < ncols) {
     const MDSX_L DevCol& col = cols[lane];
-    const uint64_t data = reinterpret_cast<uint64_t>(col.data);
-    k.cur = col.var_index < 0
-                ? data + row0 * col.row_bytes
-                : data + uint64_t(a.tile_prefix[uint64_t(col.var_index) * a.nscan + tile]);
+    cr.data = reinterpret_cast<uint64_t>(col.data);
+    cr.capacity = col.capacity;
+    cr.row_bytes = col.row_bytes;
+    cr.var_index = col.var_index;
+    cr.utf8 = col.kind == MDSX_KIND_STR && col.flags != nullptr;
+    k.cur = cr.var_index < 0
+                ? cr.data + row0 * cr.row_bytes
+                : cr.data + uint64_t(a.tile_prefix[uint64_t(cr.var_index) * a.nscan + tile]);
   }
   k.cst = k.cur;
 
   Stream st;
   const uint64_t first = reinterpret_cast<uint64_t>(v.shard) + __builtin_amdgcn_readfirstlane(ob);
-  const uint64_t sbase = first & ~uint64_t(15);
+  uint64_t sbase = first & ~uint64_t(15);
   st.base = reinterpret_cast<const uint4*>(sbase);
   st.nq = 0;
   st.nslots = 0;
   st.issued = 0;
   st.ops = 0;
   st.op_at = 0;
+  st.dbg = a.stage_debug;
+  st.wait_cycles = 0;
+  const uint64_t t_start = (st.dbg & 16) ? __builtin_readcyclecounter() : 0;
   if (fast) {
     const uint64_t last =
         reinterpret_cast<uint64_t>(v.shard) + uint32_t(__builtin_amdgcn_readlane(int(ob), n));
@@ -271,20 +316,25 @@ __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) 
     const uint64_t srow = reinterpret_cast<uint64_t>(v.shard) + b;  // the sample's first byte
     const uint32_t size = e - b;
     int rc = MDSX_OK;
-    if (!fast) {
+    if (!fast) {  // the sample on its own: its own stream, once the previous one has landed
       if (!(v.hdr_end <= b && b <= e && e <= v.d.bytes)) rc = MDSX_E_BOUNDS;
       else if (b == e) rc = MDSX_E_EMPTY;
+      if (rc == MDSX_OK) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        sbase = srow & ~uint64_t(15);
+        st.base = reinterpret_cast<const uint4*>(sbase);
+        st.nq = uint32_t((srow + size - sbase + 15) >> 4);
+        st.nslots = (st.nq + 63) >> 6;
+        st.issued = 0;
+        pump<S, kNT>(st, ring_lds, 0, lane);
+      }
     }
-    const uint32_t sp = uint32_t(srow - sbase);  // stream position (fast path)
+    const uint32_t sp = uint32_t(srow - sbase);  // stream position of the sample
     // size heads: lane vi holds head vi
     uint32_t h = 0;
     if (rc == MDSX_OK && 4u * uint32_t(nvar) <= size && nvar > 0) {
-      if (fast) {
-        ensure<S, kNT>(st, ring_lds, sp, sp + 4u * uint32_t(nvar) + 3u, lane);
-        if (lane < nvar) h = ring_u32<S>(ring, sp + 4u * uint32_t(lane));
-      } else if (lane < nvar) {
-        h = load_u32_any(reinterpret_cast<const uint8_t*>(srow) + 4u * uint32_t(lane));
-      }
+      ensure<S, kNT>(st, ring_lds, sp, sp + 4u * uint32_t(nvar) + 3u, lane);
+      if (lane < nvar) h = ring_u32<S>(ring, sp + 4u * uint32_t(lane));
     }
     if (rc == MDSX_OK) {
       if (4u * uint32_t(nvar) > size) {
@@ -292,8 +342,9 @@ __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) 
       } else {
         uint64_t need = 4ull * uint32_t(nvar);
         for (int c = 0; c < ncols; ++c) {
-          const int vi = cols[c].var_index;
-          need += vi >= 0 ? uint32_t(__builtin_amdgcn_readlane(int(h), vi)) : cols[c].row_bytes;
+          const int vi = __builtin_amdgcn_readlane(cr.var_index, c);
+          need += vi >= 0 ? uint32_t(__builtin_amdgcn_readlane(int(h), vi))
+                          : uint32_t(__builtin_amdgcn_readlane(int(cr.row_bytes), c));
         }
         if (need > size) rc = MDSX_E_BOUNDS;
       }
@@ -301,34 +352,39 @@ __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) 
     if (rc != MDSX_OK && lane == 0) report(a.status, rc, v.shard_idx, int(v.r0 + j), -1);
     uint32_t rel = 4u * uint32_t(nvar);
     for (int c = 0; c < ncols; ++c) {
-      const MDSX_L DevCol& col = cols[c];
-      const int vi = col.var_index;
+      const int vi = __builtin_amdgcn_readlane(cr.var_index, c);
+      const uint32_t rb = uint32_t(__builtin_amdgcn_readlane(int(cr.row_bytes), c));
+      const uint64_t data = readlane64(cr.data, c);
       const uint32_t len = rc != MDSX_OK ? 0u
                            : vi >= 0     ? uint32_t(__builtin_amdgcn_readlane(int(h), vi))
-                                         : col.row_bytes;
-      const bool utf8 = col.kind == MDSX_KIND_STR && col.flags != nullptr;
+                                         : rb;
+      const bool utf8 = __builtin_amdgcn_readlane(int(cr.utf8), c) != 0;
       uint64_t d = readlane64(k.cur, c);
-      if (vi < 0) d = reinterpret_cast<uint64_t>(col.data) + (row0 + j) * col.row_bytes;
-      if (vi >= 0 && lane == 0) obuf[vi * TR + j] = int64_t(d - reinterpret_cast<uint64_t>(col.data));
+      if (vi < 0) d = data + (row0 + j) * rb;
+      if (vi >= 0 && lane == 0) obuf[vi * TR + j] = int64_t(d - data);
       bool bad = false;
-      if (len && vi >= 0 && d - reinterpret_cast<uint64_t>(col.data) + len > col.capacity) {
+      if (len && vi >= 0 && d - data + len > readlane64(cr.capacity, c)) {
         if (lane == 0) report(a.status, MDSX_E_CAPACITY, v.shard_idx, int(v.r0 + j), c);
-      } else if (len && fast) {
-        bad = copy_segment<S, kNT>(st, ring, ring_lds, k, c, d, len, sp + rel, utf8, lane);
+      } else if (len && (st.dbg & 4)) {
+        if (lane == c) k.cur = d + len;
       } else if (len) {
-        const uint8_t* src = reinterpret_cast<const uint8_t*>(srow) + rel;
-        uint8_t* dst = reinterpret_cast<uint8_t*>(d);
-        bad = utf8 ? wave_copy<true, 2, kNT>(src, dst, len, lane)
-                   : wave_copy<false, 2, kNT>(src, dst, len, lane);
-        if (lane == c) k.cur = d + len, k.cst = d + len;
+        bad = copy_segment<S, kNT>(st, ring, ring_lds, k, c, d, len, sp + rel, utf8, lane);
       }
       if (utf8 && lane == 0) fbuf[vi * TR + j] = bad ? 1 : 0;
       rel += len;
     }
   }
+  if (st.dbg & 16) {  // measurement only: cycles waiting for the ring, and in all
+    if (lane == 0) {
+      unsigned long long* acc = reinterpret_cast<unsigned long long*>(
+          reinterpret_cast<uint8_t*>(a.status) + kStageTimeOffset);
+      atomicAdd(acc, st.wait_cycles);
+      atomicAdd(acc + 1, __builtin_readcyclecounter() - t_start);
+      atomicAdd(acc + 2, 1ull);
+    }
+  }
   // the partly filled last chunk of every column; the run's offsets and flags
-  if (fast)
-    for (int c = 0; c < ncols; ++c) flush(k, c, lane);
+  for (int c = 0; c < ncols; ++c) flush(k, c, lane);
   for (int c = 0; c < ncols; ++c) {
     const MDSX_L DevCol& col = cols[c];
     const int vi = col.var_index;
@@ -342,6 +398,12 @@ __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) 
 }  // namespace
 
 int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
+  if (a.stage_debug & 16) {  // measurement only: the cycle sums
+    const int rc = hip_check(hipMemsetAsync(reinterpret_cast<uint8_t*>(a.status) + kStageTimeOffset,
+                                            0, kStatusBlock - kStageTimeOffset, s),
+                             "hipMemsetAsync");
+    if (rc != MDSX_OK) return rc;
+  }
   const unsigned grid = (a.ntiles + kRunWaves - 1) / kRunWaves;
   const size_t lds = size_t(kRunWaves) * run_wave_lds(a.run_slots, a.tile_rows, a.nvar);
   if (a.tile_rows > kRunMaxRows)
