@@ -28,8 +28,9 @@ import csv, glob, sys, collections
 agg = collections.defaultdict(list)
 for f in glob.glob(sys.argv[1] + '/**/*counter_collection.csv', recursive=True):
     for r in csv.DictReader(open(f)):
-        k = r['Kernel_Name'].split('(')[0]
-        if any(x in k for x in ('decode_kernel', 'scan_tiles', 'copy_probe', 'gather_ragged')):
+        k = r['Kernel_Name'].replace('(anonymous namespace)::', '').split('(')[0]
+        if any(x in k for x in ('decode_kernel', 'scan_tiles', 'stage_totals', 'copy_probe',
+                                'gather_ragged')):
             agg[(k[-48:], r['Counter_Name'])].append(float(r['Counter_Value']))
 for (k, c), v in sorted(agg.items()):
     print(sys.argv[2], '%-48s %-26s n=%d %.4g' % (k, c, len(v), sum(v) / len(v)))

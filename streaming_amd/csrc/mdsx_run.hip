@@ -182,39 +182,49 @@ __device__ __forceinline__ bool copy_segment(Stream& st, const lds_u8* ring, uin
   bool bad = false;
   uint32_t prev_w = 0;
   uint4 last = make_uint4(0, 0, 0, 0);
-  for (uint32_t g0 = 0; g0 < nch; g0 += 64) {
-    ensure<S, kNT>(st, ring_lds, g0 ? s0 + 16u * g0 : sp, s0 + 16u * g0 + 64u * 16u + 15u, lane);
-    const uint32_t kk = g0 + uint32_t(lane);
-    const uint32_t q = q0 + kk;
-    uint4 val = ring_chunk<S>(ring, q);
-    if (sh) val = funnel16(val, ring_chunk<S>(ring, q + 1), sh);
-    if (g0 == 0 && head) {  // the bytes carried from the column's previous value
+  constexpr uint32_t U = S >= 8 ? 4 : 2;  // chunks per lane per step (a step spans <= S slots)
+  for (uint32_t g = 0; g < nch; g += 64 * U) {
+    ensure<S, kNT>(st, ring_lds, g ? s0 + 16u * g : sp, s0 + 16u * g + 64u * 16u * U + 15u, lane);
+    uint4 val[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t q = q0 + g + 64 * u + uint32_t(lane);
+      val[u] = ring_chunk<S>(ring, q);
+      if (sh) val[u] = funnel16(val[u], ring_chunk<S>(ring, q + 1), sh);
+    }
+    if (g == 0 && head) {  // the bytes carried from the column's previous value
       const uint4 carry = readlane4(k.carry, c);
-      if (lane == 0) val = merge_bytes(val, carry, 0, head);
+      if (lane == 0) val[0] = merge_bytes(val[0], carry, 0, head);
     }
-    // whole chunks are stored whole, except the stretch's shared first chunk (its own bytes only)
-    const uint32_t f1 = min(nfull, g0 + 64);
-    const bool kc_here = kc >= g0 && kc < f1;
-    if (!(st.dbg & 1)) {
-      if (kk < nfull && kk != kc) st16<kNT>(dbeg + 16ull * kk, val);
-      if (f1 > g0 + (kc_here ? 1u : 0u)) ++st.ops;  // a store certain to have issued
-    }
-    if (kc_here) wave_edge_store(val, int(kc - g0), cchunk, cst, cchunk + 16, lane);
-    const bool last_here = nch - 1 < g0 + 64;
-    if (utf8 && !(st.dbg & 2)) {
-      // this value's bytes only: the carried ones and those past its end zeroed
-      uint4 vout = kk < nch ? val : make_uint4(0, 0, 0, 0);
-      if (g0 == 0 && head && lane == 0) vout = zero_below(vout, head);
-      if (last_here && tail && kk == nch - 1) vout = keep_range(vout, 0, 0, tail);
-      const uint32_t any8 = (vout.x | vout.y | vout.z | vout.w) & 0x80808080u;
-      if (__any(any8 != 0) || hi_c0(prev_w)) {  // some byte >= 0x80 (or a sequence open before)
-        uint32_t pw = __shfl_up(vout.w, 1);
-        if (lane == 0) pw = prev_w;
-        if (kk < nch) bad |= utf8_chunk_bad(vout, pw, kk == nch - 1);
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t g0 = g + 64 * u;
+      if (g0 >= nch) break;  // uniform
+      const uint32_t kk = g0 + uint32_t(lane);
+      // whole chunks are stored whole, except the stretch's shared first chunk (its own bytes)
+      const uint32_t f1 = min(nfull, g0 + 64);
+      const bool kc_here = kc >= g0 && kc < f1;
+      if (!(st.dbg & 1)) {
+        if (kk < nfull && kk != kc) st16<kNT>(dbeg + 16ull * kk, val[u]);
+        if (f1 > g0 + (kc_here ? 1u : 0u)) ++st.ops;  // a store certain to have issued
       }
-      prev_w = __builtin_amdgcn_readlane(vout.w, 63);
+      if (kc_here) wave_edge_store(val[u], int(kc - g0), cchunk, cst, cchunk + 16, lane);
+      const bool last_here = nch - 1 < g0 + 64;
+      if (utf8 && !(st.dbg & 2)) {
+        // this value's bytes only: the carried ones and those past its end zeroed
+        uint4 vout = kk < nch ? val[u] : make_uint4(0, 0, 0, 0);
+        if (g0 == 0 && head && lane == 0) vout = zero_below(vout, head);
+        if (last_here && tail && kk == nch - 1) vout = keep_range(vout, 0, 0, tail);
+        const uint32_t any8 = (vout.x | vout.y | vout.z | vout.w) & 0x80808080u;
+        if (__any(any8 != 0) || hi_c0(prev_w)) {  // a byte >= 0x80 (or a sequence open before)
+          uint32_t pw = __shfl_up(vout.w, 1);
+          if (lane == 0) pw = prev_w;
+          if (kk < nch) bad |= utf8_chunk_bad(vout, pw, kk == nch - 1);
+        }
+        prev_w = __builtin_amdgcn_readlane(vout.w, 63);
+      }
+      if (last_here && tail) last = readlane4(val[u], int(nch - 1 - g0));
     }
-    if (last_here && tail) last = readlane4(val, int(nch - 1 - g0));
   }
   if (lane == c) {
     k.cur = dend;
@@ -292,7 +302,9 @@ __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) 
 
   Stream st;
   const uint64_t first = reinterpret_cast<uint64_t>(v.shard) + __builtin_amdgcn_readfirstlane(ob);
-  uint64_t sbase = first & ~uint64_t(15);
+  // streams start on a 128-byte line: every 1 KiB slot load is 8 whole lines (a slot straddling
+  // lines makes the next slot fetch the shared line again, measured +7% reads)
+  uint64_t sbase = first & ~uint64_t(127);
   st.base = reinterpret_cast<const uint4*>(sbase);
   st.nq = 0;
   st.nslots = 0;
@@ -321,7 +333,7 @@ __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) 
       else if (b == e) rc = MDSX_E_EMPTY;
       if (rc == MDSX_OK) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        sbase = srow & ~uint64_t(15);
+        sbase = srow & ~uint64_t(127);
         st.base = reinterpret_cast<const uint4*>(sbase);
         st.nq = uint32_t((srow + size - sbase + 15) >> 4);
         st.nslots = (st.nq + 63) >> 6;
