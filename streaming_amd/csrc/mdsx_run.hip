@@ -182,16 +182,20 @@ __device__ __forceinline__ bool copy_segment(Stream& st, const lds_u8* ring, uin
   bool bad = false;
   uint32_t prev_w = 0;
   uint4 last = make_uint4(0, 0, 0, 0);
-  constexpr uint32_t U = S >= 8 ? 4 : 2;  // chunks per lane per step (a step spans <= S slots)
+  constexpr uint32_t U = 2;  // chunks per lane per step (a step spans <= 4 <= S slots)
   for (uint32_t g = 0; g < nch; g += 64 * U) {
     ensure<S, kNT>(st, ring_lds, g ? s0 + 16u * g : sp, s0 + 16u * g + 64u * 16u * U + 15u, lane);
-    uint4 val[U];
+    // all 2U ring reads issued back to back, then realigned (funnel16 with shift 0 is the
+    // identity)
+    uint4 lo[U], hi[U], val[U];
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) {
       const uint32_t q = q0 + g + 64 * u + uint32_t(lane);
-      val[u] = ring_chunk<S>(ring, q);
-      if (sh) val[u] = funnel16(val[u], ring_chunk<S>(ring, q + 1), sh);
+      lo[u] = ring_chunk<S>(ring, q);
+      hi[u] = ring_chunk<S>(ring, q + 1);
     }
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) val[u] = funnel16(lo[u], hi[u], sh);
     if (g == 0 && head) {  // the bytes carried from the column's previous value
       const uint4 carry = readlane4(k.carry, c);
       if (lane == 0) val[0] = merge_bytes(val[0], carry, 0, head);
