@@ -249,6 +249,14 @@ def check_fork() -> None:
             "num_workers=4, multiprocessing_context='spawn').")
 
 
+def require_gpu() -> None:
+    """Fail loudly where a decode would need the GPU and there is none: the package has no CPU
+    fallback (its only CPU decoder is the test oracle, which it never calls)."""
+    if not torch.cuda.is_available():
+        raise RuntimeError('streaming_amd decodes MDS shards on the GPU (HIP, gfx950), and no GPU '
+                           'is visible to this process.')
+
+
 def last_kernel() -> str:
     """Template name of the decode kernel this thread launched last (rocprofv3's name)."""
     name = lib().mdsx_last_kernel()

@@ -72,6 +72,13 @@ class DecodedShardCache:
             self.put(key, value, nbytes)
             return value
 
+    def __getstate__(self) -> dict:
+        # a copy in another process (a spawned DataLoader worker) starts empty, with the same bound
+        return {'limit_bytes': self.limit_bytes}
+
+    def __setstate__(self, state: dict) -> None:
+        self.__init__(state['limit_bytes'])
+
     def put(self, key: int, value: Any, nbytes: int) -> None:
         with self._lock:
             self.discard(key)

@@ -22,6 +22,7 @@ from streaming_amd.array import Array
 from streaming_amd.cache import DecodedShardCache
 from streaming_amd.decoder import DecodedBatch, decode_batch, stage_shards
 from streaming_amd.distributed import owned_shards
+from streaming_amd.order import DeviceSampleGather
 from streaming_amd.reader import MDSReader, get_plan, load_index, reader_from_json
 from streaming_amd.spanner import Spanner
 
@@ -61,7 +62,6 @@ class LocalDataset(Array, Dataset):
         ]
         self.num_samples = sum(shard.samples for shard in self.shards)
         self.spanner = Spanner(np.array([s.samples for s in self.shards], np.int64))
-        self._all: Optional[DecodedBatch] = None
 
     def __len__(self) -> int:
         return self.num_samples
@@ -78,12 +78,15 @@ class LocalDataset(Array, Dataset):
                      batch_size: int) -> Iterator[DecodedBatch]:
         """Device batches of ``batch_size`` samples in the order of ``sample_ids`` (global ids,
         ``-1`` padding skipped as the reference's ``_each_sample_id`` does,
-        ``dataset.py:1430-1473``): every shard decoded once, each batch gathered on device."""
-        if self._all is None:
-            self._all = self.decode_all()
-        ids = torch.as_tensor(np.asarray(sample_ids, np.int64)).reshape(-1)
-        for lo in range(0, ids.numel(), batch_size):
-            yield self._all.gather(ids[lo:lo + batch_size])
+        ``dataset.py:1430-1473``; e.g. one worker's slice of ``generate_work``'s ids,
+        :func:`streaming_amd.order.worker_sample_ids`): the shards a batch touches are decoded on
+        demand through the bounded decoded-shard cache and each batch is gathered on the device
+        (:class:`streaming_amd.order.DeviceSampleGather`)."""
+        return self.sample_gather.iter_batches(sample_ids, batch_size)
+
+    @property
+    def sample_gather(self) -> DeviceSampleGather:
+        return DeviceSampleGather(self.shards)
 
     def decode_all(self, shard_ids: Optional[Sequence[int]] = None,
                    check: bool = True) -> DecodedBatch:

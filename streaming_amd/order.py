@@ -1,0 +1,135 @@
+"""Device batches in the reference's sample order.
+
+``StreamingDataset.__iter__`` (``streaming/base/dataset.py:1475-1513``) takes this worker's slice
+of the epoch's sample-id array that ``generate_work`` lays out (``batching/__init__.py:28-45``:
+``[nodes, ranks per node, workers per rank, batches, batch]``, ``-1`` padding;
+``dataset.py:1054-1056`` flattens the worker's slice), walks it skipping ``-1``
+(``_each_sample_id``, ``dataset.py:1430-1473``) and fetches each id with ``get_item``
+(``dataset.py:1237-1293``: ``spanner`` -> ``shard[idx]``). The DataLoader then collates runs of
+``batch_size`` samples.
+
+:class:`DeviceSampleGather` is the device side of that loop: the same ids, in the same order, as
+device batches. For each batch the touched shards are decoded on demand through the readers'
+bounded decoded-shard cache (:mod:`streaming_amd.cache`; a shard decoded once stays resident while
+the cache holds it), each shard's rows are gathered on the device (``mdsx_gather_*``), and the
+per-shard parts are put back in batch order by one more device gather. Resumption is the
+reference's: ``state_dict`` / ``load_state_dict`` move ``sample_in_epoch``, and ``generate_work``
+then hands out the rest of the epoch (``dataset.py:778-856``); this module takes those ids as they
+come.
+
+Errors follow ``get_item``: a missing shard file raises ``FileNotFoundError`` (the caller
+re-prepares it, ``dataset.py:1274-1291``); a malformed sample raises for that sample only
+(``IndexError`` for an empty one, ``ValueError`` for a range error); ``str`` values that are not
+well-formed UTF-8 come back flagged in the column's ``flags`` (where ``bytes.decode('utf-8')``
+raises, ``encodings.py:80-81``).
+"""
+
+from __future__ import annotations
+
+import os
+from typing import Iterator, Sequence, Union
+
+import numpy as np
+import torch
+
+from streaming_amd.decoder import DecodedBatch, RaggedColumn
+from streaming_amd.reader import MDSReader
+
+__all__ = ['worker_sample_ids', 'concat_batches', 'DeviceSampleGather']
+
+
+def worker_sample_ids(epoch_sample_ids: np.ndarray, node: int, rank_of_node: int,
+                      worker_of_rank: int) -> np.ndarray:
+    """One worker's portion of ``generate_work``'s array, flattened (``dataset.py:1054-1056``);
+    the ``-1`` padding is kept (the iteration skips it)."""
+    return np.asarray(epoch_sample_ids, np.int64)[node, rank_of_node, worker_of_rank].reshape(-1)
+
+
+def concat_batches(parts: Sequence[DecodedBatch]) -> DecodedBatch:
+    """Rows of ``parts`` one after the other (device tensors; ragged offsets rebased on the
+    device, no host sync)."""
+    if not parts:
+        raise ValueError('concat_batches: no parts')
+    if len(parts) == 1:
+        return parts[0]
+    cols: dict[str, Union[torch.Tensor, RaggedColumn]] = {}
+    for name, first in parts[0].columns.items():
+        xs = [p.columns[name] for p in parts]
+        if isinstance(first, RaggedColumn):
+            ends = torch.stack([x.offsets[-1] for x in xs])
+            bases = torch.cumsum(ends, 0) - ends
+            offs = [xs[0].offsets] + [x.offsets[1:] + b for x, b in zip(xs[1:], bases[1:])]
+            vals = torch.cat([x.values for x in xs])  # gathered values: exactly offsets[-1]
+            flags = torch.cat([x.flags for x in xs]) if first.flags is not None else None
+            cols[name] = RaggedColumn(vals, torch.cat(offs), flags)
+        else:
+            cols[name] = torch.cat(xs)
+    return DecodedBatch(cols, sum(p.rows for p in parts))
+
+
+class DeviceSampleGather:
+    """Device batches of global sample ids over a list of shards (``MDSReader``\\ s, in the
+    dataset's shard order: global id -> (shard, local id) as ``Spanner``, ``spanner.py:40-59``).
+
+    Args:
+        shards: the dataset's readers (``LocalDataset.shards``, or the readers a device
+            ``Stream`` returns).
+    """
+
+    def __init__(self, shards: Sequence[MDSReader]) -> None:
+        self.shards = list(shards)
+        counts = np.array([s.samples for s in self.shards], np.int64)
+        self.starts = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+        self.num_samples = int(self.starts[-1])
+
+    def locate(self, ids: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+        """(shard, local id) of each global id."""
+        ids = np.asarray(ids, np.int64)
+        bad = (ids < 0) | (ids >= self.num_samples)
+        if bad.any():
+            raise IndexError(f'Index {int(ids[bad][0])} out of range for dataset of '
+                             f'{self.num_samples} samples')
+        shard = np.searchsorted(self.starts, ids, side='right') - 1
+        return shard, ids - self.starts[shard]
+
+    def _shard_rows(self, s: int, local: np.ndarray) -> DecodedBatch:
+        reader = self.shards[s]
+        os.stat(reader._filename())  # FileNotFoundError once evicted (the reference's open())
+        entry = reader._decode_entry()
+        if entry.status.code != 0:  # raise only for the bad samples this batch reads
+            for idx in np.unique(local):
+                reader._check_row(entry, int(idx))
+        return entry.decoded.gather(torch.from_numpy(np.ascontiguousarray(local)))
+
+    def gather(self, sample_ids: Union[Sequence[int], np.ndarray, torch.Tensor]) -> DecodedBatch:
+        """The samples ``sample_ids`` (global ids; ``-1`` skipped), in that order."""
+        ids = np.asarray(torch.as_tensor(sample_ids).cpu().numpy() if isinstance(
+            sample_ids, torch.Tensor) else sample_ids, np.int64).reshape(-1)
+        ids = ids[ids != -1]
+        if ids.size == 0:
+            raise ValueError('gather: no samples')
+        shard, local = self.locate(ids)
+        order = np.argsort(shard, kind='stable')
+        sorted_shards = shard[order]
+        cuts = np.flatnonzero(np.diff(sorted_shards)) + 1
+        parts = []
+        for grp in np.split(order, cuts):
+            parts.append(self._shard_rows(int(shard[grp[0]]), local[grp]))
+        out = concat_batches(parts)
+        if np.array_equal(order, np.arange(ids.size)):
+            return out
+        inv = np.empty_like(order)
+        inv[order] = np.arange(ids.size)  # batch position i is row inv[i] of the shard-major rows
+        return out.gather(torch.from_numpy(inv))
+
+    def iter_batches(self, sample_ids: Union[Sequence[int], np.ndarray, torch.Tensor],
+                     batch_size: int) -> Iterator[DecodedBatch]:
+        """Device batches of ``batch_size`` samples over ``sample_ids`` (one worker's ids,
+        flattened, ``-1`` skipped; the last batch may be short), in the reference's order."""
+        if batch_size <= 0:
+            raise ValueError('batch_size must be positive')
+        ids = np.asarray(torch.as_tensor(sample_ids).cpu().numpy() if isinstance(
+            sample_ids, torch.Tensor) else sample_ids, np.int64).reshape(-1)
+        ids = ids[ids != -1]
+        for lo in range(0, ids.size, batch_size):
+            yield self.gather(ids[lo:lo + batch_size])

@@ -268,6 +268,19 @@ class MDSReader(JointReader):
         self._cache = cache
         self._key = next(_reader_keys)
 
+    def __getstate__(self) -> dict[str, Any]:
+        # pickled into spawned DataLoader workers: no lock, and the decoded shards stay behind
+        # (a given cache travels as an empty cache with the same bound, shared by the readers
+        # pickled with it)
+        state = self.__dict__.copy()
+        del state['_lock']
+        return state
+
+    def __setstate__(self, state: dict[str, Any]) -> None:
+        self.__dict__.update(state)
+        self._lock = threading.Lock()
+        self._key = next(_reader_keys)
+
     @classmethod
     def from_json(cls, dirname: str, split: Optional[str], obj: dict[str, Any],
                   device: Union[str, torch.device, None] = None,
@@ -318,6 +331,7 @@ class MDSReader(JointReader):
 
         def create() -> tuple[_Decoded, int]:
             _native.check_fork()
+            _native.require_gpu()
             data = self.read_shard_bytes()
             plan = self.plan
             batch = stage_shards([data], [self.samples], plan, device=self.device)

@@ -1,0 +1,32 @@
+"""The plugin against the REAL reference (build container only; skipped where /root/reference is
+absent, e.g. on the GPU box): StreamingDataset(stream_name='mdsx') built by the reference's own
+registry-based construction (dataset.py:447-468) holds device readers for every shard, its
+control plane (generate_work) lays out the recorded reference order over them, and reading a sample
+goes to the device reader (no silent CPU fallback: without a GPU it raises)."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REF = os.environ.get('MDSX_REFERENCE', '/root/reference')
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+pytestmark = pytest.mark.skipif(not os.path.isdir(os.path.join(REF, 'streaming')),
+                                reason='the reference source tree is not present')
+
+
+def test_streaming_dataset_with_device_stream(tmp_path):
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE='1', HIP_VISIBLE_DEVICES='')
+    res = subprocess.run([sys.executable, os.path.join(HERE, 'integration', 'plugin_ref_check.py'),
+                          REF, str(tmp_path)], capture_output=True, text=True, timeout=300,
+                         env=env)
+    assert res.returncode == 0, res.stderr[-3000:]
+    out = json.loads(res.stdout.strip().splitlines()[-1])
+    assert out['stream_class'] == 'DeviceStream'
+    assert out['all_device_readers']
+    assert out['shards'] == 64 and out['num_samples'] == 10_000
+    assert out['ids_match_fixture']
+    assert out['get_item'].startswith('RuntimeError') and 'GPU' in out['get_item']
