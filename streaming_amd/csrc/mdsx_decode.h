@@ -130,6 +130,19 @@ __device__ __forceinline__ int64_t block_exclusive_scan(int64_t x, int64_t* s_ws
 // Byte offset, inside the workspace's 256-byte status block, of the staged decode's count of
 // huge rows (listed in the src_abs region; mdsx_stage.hip).
 constexpr uint64_t kHugeCountOffset = 192;
+// Bit (-code) set for every kind of error a decode kernel reported (the status record keeps only
+// the first): the gather pass runs when every error is a per-sample one (empty sample, range),
+// which leaves its row zero-length and every offset consistent.
+constexpr uint64_t kErrKindsOffset = 64;
+constexpr uint32_t kRowLevelErrors = (1u << -MDSX_E_BOUNDS) | (1u << -MDSX_E_EMPTY);
+
+__device__ __forceinline__ void report_decode(const DevArgs& a, int code, int shard, int row,
+                                              int col) {
+  report(a.status, code, shard, row, col);
+  atomicOr(reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(a.status) + kErrKindsOffset),
+           1u << ((-code) & 31));
+}
+
 // measurement only (stage_debug & 16): 7 u64 cycle sums of the staged decode's phases
 constexpr uint64_t kStageTimeOffset = 200;
 constexpr uint64_t kStatusBlock = 256;

@@ -337,7 +337,7 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
   const TileView v = tile_view(a, tile);
 
   if (!v.table_ok) {
-    if (t == 0 && tile == v.d.tile0) report(a.status, MDSX_E_HEADER, v.shard_idx, -1, -1);
+    if (t == 0 && tile == v.d.tile0) report_decode(a, MDSX_E_HEADER, v.shard_idx, -1, -1);
     if constexpr (!kSingle) return;  // block-uniform (kSingle: the tile still publishes zeros)
   }
   if (t == 0 && tile == v.d.tile0 && v.table_ok) {
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
     const uint32_t n = *reinterpret_cast<const uint32_t*>(v.shard);
     const uint32_t first = v.offs[0];
     if (n != v.d.samples || first < v.hdr_end || v.offs[v.d.samples] > v.d.bytes)
-      report(a.status, MDSX_E_HEADER, v.shard_idx, -1, -1);
+      report_decode(a, MDSX_E_HEADER, v.shard_idx, -1, -1);
   }
   const int nrows = v.table_ok ? int(v.nrows) : 0;
 
@@ -381,7 +381,7 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
     }
     if (!ok) {
       for (int vi = 0; vi < a.nvar; ++vi) s_vlen[vi * TR + t] = 0;
-      if (rc != MDSX_OK) report(a.status, rc, v.shard_idx, int(i), -1);
+      if (rc != MDSX_OK) report_decode(a, rc, v.shard_idx, int(i), -1);
     }
     s_ok[t] = ok ? 1 : 0;
   }
@@ -435,7 +435,7 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
           uint64_t x = (!done && !wait && ((span >> kk) & 1)) ? (w & kLbValue) : 0;
           for (int o = W >> 1; o > 0; o >>= 1) x += __shfl_xor(x, o);
           if (!done && !wait) {
-            if ((none & span) != 0 && kk == 0) report(a.status, MDSX_E_HIP, v.shard_idx, -1, -1);
+            if ((none & span) != 0 && kk == 0) report_decode(a, MDSX_E_HIP, v.shard_idx, -1, -1);
             base += x;
             if (incl) done = true;
             else j -= W;
@@ -480,7 +480,7 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
       if (!ok) continue;
       const uint64_t len = s_vlen[vi * TR + t];
       if (uint64_t(off) + len > col.capacity) {
-        report(a.status, MDSX_E_CAPACITY, v.shard_idx, int(i), c);
+        report_decode(a, MDSX_E_CAPACITY, v.shard_idx, int(i), c);
         ok = false;
         continue;
       }
@@ -779,7 +779,10 @@ __global__ __launch_bounds__(kBlock) void gather_ragged_kernel(const DevArgs a) 
   while (a.cols[ci].var_index != vi) ++ci;
   const DevCol& col = a.cols[ci];
   const int64_t tot = col.offsets[a.rows];
-  if (a.status->code != 0) return;  // decode failed
+  // a decode error other than per-sample ones (empty sample, range) leaves offsets unreliable
+  const uint32_t kinds =
+      *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(a.status) + kErrKindsOffset);
+  if (kinds & ~kRowLevelErrors) return;
   const uint32_t* map = a.row_map + uint64_t(vi) * a.map_len;
   const uint64_t* src = a.src_abs + uint64_t(vi) * a.rows;
   const uint64_t stride = a.gather_block0[vi + 1] - a.gather_block0[vi];
@@ -1208,7 +1211,7 @@ int mdsx_scan_shards(const mdsx_plan* plan, const mdsx_batch* batch, const mdsx_
   int rc = build_args(plan, batch, outs, d_workspace, workspace_bytes, d_totals, &a);
   if (rc != MDSX_OK) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  rc = hip_check(hipMemsetAsync(d_workspace, 0, sizeof(mdsx_status), s), "hipMemsetAsync");
+  rc = hip_check(hipMemsetAsync(d_workspace, 0, kStatusBlock, s), "hipMemsetAsync");
   if (rc != MDSX_OK || plan->nvar == 0) return rc;
   if (a.ntiles > 0 && (a.stage_bytes || a.run_slots)) {
     rc = launch_stage_totals(a, s);

@@ -273,7 +273,7 @@ __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) 
     // header written by encode_joint_shard (mds/writer.py:133-144): u32 N, then N + 1 offsets
     if (!v.table_ok || *reinterpret_cast<const uint32_t*>(v.shard) != v.d.samples ||
         v.offs[0] < v.hdr_end || v.offs[v.d.samples] > v.d.bytes)
-      report(a.status, MDSX_E_HEADER, v.shard_idx, -1, -1);
+      report_decode(a, MDSX_E_HEADER, v.shard_idx, -1, -1);
   }
   if (!v.table_ok) return;
   const int n = int(v.nrows);
@@ -365,7 +365,7 @@ __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) 
         if (need > size) rc = MDSX_E_BOUNDS;
       }
     }
-    if (rc != MDSX_OK && lane == 0) report(a.status, rc, v.shard_idx, int(v.r0 + j), -1);
+    if (rc != MDSX_OK && lane == 0) report_decode(a, rc, v.shard_idx, int(v.r0 + j), -1);
     uint32_t rel = 4u * uint32_t(nvar);
     for (int c = 0; c < ncols; ++c) {
       const int vi = __builtin_amdgcn_readlane(cr.var_index, c);
@@ -380,7 +380,7 @@ __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) 
       if (vi >= 0 && lane == 0) obuf[vi * TR + j] = int64_t(d - data);
       bool bad = false;
       if (len && vi >= 0 && d - data + len > readlane64(cr.capacity, c)) {
-        if (lane == 0) report(a.status, MDSX_E_CAPACITY, v.shard_idx, int(v.r0 + j), c);
+        if (lane == 0) report_decode(a, MDSX_E_CAPACITY, v.shard_idx, int(v.r0 + j), c);
       } else if (len && (st.dbg & 4)) {
         if (lane == c) k.cur = d + len;
       } else if (len) {

@@ -293,7 +293,7 @@ __device__ __forceinline__ void write_columns(const DevArgs& a, const MDSX_L Dev
     uint64_t d0, d1;
     column_range(col, td, R, TR, ga, gb, &d0, &d1);
     if (vi >= 0 && d1 > col.capacity) {  // block-uniform
-      if (ct == 0) report(a.status, MDSX_E_CAPACITY, td.shard, int(td.r0 + ga), c);
+      if (ct == 0) report_decode(a, MDSX_E_CAPACITY, td.shard, int(td.r0 + ga), c);
       continue;
     }
     if (d1 <= d0) continue;
@@ -408,7 +408,7 @@ __device__ __forceinline__ void fail_row(const DevArgs& a, const TileDesc& td, c
                                          int TR, int t, int rc) {
   R.ok[t] = 0;
   for (int vi = 0; vi < a.nvar; ++vi) R.len[vi * TR + t] = 0;
-  report(a.status, rc, td.shard, int(td.r0 + t), -1);
+  report_decode(a, rc, td.shard, int(td.r0 + t), -1);
 }
 
 }  // namespace
@@ -499,7 +499,7 @@ __global__ __launch_bounds__(kBlock) void stage_huge_kernel(const DevArgs a) {
       if (col.var_index >= 0) {
         d = uint64_t(col.offsets[row]);  // final (written by the staged kernel)
         if (d + len > col.capacity) {
-          if (threadIdx.x == 0) report(a.status, MDSX_E_CAPACITY, v.shard_idx, int(v.r0 + t), c);
+          if (threadIdx.x == 0) report_decode(a, MDSX_E_CAPACITY, v.shard_idx, int(v.r0 + t), c);
           continue;
         }
       }
@@ -578,7 +578,7 @@ __global__ __launch_bounds__(kStageBlock) void stage_decode_kernel(const DevArgs
       const uint32_t* offs = reinterpret_cast<const uint32_t*>(shard + 4);
       if (!td.table_ok || *reinterpret_cast<const uint32_t*>(shard) != d.samples ||
           offs[0] < 4ull + 4ull * (uint64_t(d.samples) + 1ull) || offs[d.samples] > d.bytes)
-        report(a.status, MDSX_E_HEADER, int(si), -1, -1);
+        report_decode(a, MDSX_E_HEADER, int(si), -1, -1);
     }
   }
   __syncthreads();
