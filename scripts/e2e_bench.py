@@ -23,13 +23,15 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from streaming_amd.compression import compress  # noqa: E402
+from streaming_amd.hashing import get_hash  # noqa: E402
 from streaming_amd.decoder import BatchDecoder, Plan, make_batch, output_bytes  # noqa: E402
-from streaming_amd.pipeline import ShardFile, ShardPipeline, _fill, to_host  # noqa: E402
+from streaming_amd.pipeline import (PIPELINE_DEVICE_HASHES, ShardFile, ShardPipeline,  # noqa: E402
+                                    _fill, to_host)
 from streaming_amd.synth import var_c_shards  # noqa: E402
 from streaming_amd.writer import encode_fixed_shard, shard_config_bytes  # noqa: E402
 
 
-def make_files(cfg, samples, out, workers):
+def make_files(cfg, samples, out, workers, hashes=()):
     rng = np.random.default_rng(5)
     files = []
     if cfg in ('B', 'E'):
@@ -59,11 +61,32 @@ def make_files(cfg, samples, out, workers):
         blob = compress('zstd', raw) if comp else raw
         with open(path, 'wb') as f:
             f.write(blob)
-        return ShardFile(path, len(raw), n, comp), len(blob)
+        digests = {algo: get_hash(algo, raw) for algo in hashes}  # index.json raw_data.hashes
+        return ShardFile(path, len(raw), n, comp, digests), len(blob)
 
     with ThreadPoolExecutor(workers) as ex:
         res = list(ex.map(write, enumerate(shards)))
     return Plan(names, encs, sizes), [r[0] for r in res], sum(r[1] for r in res)
+
+
+def _validate_runs(args, plan, files, raw_bytes, rows, algos, res):
+    """The pipelined end-to-end run (device hand-off) with each shard's hash checked."""
+    for algo in [None] + algos:
+        pipe = ShardPipeline(plan, files, shards_per_batch=args.per_batch, depth=2,
+                             workers=args.workers, validate_hash=algo)
+        for _ in pipe:  # warm-up pass
+            pass
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        n = sum(b.rows for b in pipe)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        pipe.close()
+        assert n == rows
+        where = 'device' if algo in PIPELINE_DEVICE_HASHES else 'host threads'
+        res[f'e2e_validate_{algo or "none"}'] = {
+            'samples_per_s': rows / dt, 'raw_GiBps': raw_bytes / dt / 2**30, 'seconds': dt,
+            'hash_on': None if algo is None else where}
 
 
 def main():
@@ -73,18 +96,28 @@ def main():
     ap.add_argument('--workers', type=int, default=16)
     ap.add_argument('--per-batch', type=int, default=8)
     ap.add_argument('--dir', default=None)
+    ap.add_argument('--validate', default='',
+                    help='comma-separated hash algorithms: also time the pipeline validating each '
+                         '(ShardPipeline validate_hash; xxh3 on the device, the rest on the host '
+                         'threads)')
+    ap.add_argument('--skip-stages', action='store_true', help='only the pipelined runs')
     args = ap.parse_args()
+    algos = [a for a in args.validate.split(',') if a]
     torch.cuda.set_device(0)
     tmp = tempfile.mkdtemp(prefix='mdsx_e2e_', dir=args.dir)
     try:
         t0 = time.perf_counter()
-        plan, files, file_bytes = make_files(args.config, args.samples, tmp, args.workers)
+        plan, files, file_bytes = make_files(args.config, args.samples, tmp, args.workers, algos)
         gen_s = time.perf_counter() - t0
         raw_bytes = sum(f.raw_bytes for f in files)
         rows = sum(f.samples for f in files)
         res = {'config': args.config, 'samples': rows, 'shards': len(files),
                'raw_bytes': raw_bytes, 'file_bytes': file_bytes, 'workers': args.workers,
                'host_cpus': len(os.sched_getaffinity(0)), 'generate_s': gen_s}
+        if args.skip_stages:
+            _validate_runs(args, plan, files, raw_bytes, rows, algos, res)
+            print(json.dumps(res, indent=1))
+            return
         # 1. stage everything into one pinned buffer (page cache -> pinned), threads
         batch = make_batch(plan, [f.raw_bytes for f in files], [f.samples for f in files])
         pinned = torch.empty(batch.buffer.numel(), dtype=torch.uint8, pin_memory=True)
@@ -147,6 +180,7 @@ def main():
             key = 'e2e_with_d2h' if d2h else 'e2e_device_handoff'
             res[key] = {'samples_per_s': rows / dt, 'raw_GiBps': raw_bytes / dt / 2**30,
                         'seconds': dt}
+        _validate_runs(args, plan, files, raw_bytes, rows, algos, res)
         print(json.dumps(res, indent=1))
     finally:
         shutil.rmtree(tmp, ignore_errors=True)

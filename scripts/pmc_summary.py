@@ -1,15 +1,18 @@
 """Summarise rocprofv3 runs of bench.py into per-(workload, kernel) traffic entries.
 
 Usage: python scripts/pmc_summary.py <dir>   (the layout scripts/profile_bench.sh writes:
-<dir>/trace (kernel-trace --stats), <dir>/fetch (--pmc FETCH_SIZE), <dir>/write (--pmc WRITE_SIZE),
-and the bench JSON line in <dir>/trace.log).
+<dir>/trace (kernel-trace --stats), <dir>/read (--pmc TCC_EA0_RDREQ by request size),
+<dir>/write (--pmc TCC_EA0_WRREQ, _64B), and the bench JSON line in <dir>/trace.log).
 
 For every config of the bench line (headline + ``config_c``) the entry holds the workload key
 and the exact decode-kernel template name the bench reported, that kernel's rocprofv3 stats and
-its per-launch HBM traffic: FETCH_SIZE / WRITE_SIZE are KiB per dispatch; per
-MI355X_MICROARCH.md §HBM, FETCH_SIZE on gfx950 reads exactly half the bytes of a wide (16 B/lane)
-coalesced streaming read, so the read side is doubled; WRITE_SIZE is exact for 16 B/lane
-streaming stores. bench.py uses an entry only when both the workload key and the kernel match.
+its per-launch HBM traffic from the request counters by size: read bytes = 32 x RDREQ_32B +
+64 x RDREQ_64B + 128 x RDREQ_128B, write bytes = 64 x WRREQ_64B + 32 x (WRREQ - WRREQ_64B).
+Calibrated on the copy probe (profiles/r02/counters_calibration.txt): a copy of N bytes counts
+exactly N / 128 128-byte reads and N / 64 64-byte writes (FETCH_SIZE, which tallies a 128-byte
+request at 64 bytes, reads half of that on gfx950, MI355X_MICROARCH.md §HBM, and mis-weighs
+narrower requests). bench.py uses an entry only when the workload key, the kernel and the library
+build match.
 """
 import csv
 import glob
@@ -28,7 +31,7 @@ def rows(out, pattern):
 
 def bench_lines(out):
     lines = []
-    for log in ('trace.log', 'fetch.log', 'write.log'):
+    for log in ('trace.log', 'read.log', 'write.log'):
         p = os.path.join(out, log)
         if not os.path.exists(p):
             continue
@@ -48,9 +51,15 @@ def configs(line):
 def counter(out, sub, name, kernel):
     vals = []
     for r in rows(out, f'{sub}/**/*counter_collection.csv'):
-        if kernel in r.get('Kernel_Name', '') and r.get('Counter_Name') == name:
+        if kernel in r.get('Kernel_Name', '').replace('(anonymous namespace)::', '') and \
+                r.get('Counter_Name') == name:
             vals.append(float(r['Counter_Value']))
     return vals
+
+
+def mean(out, sub, name, kernel):
+    vals = counter(out, sub, name, kernel)
+    return sum(vals) / len(vals) if vals else None
 
 
 def main(out):
@@ -69,17 +78,23 @@ def main(out):
             'algorithmic_bytes_per_launch': cfg['roofline']['algorithmic_bytes_per_launch'],
             'kernel_stats': [r for r in stats if kernel in r['Name']],
         }
-        fetch = counter(out, 'fetch', 'FETCH_SIZE', kernel)
-        write = counter(out, 'write', 'WRITE_SIZE', kernel)
-        if fetch and write:
-            f = sum(fetch) / len(fetch) * 1024
-            w = sum(write) / len(write) * 1024
+        # memory-side requests by size (TCC_EA0_*: the L2's requests to HBM / fabric), exact
+        # bytes: a copy of N bytes counts N / 128 128-byte reads and N / 64 64-byte writes
+        n32, n64, n128, nrd = (mean(out, 'read', f'TCC_EA0_RDREQ{s}_sum', kernel)
+                               for s in ('_32B', '_64B', '_128B', ''))
+        nwr, nw64 = (mean(out, 'write', f'TCC_EA0_WRREQ{s}_sum', kernel) for s in ('', '_64B'))
+        if None not in (n32, n64, n128, nwr, nw64):
+            rd = 32 * n32 + 64 * n64 + 128 * n128
+            wr = 64 * nw64 + 32 * (nwr - nw64)
             e.update({
-                'fetch_size_bytes_per_launch_raw': f,
-                'write_size_bytes_per_launch': w,
-                'hbm_traffic_bytes_per_launch': 2 * f + w,
-                'traffic_over_algorithmic': (2 * f + w) / e['algorithmic_bytes_per_launch'],
-                'launches_counted': [len(fetch), len(write)],
+                'read_requests': {'32B': n32, '64B': n64, '128B': n128, 'all': nrd},
+                'write_requests': {'64B': nw64, 'all': nwr},
+                'read_bytes_per_launch': rd,
+                'write_bytes_per_launch': wr,
+                'hbm_traffic_bytes_per_launch': rd + wr,
+                'traffic_over_algorithmic': (rd + wr) / e['algorithmic_bytes_per_launch'],
+                'read_over_R': rd / cfg['roofline']['algorithmic']['R'],
+                'write_over_W': wr / cfg['roofline']['algorithmic']['W'],
             })
         entries.append(e)
     # every kernel of the trace, for context (scan passes, gather, copy probe)
