@@ -50,35 +50,42 @@ constexpr int kRunBlock = 256;  // 4 waves, one tile each
 constexpr int kRunWaves = kRunBlock / 64;
 constexpr int kRunMaxRows = 32;  // rows of a tile: one offsets-table entry per lane (+1)
 
+// A wave's LDS: its ring (S KiB, stream byte p at p % S KiB), a 64-byte mirror of the ring's
+// first bytes behind it (so a read that wraps is one contiguous read), offsets and flags of its run.
+constexpr uint32_t kMirror = 64;
 __host__ __device__ __forceinline__ uint32_t run_wave_lds(int S, int TR, int nvar) {
-  return (uint32_t(S) * 1024u + uint32_t(nvar) * uint32_t(TR) * 9u + 15u) & ~15u;
+  return (uint32_t(S) * 1024u + kMirror + uint32_t(nvar) * uint32_t(TR) * 5u + 15u) & ~15u;
 }
 
-// Stream chunk q (16 bytes) of the ring: slot (q / 64) % S, position q % 64.
+// 16 stream bytes at stream byte p: one ds_read_b128 at any byte address (gfx950 reads LDS
+// unaligned; the 16-byte realignment costs no instructions).
 template <int S>
-__device__ __forceinline__ uint4 ring_chunk(const lds_u8* ring, uint32_t q) {
-  const u32x4 v = *(const MDSX_L u32x4*)(ring + ((((q >> 6) & (S - 1)) << 10) | ((q & 63u) << 4)));
+__device__ __forceinline__ uint4 ring16(const lds_u8* ring, uint32_t p) {
+  const u32x4 v = *(const MDSX_L u32x4*)(ring + (p & (S * 1024u - 1u)));
   return make_uint4(v.x, v.y, v.z, v.w);
-}
-
-// 16 stream bytes at stream byte p (any alignment; bytes before the stream start read as zero).
-template <int S>
-__device__ __forceinline__ uint4 ring16(const lds_u8* ring, int64_t p) {
-  const int64_t q = p >> 4;  // floor
-  const uint4 lo = q >= 0 ? ring_chunk<S>(ring, uint32_t(q)) : make_uint4(0, 0, 0, 0);
-  return funnel16_lane(lo, ring_chunk<S>(ring, uint32_t(q + 1)), uint32_t(p) & 15u);
 }
 
 // u32 at stream byte p (any alignment).
 template <int S>
 __device__ __forceinline__ uint32_t ring_u32(const lds_u8* ring, uint32_t p) {
-  auto dw = [&](uint32_t w) {  // stream dword w
-    const uint32_t q = w >> 2;
-    return *(const MDSX_L uint32_t*)(ring + ((((q >> 6) & (S - 1)) << 10) | ((q & 63u) << 4) |
-                                             ((w & 3u) << 2)));
-  };
-  const uint32_t w = p >> 2;
-  return alignbyte(dw(w + 1), dw(w), p & 3u);
+  return *(const MDSX_L uint32_t*)(ring + (p & (S * 1024u - 1u)));
+}
+
+// s_waitcnt vmcnt(m), m the largest of 0, 1, 2, 4, 8, 16, 32 not above n (three compares).
+__device__ __forceinline__ void wait_vm_coarse(uint32_t n) {
+  if (n >= 16) {
+    if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else if (n >= 4) {
+    if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else if (n >= 2) {
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  } else if (n == 1) {
+    asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
 }
 
 // The wave's stream: chunks [0, nq) from base, in slots of 64 chunks.
@@ -88,9 +95,7 @@ struct Stream {
   uint32_t issued;  // slots issued
   uint32_t ops;     // vector-memory operations issued by this wave (loads; stores certain to issue)
   uint32_t op_at;   // lane r: `ops` when the slot now in ring position r was issued
-  uint32_t dbg;     // measurement only (MDSX_TUNE sdbg): 1 no stores, 2 no UTF-8, 4 no copies,
-                    // 8 no ring waits, 16 cycle sums
-  uint64_t wait_cycles;
+  uint32_t mirrored;  // the last slot at ring position 0 copied to the mirror
 };
 
 // Issue slots while they fit in the ring above slot `low`: the stream bytes still to be read
@@ -106,17 +111,21 @@ __device__ __forceinline__ void pump(Stream& st, uint32_t ring_lds, uint32_t low
   }
 }
 
-// pump, then wait until stream bytes [lo, hi] (hi - lo < (S - 1) KiB) have landed.
+// pump, then wait until stream bytes [lo, hi] (hi - lo < (S - 1) KiB) have landed; a slot at ring
+// position 0 that has landed is mirrored behind the ring for the reads that wrap.
 template <int S, bool kNT>
-__device__ __forceinline__ void ensure(Stream& st, uint32_t ring_lds, uint32_t lo, uint32_t hi,
-                                       int lane) {
+__device__ __forceinline__ void ensure(Stream& st, const lds_u8* ring, uint32_t ring_lds,
+                                       uint32_t lo, uint32_t hi, int lane) {
   pump<S, kNT>(st, ring_lds, lo >> 10, lane);
   const uint32_t upto = min(hi >> 10, st.nslots - 1);
-  if (st.dbg & 8) return;
-  const uint64_t t0 = (st.dbg & 16) ? __builtin_readcyclecounter() : 0;
-  wait_vm_at_most(st.ops - uint32_t(__builtin_amdgcn_readlane(int(st.op_at), int(upto & (S - 1)))) -
-                  1u);
-  if (st.dbg & 16) st.wait_cycles += __builtin_readcyclecounter() - t0;
+  wait_vm_coarse(st.ops - uint32_t(__builtin_amdgcn_readlane(int(st.op_at), int(upto & (S - 1)))) -
+                 1u);
+  const uint32_t j0 = upto & ~uint32_t(S - 1);
+  if (j0 != st.mirrored) {
+    st.mirrored = j0;
+    if (lane < int(kMirror / 4))
+      *(MDSX_L uint32_t*)(ring + S * 1024 + 4 * lane) = *(const MDSX_L uint32_t*)(ring + 4 * lane);
+  }
 }
 
 __device__ __forceinline__ uint4 readlane4(const uint4 v, int l) {
@@ -129,22 +138,34 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
          (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v >> 32)), l))) << 32);
 }
 
-// The per-column state of a wave, lane-distributed (lane c: column c).
+// The per-column state of a wave, lane-distributed (lane c: column c). Output positions are
+// 32-bit and relative to the column's `base` (the run's first output byte of the column,
+// rounded down to 16): a run lies inside one shard, so its outputs span < 4 GiB.
 struct Cursors {
-  uint64_t cur;  // next output byte address of the column
-  uint64_t cst;  // first output byte of the column's current contiguous stretch (bytes below it
+  uint32_t cur;  // next output byte of the column
+  uint32_t cst;  // first output byte of the column's current contiguous stretch (bytes below it
                  // belong to another run)
   uint4 carry;   // the partly filled chunk at cur & ~15 (bytes below cur valid from cst on)
 };
 
+// Column facts, lane-distributed, read with v_readlane in the sample loop.
+struct ColRegs {
+  uint64_t base;   // the run's first output byte of the column, rounded down to 16
+  uint32_t first;  // that byte, relative to base (0..15)
+  uint32_t rb;     // fixed columns: bytes per row
+  uint32_t meta;   // bits 0-7: ragged index + 1 (0: fixed); bit 8: str with UTF-8 flags;
+                   // bit 9: skip (the run's bytes exceed the output capacity)
+};
+
 // Write out the partly filled chunk of column c (the bytes [max(cst, chunk), cur)).
-__device__ __forceinline__ void flush(const Cursors& k, int c, int lane) {
-  const uint64_t cur = readlane64(k.cur, c), cst = readlane64(k.cst, c);
+__device__ __forceinline__ void flush(const Cursors& k, uint64_t base, int c, int lane) {
+  const uint32_t cur = __builtin_amdgcn_readlane(k.cur, c);
+  const uint32_t cst = __builtin_amdgcn_readlane(k.cst, c);
   if ((cur & 15) == 0) return;
-  const uint64_t C = cur & ~uint64_t(15);
-  const uint64_t lo = max(cst, C);
+  const uint32_t C = cur & ~15u;
+  const uint32_t lo = max(cst, C);
   if (lo >= cur) return;
-  wave_edge_store(k.carry, c, C, lo, cur, lane);
+  wave_edge_store(k.carry, c, base + C, base + lo, base + cur, lane);
 }
 
 // Bytes [0, n) of `v` zeroed (n uniform, 0 <= n <= 16).
@@ -153,49 +174,42 @@ __device__ __forceinline__ uint4 zero_below(const uint4 v, uint32_t n) {
   return make_uint4(v.x & ~m.x, v.y & ~m.y, v.z & ~m.z, v.w & ~m.w);
 }
 
-// Column c of one sample: output bytes [d, d + len) from stream bytes [sp, sp + len).
-// Returns (utf8: a str column) whether the value is not well-formed UTF-8 (wave-uniform).
-// Everything but the per-lane chunk is wave-uniform: the source shift of a value is one shift
-// for all its chunks (funnel16, four v_alignbyte), the carried bytes and the value's last
-// partial chunk are handled under uniform branches.
+// Column c of one sample: output bytes [d, d + len) (relative to `base`) from stream bytes
+// [sp, sp + len). Returns (utf8: a str column) whether the value is not well-formed UTF-8
+// (wave-uniform). Everything but the per-lane chunk is wave-uniform: each chunk is one unaligned
+// ring read, the carried bytes and the value's last partial chunk are handled under uniform
+// branches.
 template <int S, bool kNT>
 __device__ __forceinline__ bool copy_segment(Stream& st, const lds_u8* ring, uint32_t ring_lds,
-                                             Cursors& k, int c, uint64_t d, uint32_t len,
-                                             uint32_t sp, bool utf8, int lane) {
-  if (readlane64(k.cur, c) != d) {  // a gap (a skipped sample's fixed bytes): a new stretch
-    flush(k, c, lane);
+                                             Cursors& k, uint64_t base, int c, uint32_t d,
+                                             uint32_t len, uint32_t sp, bool utf8, int lane) {
+  if (uint32_t(__builtin_amdgcn_readlane(k.cur, c)) != d) {  // a gap (a skipped sample's fixed
+    flush(k, base, c, lane);                                  // bytes): a new stretch
     if (lane == c) k.cst = d;
   }
-  const uint64_t cst = readlane64(k.cst, c);
-  const uint64_t dbeg = d & ~uint64_t(15), dend = d + len;
-  const uint32_t head = uint32_t(d - dbeg);                 // carried bytes in the first chunk
-  const uint32_t tail = uint32_t(dend & 15);                // bytes of the last chunk, if partial
-  const uint32_t nch = uint32_t((dend + 15 - dbeg) >> 4);   // chunks touched
-  const uint32_t nfull = uint32_t((dend - dbeg) >> 4);      // chunks completed by this value
+  const uint32_t cst = __builtin_amdgcn_readlane(k.cst, c);
+  const uint32_t dbeg = d & ~15u, dend = d + len;
+  const uint32_t head = d & 15u;               // carried bytes in the first chunk
+  const uint32_t tail = dend & 15u;            // bytes of the last chunk, if partial
+  const uint32_t nch = (dend + 15 - dbeg) >> 4;  // chunks touched
+  const uint32_t nfull = (dend - dbeg) >> 4;     // chunks completed by this value
   // the stretch's first chunk, when another run owns its leading bytes: index inside this value
-  const uint64_t cchunk = cst & ~uint64_t(15);
-  const uint32_t kc =
-      (cst & 15) && cchunk >= dbeg ? uint32_t((cchunk - dbeg) >> 4) : 0xffffffffu;
-  // chunk kk of the value holds stream bytes from sp - head + 16 kk: stream chunk q0 + kk, shift sh
-  const uint32_t s0 = sp - head;  // wraps below 0 only on the first value of the stream
-  const uint32_t q0 = uint32_t(int32_t(s0) >> 4), sh = s0 & 15u;
+  const uint32_t cchunk = cst & ~15u;
+  const uint32_t kc = (cst & 15) && cchunk >= dbeg ? (cchunk - dbeg) >> 4 : 0xffffffffu;
+  // chunk kk of the value holds stream bytes from s0 + 16 kk (s0 wraps below 0 only on the first
+  // value of the stream: those bytes are the carried ones, replaced below)
+  const uint32_t s0 = sp - head;
+  const uint64_t out = base + dbeg;
   bool bad = false;
   uint32_t prev_w = 0;
   uint4 last = make_uint4(0, 0, 0, 0);
   constexpr uint32_t U = 2;  // chunks per lane per step (a step spans <= 4 <= S slots)
   for (uint32_t g = 0; g < nch; g += 64 * U) {
-    ensure<S, kNT>(st, ring_lds, g ? s0 + 16u * g : sp, s0 + 16u * g + 64u * 16u * U + 15u, lane);
-    // all 2U ring reads issued back to back, then realigned (funnel16 with shift 0 is the
-    // identity)
-    uint4 lo[U], hi[U], val[U];
+    ensure<S, kNT>(st, ring, ring_lds, g ? s0 + 16u * g : sp, s0 + 16u * g + 64u * 16u * U + 15u,
+                   lane);
+    uint4 val[U];
 #pragma unroll
-    for (uint32_t u = 0; u < U; ++u) {
-      const uint32_t q = q0 + g + 64 * u + uint32_t(lane);
-      lo[u] = ring_chunk<S>(ring, q);
-      hi[u] = ring_chunk<S>(ring, q + 1);
-    }
-#pragma unroll
-    for (uint32_t u = 0; u < U; ++u) val[u] = funnel16(lo[u], hi[u], sh);
+    for (uint32_t u = 0; u < U; ++u) val[u] = ring16<S>(ring, s0 + 16u * (g + 64 * u + lane));
     if (g == 0 && head) {  // the bytes carried from the column's previous value
       const uint4 carry = readlane4(k.carry, c);
       if (lane == 0) val[0] = merge_bytes(val[0], carry, 0, head);
@@ -208,13 +222,12 @@ __device__ __forceinline__ bool copy_segment(Stream& st, const lds_u8* ring, uin
       // whole chunks are stored whole, except the stretch's shared first chunk (its own bytes)
       const uint32_t f1 = min(nfull, g0 + 64);
       const bool kc_here = kc >= g0 && kc < f1;
-      if (!(st.dbg & 1)) {
-        if (kk < nfull && kk != kc) st16<kNT>(dbeg + 16ull * kk, val[u]);
-        if (f1 > g0 + (kc_here ? 1u : 0u)) ++st.ops;  // a store certain to have issued
-      }
-      if (kc_here) wave_edge_store(val[u], int(kc - g0), cchunk, cst, cchunk + 16, lane);
+      if (kk < nfull && kk != kc) st16<kNT>(out + 16ull * kk, val[u]);
+      if (f1 > g0 + (kc_here ? 1u : 0u)) ++st.ops;  // a store certain to have issued
+      if (kc_here)
+        wave_edge_store(val[u], int(kc - g0), base + cchunk, base + cst, base + cchunk + 16, lane);
       const bool last_here = nch - 1 < g0 + 64;
-      if (utf8 && !(st.dbg & 2)) {
+      if (utf8) {
         // this value's bytes only: the carried ones and those past its end zeroed
         uint4 vout = kk < nch ? val[u] : make_uint4(0, 0, 0, 0);
         if (g0 == 0 && head && lane == 0) vout = zero_below(vout, head);
@@ -237,15 +250,6 @@ __device__ __forceinline__ bool copy_segment(Stream& st, const lds_u8* ring, uin
   return utf8 ? __any(bad) : false;
 }
 
-// Column facts, lane-distributed (lane c: column c), read with v_readlane in the sample loop.
-struct ColRegs {
-  uint64_t data;
-  uint64_t capacity;
-  uint32_t row_bytes;
-  int32_t var_index;
-  uint32_t utf8;  // a str column with UTF-8 flags
-};
-
 template <int S, bool kNT>
 __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -263,8 +267,8 @@ __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) 
   const int ncols = a.ncols, nvar = a.nvar;
   uint8_t* wl = smem + size_t(wave) * run_wave_lds(S, TR, nvar);
   const lds_u8* ring = (const lds_u8*)wl;
-  MDSX_L int64_t* obuf = (MDSX_L int64_t*)(wl + S * 1024);         // [nvar][TR]
-  MDSX_L uint8_t* fbuf = (MDSX_L uint8_t*)(wl + S * 1024 + nvar * TR * 8);  // [nvar][TR]
+  MDSX_L uint32_t* obuf = (MDSX_L uint32_t*)(wl + S * 1024 + kMirror);  // [nvar][TR]
+  MDSX_L uint8_t* fbuf = (MDSX_L uint8_t*)(wl + S * 1024 + kMirror + nvar * TR * 4);  // [nvar][TR]
   const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(
       static_cast<uint32_t>(reinterpret_cast<uintptr_t>((const MDSX_L uint8_t*)wl)));
 
@@ -286,21 +290,31 @@ __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) 
   const bool range_ok = lane >= n || (v.hdr_end <= ob && ob < oe && oe <= v.d.bytes);
   const bool fast = __all(range_ok);
 
-  // column facts and cursors (at the run's first output byte), lane-distributed
-  ColRegs cr = {0, 0, 0, -1, 0};
+  // column facts and cursors at the run's first output byte, lane-distributed
+  ColRegs cr = {0, 0, 0, 0};
   Cursors k;
   k.carry = make_uint4(0, 0, 0, 0);
   k.cur = 0;
   if (lane < ncols) {
     const MDSX_L DevCol& col = cols[lane];
-    cr.data = reinterpret_cast<uint64_t>(col.data);
-    cr.capacity = col.capacity;
-    cr.row_bytes = col.row_bytes;
-    cr.var_index = col.var_index;
-    cr.utf8 = col.kind == MDSX_KIND_STR && col.flags != nullptr;
-    k.cur = cr.var_index < 0
-                ? cr.data + row0 * cr.row_bytes
-                : cr.data + uint64_t(a.tile_prefix[uint64_t(cr.var_index) * a.nscan + tile]);
+    const uint64_t data = reinterpret_cast<uint64_t>(col.data);
+    const int vi = col.var_index;
+    uint64_t first = data + row0 * col.row_bytes;
+    uint32_t meta = uint32_t(vi + 1) & 255u;
+    if (vi >= 0) {
+      const uint64_t off = uint64_t(a.tile_prefix[uint64_t(vi) * a.nscan + tile]);
+      first = data + off;
+      if (off + uint64_t(a.tile_total[uint64_t(vi) * a.nscan + tile]) > col.capacity) {
+        report_decode(a, MDSX_E_CAPACITY, v.shard_idx, int(v.r0), lane);
+        meta |= 1u << 9;  // this run writes nothing of the column
+      }
+      if (col.kind == MDSX_KIND_STR && col.flags != nullptr) meta |= 1u << 8;
+    }
+    cr.base = first & ~uint64_t(15);
+    cr.first = uint32_t(first & 15);
+    cr.rb = col.row_bytes;
+    cr.meta = meta;
+    k.cur = cr.first;
   }
   k.cst = k.cur;
 
@@ -315,9 +329,7 @@ __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) 
   st.issued = 0;
   st.ops = 0;
   st.op_at = 0;
-  st.dbg = a.stage_debug;
-  st.wait_cycles = 0;
-  const uint64_t t_start = (st.dbg & 16) ? __builtin_readcyclecounter() : 0;
+  st.mirrored = 0xffffffffu;
   if (fast) {
     const uint64_t last =
         reinterpret_cast<uint64_t>(v.shard) + uint32_t(__builtin_amdgcn_readlane(int(ob), n));
@@ -342,6 +354,7 @@ __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) 
         st.nq = uint32_t((srow + size - sbase + 15) >> 4);
         st.nslots = (st.nq + 63) >> 6;
         st.issued = 0;
+        st.mirrored = 0xffffffffu;
         pump<S, kNT>(st, ring_lds, 0, lane);
       }
     }
@@ -349,7 +362,7 @@ __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) 
     // size heads: lane vi holds head vi
     uint32_t h = 0;
     if (rc == MDSX_OK && 4u * uint32_t(nvar) <= size && nvar > 0) {
-      ensure<S, kNT>(st, ring_lds, sp, sp + 4u * uint32_t(nvar) + 3u, lane);
+      ensure<S, kNT>(st, ring, ring_lds, sp, sp + 4u * uint32_t(nvar) + 3u, lane);
       if (lane < nvar) h = ring_u32<S>(ring, sp + 4u * uint32_t(lane));
     }
     if (rc == MDSX_OK) {
@@ -358,9 +371,9 @@ __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) 
       } else {
         uint64_t need = 4ull * uint32_t(nvar);
         for (int c = 0; c < ncols; ++c) {
-          const int vi = __builtin_amdgcn_readlane(cr.var_index, c);
+          const int vi = int(__builtin_amdgcn_readlane(cr.meta, c) & 255u) - 1;
           need += vi >= 0 ? uint32_t(__builtin_amdgcn_readlane(int(h), vi))
-                          : uint32_t(__builtin_amdgcn_readlane(int(cr.row_bytes), c));
+                          : uint32_t(__builtin_amdgcn_readlane(cr.rb, c));
         }
         if (need > size) rc = MDSX_E_BOUNDS;
       }
@@ -368,44 +381,33 @@ __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) 
     if (rc != MDSX_OK && lane == 0) report_decode(a, rc, v.shard_idx, int(v.r0 + j), -1);
     uint32_t rel = 4u * uint32_t(nvar);
     for (int c = 0; c < ncols; ++c) {
-      const int vi = __builtin_amdgcn_readlane(cr.var_index, c);
-      const uint32_t rb = uint32_t(__builtin_amdgcn_readlane(int(cr.row_bytes), c));
-      const uint64_t data = readlane64(cr.data, c);
+      const uint32_t meta = __builtin_amdgcn_readlane(cr.meta, c);
+      const int vi = int(meta & 255u) - 1;
+      const uint32_t rb = __builtin_amdgcn_readlane(cr.rb, c);
       const uint32_t len = rc != MDSX_OK ? 0u
                            : vi >= 0     ? uint32_t(__builtin_amdgcn_readlane(int(h), vi))
                                          : rb;
-      const bool utf8 = __builtin_amdgcn_readlane(int(cr.utf8), c) != 0;
-      uint64_t d = readlane64(k.cur, c);
-      if (vi < 0) d = data + (row0 + j) * rb;
-      if (vi >= 0 && lane == 0) obuf[vi * TR + j] = int64_t(d - data);
+      const bool utf8 = (meta >> 8) & 1u;
+      const uint32_t d = vi < 0 ? __builtin_amdgcn_readlane(cr.first, c) + uint32_t(j) * rb
+                                : __builtin_amdgcn_readlane(k.cur, c);
+      if (vi >= 0 && lane == 0) obuf[vi * TR + j] = d;
       bool bad = false;
-      if (len && vi >= 0 && d - data + len > readlane64(cr.capacity, c)) {
-        if (lane == 0) report_decode(a, MDSX_E_CAPACITY, v.shard_idx, int(v.r0 + j), c);
-      } else if (len && (st.dbg & 4)) {
-        if (lane == c) k.cur = d + len;
-      } else if (len) {
-        bad = copy_segment<S, kNT>(st, ring, ring_lds, k, c, d, len, sp + rel, utf8, lane);
-      }
+      if (len && !((meta >> 9) & 1u))
+        bad = copy_segment<S, kNT>(st, ring, ring_lds, k, readlane64(cr.base, c), c, d, len,
+                                   sp + rel, utf8, lane);
       if (utf8 && lane == 0) fbuf[vi * TR + j] = bad ? 1 : 0;
       rel += len;
     }
   }
-  if (st.dbg & 16) {  // measurement only: cycles waiting for the ring, and in all
-    if (lane == 0) {
-      unsigned long long* acc = reinterpret_cast<unsigned long long*>(
-          reinterpret_cast<uint8_t*>(a.status) + kStageTimeOffset);
-      atomicAdd(acc, st.wait_cycles);
-      atomicAdd(acc + 1, __builtin_readcyclecounter() - t_start);
-      atomicAdd(acc + 2, 1ull);
-    }
-  }
   // the partly filled last chunk of every column; the run's offsets and flags
-  for (int c = 0; c < ncols; ++c) flush(k, c, lane);
+  for (int c = 0; c < ncols; ++c) flush(k, readlane64(cr.base, c), c, lane);
   for (int c = 0; c < ncols; ++c) {
     const MDSX_L DevCol& col = cols[c];
     const int vi = col.var_index;
     if (vi < 0) continue;
-    if (lane < n) *gp(col.offsets + row0 + lane) = obuf[vi * TR + lane];
+    // offsets[row] = (base - data) + the row's position relative to base
+    const int64_t obase = int64_t(readlane64(cr.base, c) - reinterpret_cast<uint64_t>(col.data));
+    if (lane < n) *gp(col.offsets + row0 + lane) = obase + int64_t(obuf[vi * TR + lane]);
     if (col.kind == MDSX_KIND_STR && col.flags && lane < n)
       *gp(col.flags + row0 + lane) = fbuf[vi * TR + lane];
   }
@@ -414,12 +416,6 @@ __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) 
 }  // namespace
 
 int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
-  if (a.stage_debug & 16) {  // measurement only: the cycle sums
-    const int rc = hip_check(hipMemsetAsync(reinterpret_cast<uint8_t*>(a.status) + kStageTimeOffset,
-                                            0, kStatusBlock - kStageTimeOffset, s),
-                             "hipMemsetAsync");
-    if (rc != MDSX_OK) return rc;
-  }
   const unsigned grid = (a.ntiles + kRunWaves - 1) / kRunWaves;
   const size_t lds = size_t(kRunWaves) * run_wave_lds(a.run_slots, a.tile_rows, a.nvar);
   if (a.tile_rows > kRunMaxRows)
