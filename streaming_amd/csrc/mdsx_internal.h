@@ -50,6 +50,7 @@ struct mdsx_plan {
   int stage_fill = 70;  // percent of a stage buffer a tile's samples fill on average (tile sizing)
   int run_slots = 0;    // ragged plans: KiB of the streaming decode's per-wave LDS ring (0: off)
   int run_kb = 64;      // streaming decode: about this many KiB of samples per tile (tile sizing)
+  int64_t run_min = 2048;  // streaming decode for batches whose samples average >= this many bytes
   int gather_chunks = 2;  // 16-byte chunks per lane in the ragged gather (tile = 4 KiB x this)
   int gather_min = 256;   // ragged columns averaging fewer bytes per row use the gather kernel
   int group_max = 1024;   // ... fewer than this (and >= gather_min): four rows per wave
@@ -57,3 +58,11 @@ struct mdsx_plan {
   bool safe = true;
   mdsx::ColumnSpec cols[MDSX_MAX_COLUMNS];
 };
+
+// Whether a batch of `bytes` shard bytes and `rows` samples decodes through the streaming decode
+// (mdsx_run.hip): ragged plans whose samples average at least run_min bytes (config C's 4.4 KB
+// samples: 4.76 vs 4.70 TB/s, 1.02x vs 1.15x traffic; short and medium rows stay on the
+// register decode, measured 2x and 1.3x faster there).
+inline bool use_run_decode(const mdsx_plan* p, uint64_t bytes, uint64_t rows) {
+  return p->nvar > 0 && p->run_slots > 0 && rows > 0 && bytes / rows >= uint64_t(p->run_min);
+}

@@ -869,7 +869,7 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   a->stage_bytes = plan->nvar > 0 ? uint32_t(plan->stage_kb) * 1024u : 0u;
   a->stage_tiles = plan->stage_tiles ? uint32_t(plan->stage_tiles) : stage_tiles_per_wg(b->ntiles);
   a->stage_debug = uint32_t(plan->stage_debug);
-  a->run_slots = plan->nvar > 0 ? uint32_t(plan->run_slots) : 0u;
+  a->run_slots = use_run_decode(plan, b->bytes, b->rows) ? uint32_t(plan->run_slots) : 0u;
   if (a->run_slots) a->stage_bytes = 0;  // the streaming decode takes precedence
   if (a->run_slots && tr > 32)
     return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode tiles hold at most 32 rows");

@@ -211,6 +211,8 @@ void apply_tuning(mdsx_plan* p) {
       p->stage_fill = int(v);
     } else if (key == "run" && (v == 0 || v == 4 || v == 8 || v == 16)) {
       p->run_slots = int(v);
+    } else if (key == "rmin" && v >= 0) {
+      p->run_min = v;
     } else if (key == "rkb" && v >= 1 && v <= 4096) {
       p->run_kb = int(v);
     }
@@ -284,9 +286,10 @@ int mdsx_plan_create(const char* const* encodings, const int64_t* column_sizes, 
   // Tile = rows of one workgroup. All-fixed plans: about 32 KiB of rows per tile (>= 4 rows),
   // so the resident workgroups stream through a narrow window of the shard buffer -- measured
   // on config B (4 KiB rows): 4-8-row tiles 5.87 TB/s, 16: 5.66, 64: 5.52, and the plain copy
-  // probe 5.42 on the same box (scripts/tune_decode.py). Ragged plans: 32-row tiles (config C,
-  // 4 KiB blobs + ~340-byte strings: 4.19 vs 3.99 TB/s at 64 rows; 256-1024-byte blobs +
-  // 64-256-code-point strings: 1.99 vs 1.99; 32-256-byte rows 0.81 vs 0.86). LDS per tile: a u32
+  // probe 5.42 on the same box (scripts/tune_decode.py). Ragged plans on the register decode:
+  // 32-row tiles (256-1024-byte blobs + 64-256-code-point strings: 2.08 vs 1.97 TB/s at 16 rows;
+  // 32-256-byte rows 0.87 vs 0.76; long samples go to the streaming decode, which sizes its own
+  // tiles, mdsx_plan_tile_rows_for). LDS per tile: a u32
   // source offset per (row, column), and per ragged column a u32 length and a u64 destination
   // offset per row (<= 16.4 KiB at 64 columns and 64 rows).
   if (p->nvar == 0) {
@@ -315,6 +318,9 @@ int mdsx_plan_create(const char* const* encodings, const int64_t* column_sizes, 
   // 4.3 TB/s for the register/ring decode, and 0.56-0.71 vs 0.89 TB/s on short rows
   // (scripts/gpu_stage_dbg.sh, profiles/r02/stage_phases.txt).
   p->stage_kb = 0;
+  // Ragged batches of long samples decode through the streaming decode (mdsx_run.hip, 4 KiB ring
+  // per wave): every shard byte read once, whole-chunk stores (use_run_decode).
+  p->run_slots = p->nvar > 0 ? 4 : 0;
   p->stage_fill = 70;
   apply_tuning(p);
   *out = p;
@@ -331,7 +337,7 @@ int mdsx_plan_tile_rows(const mdsx_plan* plan) { return plan ? plan->tile_rows :
 
 int mdsx_plan_tile_rows_for(const mdsx_plan* plan, uint64_t shard_bytes, uint64_t rows) {
   if (!plan) return MDSX_E_ARG;
-  if (plan->nvar > 0 && plan->run_slots > 0 && rows > 0) {
+  if (use_run_decode(plan, shard_bytes, rows)) {
     // streaming decode: about run_kb KiB of samples per tile (one wave's run), 1..32 rows
     const uint64_t per_row = std::max<uint64_t>(1, shard_bytes / rows);
     int tr = 1;

@@ -30,19 +30,19 @@ pytestmark = pytest.mark.gpu
 
 MODES = {
     'default': '',
-    'run': 'run=8',  # the streaming decode (mdsx_run.hip)
-    'run4': 'run=4,rkb=4',  # small ring, 1-2-row tiles
-    'run16': 'run=16,rkb=1024',  # 32-row tiles
-    'stage': 'stage=24',  # the staged decode (opt-in; measured slower)
-    'stage_overflow': 'stage=4,fill=300',  # tiles of ~3x the stage: several row groups each
-    'stage_tiny': 'stage=1',  # rows over 1 KiB go through the huge-row kernel
-    'stage_big': 'stage=64,fill=90',
-    'gather': 'stage=0,gmin=1000000000',
-    'group': 'stage=0,gmin=0,gmax=1000000000',
-    'group_nt': 'stage=0,gmin=0,gmax=1000000000,strc=0',  # str rows streamed (non-temporal) too
-    'wave': 'stage=0,gmin=0,gmax=0,ring=0',
-    'ring': 'stage=0,gmin=0,gmax=0,ring=8',   # one row per wave through the LDS-DMA ring
-    'ring4': 'stage=0,gmin=0,gmax=0,ring=4',
+    'run': 'run=8,rmin=0',  # the streaming decode (mdsx_run.hip) whatever the sample size
+    'run4': 'run=4,rmin=0,rkb=4',  # small ring, 1-2-row tiles
+    'run16': 'run=16,rmin=0,rkb=1024',  # 32-row tiles
+    'stage': 'stage=24,run=0',  # the staged decode (opt-in; measured slower)
+    'stage_overflow': 'stage=4,fill=300,run=0',  # tiles of ~3x the stage: several row groups each
+    'stage_tiny': 'stage=1,run=0',  # rows over 1 KiB go through the huge-row kernel
+    'stage_big': 'stage=64,fill=90,run=0',
+    'gather': 'stage=0,run=0,gmin=1000000000',
+    'group': 'stage=0,run=0,gmin=0,gmax=1000000000',
+    'group_nt': 'stage=0,run=0,gmin=0,gmax=1000000000,strc=0',  # str rows streamed (non-temporal) too
+    'wave': 'stage=0,run=0,gmin=0,gmax=0,ring=0',
+    'ring': 'stage=0,run=0,gmin=0,gmax=0,ring=8',   # one row per wave through the LDS-DMA ring
+    'ring4': 'stage=0,run=0,gmin=0,gmax=0,ring=4',
 }
 
 
