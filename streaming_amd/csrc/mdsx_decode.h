@@ -30,6 +30,21 @@ struct DevCol {
   int8_t group;   // ragged column of medium rows: four rows per wave (group_copy)
 };
 
+// One run (tile) of the streaming decode as the scan pass describes it (stage_totals_kernel), so
+// that a wave starts streaming its run after one load instead of a chain of table loads.
+struct TileRun {
+  uint64_t stream;  // batch byte of the run's first sample (offsets[r0])
+  uint64_t offs;    // batch byte of offsets[r0] (the run's slice of the shard's offsets table)
+  uint64_t row0;    // output row of the run's first sample
+  uint32_t bytes;   // offsets[r0 + nrows] - offsets[r0] (when fast)
+  uint32_t shard;   // batch shard index
+  uint32_t r0;      // first sample of the run inside its shard
+  uint16_t nrows;
+  uint16_t fast;    // the table fits and every sample of the run passes the file checks
+  uint64_t reserved;
+};
+static_assert(sizeof(TileRun) == 48, "TileRun layout");
+
 struct DevArgs {
   const uint8_t* batch;
   const mdsx_shard_desc* shards;
@@ -38,6 +53,7 @@ struct DevArgs {
   int64_t* tile_total;   // [nvar][nscan] ragged bytes of each scan block (scan_per tiles)
   int64_t* tile_prefix;  // [nvar][nscan] their exclusive prefix
   int64_t* chunk_sum;    // [nvar][nchunk] scan of tile_total in chunks of kScanChunk entries
+  TileRun* tile_run;     // [ntiles] (streaming decode)
   int64_t* totals;       // [nvar] or null
   uint64_t* src_abs;     // [nvar][rows]  byte index into the batch of each row's ragged value
   uint32_t* row_map;     // [nvar][map_len] first row of every gather tile

@@ -811,7 +811,7 @@ __global__ __launch_bounds__(kBlock) void gather_ragged_kernel(const DevArgs a) 
 
 // ---------------------------------------------------------------------------------------------
 struct Layout {
-  uint64_t tile_total, tile_prefix, chunk_sum, src_abs, row_map, map_len, total;
+  uint64_t tile_total, tile_prefix, chunk_sum, tile_run, src_abs, row_map, map_len, total;
 };
 
 __host__ uint64_t round256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
@@ -827,7 +827,8 @@ Layout workspace_layout(const mdsx_plan* plan, const mdsx_batch* b) {
   L.tile_total = 256;
   L.tile_prefix = L.tile_total + round256(nv * b->ntiles * 8);
   L.chunk_sum = L.tile_prefix + round256(nv * b->ntiles * 8);
-  L.src_abs = L.chunk_sum + round256(nv * (b->ntiles / kScanChunk + 1) * 8);
+  L.tile_run = L.chunk_sum + round256(nv * (b->ntiles / kScanChunk + 1) * 8);
+  L.src_abs = L.tile_run + round256(nv ? uint64_t(b->ntiles) * sizeof(TileRun) : 0);
   L.row_map = L.src_abs + round256(nv * b->rows * 8);
   L.total = L.row_map + round256(nv * L.map_len * 4);
   return L;
@@ -855,6 +856,7 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   a->tile_total = reinterpret_cast<int64_t*>(ws + L.tile_total);
   a->tile_prefix = reinterpret_cast<int64_t*>(ws + L.tile_prefix);
   a->chunk_sum = reinterpret_cast<int64_t*>(ws + L.chunk_sum);
+  a->tile_run = reinterpret_cast<TileRun*>(ws + L.tile_run);
   a->src_abs = reinterpret_cast<uint64_t*>(ws + L.src_abs);
   a->row_map = reinterpret_cast<uint32_t*>(ws + L.row_map);
   a->lookback = reinterpret_cast<uint64_t*>(ws + L.tile_total);  // single pass: no tile totals

@@ -272,23 +272,43 @@ __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) 
   const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(
       static_cast<uint32_t>(reinterpret_cast<uintptr_t>((const MDSX_L uint8_t*)wl)));
 
-  const TileView v = tile_view(a, tile);
-  if (lane == 0 && tile == v.d.tile0) {
-    // header written by encode_joint_shard (mds/writer.py:133-144): u32 N, then N + 1 offsets
-    if (!v.table_ok || *reinterpret_cast<const uint32_t*>(v.shard) != v.d.samples ||
-        v.offs[0] < v.hdr_end || v.offs[v.d.samples] > v.d.bytes)
-      report_decode(a, MDSX_E_HEADER, v.shard_idx, -1, -1);
+  // the run as the scan pass described it (its header check too): one load, then the run's
+  // first S KiB in flight at once, its offsets-table slice and output bases loaded meanwhile
+  const TileRun r = a.tile_run[tile];
+  const bool fast = r.fast != 0;
+  const uint64_t batch = reinterpret_cast<uint64_t>(a.batch);
+  const uint64_t shard = batch + (r.offs - 4ull - 4ull * r.r0);  // the shard file's first byte
+  Stream st;
+  // streams start on a 128-byte line: every 1 KiB slot load is 8 whole lines (a slot straddling
+  // lines makes the next slot fetch the shared line again, measured +7% reads)
+  uint64_t sbase = (batch + r.stream) & ~uint64_t(127);
+  st.base = reinterpret_cast<const uint4*>(sbase);
+  st.nq = 0;
+  st.nslots = 0;
+  st.issued = 0;
+  st.ops = 0;
+  st.op_at = 0;
+  st.mirrored = 0xffffffffu;
+  if (fast) {
+    st.nq = uint32_t((batch + r.stream + r.bytes - sbase + 15) >> 4);
+    st.nslots = (st.nq + 63) >> 6;
+    pump<S, kNT>(st, ring_lds, 0, lane);
   }
-  if (!v.table_ok) return;
-  const int n = int(v.nrows);
+  // a run with a sample failing the file checks (or a table past its file): each sample checked
+  // against its shard, and streamed on its own
+  uint64_t hdr_end = 0, fbytes = 0;
+  if (!fast) {
+    const TileView v = tile_view(a, tile);
+    if (!v.table_ok) return;
+    hdr_end = v.hdr_end;
+    fbytes = v.d.bytes;
+  }
+  const int n = int(r.nrows);
   if (n == 0) return;
-  const uint64_t row0 = v.d.row0 + v.r0;
-
+  const uint64_t row0 = r.row0;
   // this run's offsets-table slice: lane j holds offsets[r0 + j] (j <= n)
-  const uint32_t ob = lane <= n ? v.offs[v.r0 + lane] : 0u;
-  const uint32_t oe = __shfl_down(ob, 1);
-  const bool range_ok = lane >= n || (v.hdr_end <= ob && ob < oe && oe <= v.d.bytes);
-  const bool fast = __all(range_ok);
+  const uint32_t ob = lane <= n ? *reinterpret_cast<const uint32_t*>(a.batch + r.offs + 4u * lane)
+                                : 0u;
 
   // column facts and cursors at the run's first output byte, lane-distributed
   ColRegs cr = {0, 0, 0, 0};
@@ -305,7 +325,7 @@ __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) 
       const uint64_t off = uint64_t(a.tile_prefix[uint64_t(vi) * a.nscan + tile]);
       first = data + off;
       if (off + uint64_t(a.tile_total[uint64_t(vi) * a.nscan + tile]) > col.capacity) {
-        report_decode(a, MDSX_E_CAPACITY, v.shard_idx, int(v.r0), lane);
+        report_decode(a, MDSX_E_CAPACITY, int(r.shard), int(r.r0), lane);
         meta |= 1u << 9;  // this run writes nothing of the column
       }
       if (col.kind == MDSX_KIND_STR && col.flags != nullptr) meta |= 1u << 8;
@@ -318,34 +338,15 @@ __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) 
   }
   k.cst = k.cur;
 
-  Stream st;
-  const uint64_t first = reinterpret_cast<uint64_t>(v.shard) + __builtin_amdgcn_readfirstlane(ob);
-  // streams start on a 128-byte line: every 1 KiB slot load is 8 whole lines (a slot straddling
-  // lines makes the next slot fetch the shared line again, measured +7% reads)
-  uint64_t sbase = first & ~uint64_t(127);
-  st.base = reinterpret_cast<const uint4*>(sbase);
-  st.nq = 0;
-  st.nslots = 0;
-  st.issued = 0;
-  st.ops = 0;
-  st.op_at = 0;
-  st.mirrored = 0xffffffffu;
-  if (fast) {
-    const uint64_t last =
-        reinterpret_cast<uint64_t>(v.shard) + uint32_t(__builtin_amdgcn_readlane(int(ob), n));
-    st.nq = uint32_t((last - sbase + 15) >> 4);
-    st.nslots = (st.nq + 63) >> 6;
-    pump<S, kNT>(st, ring_lds, 0, lane);  // the first S KiB in flight
-  }
 
   for (int j = 0; j < n; ++j) {  // wave-uniform
     const uint32_t b = uint32_t(__builtin_amdgcn_readlane(int(ob), j));
     const uint32_t e = uint32_t(__builtin_amdgcn_readlane(int(ob), j + 1));
-    const uint64_t srow = reinterpret_cast<uint64_t>(v.shard) + b;  // the sample's first byte
+    const uint64_t srow = shard + b;  // the sample's first byte
     const uint32_t size = e - b;
     int rc = MDSX_OK;
     if (!fast) {  // the sample on its own: its own stream, once the previous one has landed
-      if (!(v.hdr_end <= b && b <= e && e <= v.d.bytes)) rc = MDSX_E_BOUNDS;
+      if (!(hdr_end <= b && b <= e && e <= fbytes)) rc = MDSX_E_BOUNDS;
       else if (b == e) rc = MDSX_E_EMPTY;
       if (rc == MDSX_OK) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -378,7 +379,7 @@ __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) 
         if (need > size) rc = MDSX_E_BOUNDS;
       }
     }
-    if (rc != MDSX_OK && lane == 0) report_decode(a, rc, v.shard_idx, int(v.r0 + j), -1);
+    if (rc != MDSX_OK && lane == 0) report_decode(a, rc, int(r.shard), int(r.r0 + j), -1);
     uint32_t rel = 4u * uint32_t(nvar);
     for (int c = 0; c < ncols; ++c) {
       const uint32_t meta = __builtin_amdgcn_readlane(cr.meta, c);

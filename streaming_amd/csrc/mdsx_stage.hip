@@ -426,8 +426,11 @@ __global__ __launch_bounds__(kBlock) void stage_totals_kernel(const DevArgs a) {
   if (tile_ok) v = tile_view(a, tile);
   const bool in_tile = tile_ok && v.table_ok && (t % TR) < int(v.nrows);
   uint32_t b = 0, e = 0;
-  bool ok = false;
-  if (in_tile) ok = sample_range(v, v.r0 + t % TR, &b, &e) == MDSX_OK && 4ull * a.nvar <= e - b;
+  bool ok = false, range_bad = false;
+  if (in_tile) {
+    range_bad = sample_range(v, v.r0 + t % TR, &b, &e) != MDSX_OK;
+    ok = !range_bad && 4ull * a.nvar <= e - b;
+  }
   const bool few = a.nvar <= kHeadRegs;
   Heads h;
   if (ok && few) h.load(v.shard + b, a.nvar);
@@ -460,6 +463,29 @@ __global__ __launch_bounds__(kBlock) void stage_totals_kernel(const DevArgs a) {
         for (int w = wave; w < wave + TR / 64; ++w) sum += s_part[w][vi];
         a.tile_total[uint64_t(vi) * a.nscan + tile] = sum;
       }
+    }
+  }
+  if (a.run_slots && TR < 64) {  // the streaming decode's run records (its tiles: <= 32 rows)
+    const uint64_t bad = __ballot(range_bad);
+    const uint64_t seg = ((1ull << TR) - 1) << (lane & ~(TR - 1));  // this tile's lanes
+    if (tile_ok && t % TR == 0) {
+      TileRun r;
+      const bool fast = v.table_ok && v.nrows > 0 && (bad & seg) == 0;
+      r.fast = fast ? 1 : 0;
+      r.stream = v.d.offset + (fast ? v.offs[v.r0] : 0u);
+      r.bytes = fast ? v.offs[v.r0 + v.nrows] - v.offs[v.r0] : 0u;
+      r.offs = v.d.offset + 4ull + 4ull * v.r0;
+      r.row0 = v.d.row0 + v.r0;
+      r.shard = v.shard_idx;
+      r.r0 = v.r0;
+      r.nrows = uint16_t(v.nrows);
+      r.reserved = 0;
+      a.tile_run[tile] = r;
+      // header written by encode_joint_shard (mds/writer.py:133-144): u32 N, then N + 1 offsets
+      if (tile == v.d.tile0 &&
+          (!v.table_ok || *reinterpret_cast<const uint32_t*>(v.shard) != v.d.samples ||
+           v.offs[0] < v.hdr_end || v.offs[v.d.samples] > v.d.bytes))
+        report_decode(a, MDSX_E_HEADER, v.shard_idx, -1, -1);
     }
   }
 }

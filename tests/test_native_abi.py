@@ -96,10 +96,11 @@ def test_workspace_bytes():
     b.data, b.shards, b.tile_shard = 1, 1, 1
     b.bytes, b.nshards, b.ntiles, b.rows = 1 << 20, 1, 100, 6400
     r = lambda x: (x + 255) // 256 * 256
-    # status block, per-tile totals and prefixes, chunk sums of their scan, per-row addresses
-    # (also the staged decode's huge-row list), row map
-    want = 256 + 2 * r(2 * 100 * 8) + r(2 * (100 // 4096 + 1) * 8) + r(2 * 6400 * 8) + \
-        r(2 * ((1 << 20) // 4096 + 8) * 4)
+    # status block, per-tile totals and prefixes, chunk sums of their scan, the streaming
+    # decode's 48-byte run records, per-row addresses (also the staged decode's huge-row list),
+    # row map
+    want = 256 + 2 * r(2 * 100 * 8) + r(2 * (100 // 4096 + 1) * 8) + r(100 * 48) + \
+        r(2 * 6400 * 8) + r(2 * ((1 << 20) // 4096 + 8) * 4)
     assert lib.mdsx_workspace_bytes(plan.handle, ctypes.byref(b)) == want
     fixed = Plan(['id', 'x'], ['int32', 'ndarray:float32:1024'], [4, 4096])
     assert lib.mdsx_workspace_bytes(fixed.handle, ctypes.byref(b)) == 256
