@@ -96,6 +96,7 @@ struct Stream {
   uint32_t ops;     // vector-memory operations issued by this wave (loads; stores certain to issue)
   uint32_t op_at;   // lane r: `ops` when the slot now in ring position r was issued
   uint32_t mirrored;  // the last slot at ring position 0 copied to the mirror
+  uint32_t landed;    // slots [0, landed) have landed (waited for)
 };
 
 // Issue slots while they fit in the ring above slot `low`: the stream bytes still to be read
@@ -118,6 +119,8 @@ __device__ __forceinline__ void ensure(Stream& st, const lds_u8* ring, uint32_t 
                                        uint32_t lo, uint32_t hi, int lane) {
   pump<S, kNT>(st, ring_lds, lo >> 10, lane);
   const uint32_t upto = min(hi >> 10, st.nslots - 1);
+  if (upto < st.landed) return;  // waited for already
+  st.landed = upto + 1;
   wait_vm_coarse(st.ops - uint32_t(__builtin_amdgcn_readlane(int(st.op_at), int(upto & (S - 1)))) -
                  1u);
   const uint32_t j0 = upto & ~uint32_t(S - 1);
@@ -289,6 +292,7 @@ __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) 
   st.ops = 0;
   st.op_at = 0;
   st.mirrored = 0xffffffffu;
+  st.landed = 0;
   if (fast) {
     st.nq = uint32_t((batch + r.stream + r.bytes - sbase + 15) >> 4);
     st.nslots = (st.nq + 63) >> 6;
@@ -356,10 +360,15 @@ __global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) 
         st.nslots = (st.nq + 63) >> 6;
         st.issued = 0;
         st.mirrored = 0xffffffffu;
+        st.landed = 0;
         pump<S, kNT>(st, ring_lds, 0, lane);
       }
     }
     const uint32_t sp = uint32_t(srow - sbase);  // stream position of the sample
+    // a sample that fits the ring with a slot to spare: all its bytes waited for at once (the
+    // per-column waits then cost a compare each)
+    if (rc == MDSX_OK && size + 16u <= uint32_t(S - 2) * 1024u)
+      ensure<S, kNT>(st, ring, ring_lds, sp, sp + size + 15u, lane);
     // size heads: lane vi holds head vi
     uint32_t h = 0;
     if (rc == MDSX_OK && 4u * uint32_t(nvar) <= size && nvar > 0) {
