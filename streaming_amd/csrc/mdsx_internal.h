@@ -51,6 +51,8 @@ struct mdsx_plan {
   int run_slots = 0;    // ragged plans: KiB of the streaming decode's per-wave LDS ring (0: off)
   int run_kb = 64;      // streaming decode: about this many KiB of samples per tile (tile sizing)
   int64_t run_min = 2048;  // streaming decode for batches whose samples average >= this many bytes
+  int run_nt = 0;          // streaming decode: non-temporal ring loads and stores (measured: the
+                           // temporal ones let L2 merge the partial stores at run edges)
   int gather_chunks = 2;  // 16-byte chunks per lane in the ragged gather (tile = 4 KiB x this)
   int gather_min = 256;   // ragged columns averaging fewer bytes per row use the gather kernel
   int group_max = 1024;   // ... fewer than this (and >= gather_min): four rows per wave

@@ -213,6 +213,8 @@ void apply_tuning(mdsx_plan* p) {
       p->run_slots = int(v);
     } else if (key == "rmin" && v >= 0) {
       p->run_min = v;
+    } else if (key == "rnt") {
+      p->run_nt = v ? 1 : 0;
     } else if (key == "rkb" && v >= 1 && v <= 4096) {
       p->run_kb = int(v);
     }

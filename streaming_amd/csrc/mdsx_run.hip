@@ -431,7 +431,7 @@ int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
   if (a.tile_rows > kRunMaxRows)
     return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode tiles hold at most 32 rows");
 #define MDSX_RUN_CASE(S, NT)                                                              \
-  if (a.run_slots == S && bool(plan->nontemporal) == NT) {                                \
+  if (a.run_slots == S && bool(plan->run_nt) == NT) {                                     \
     if (lds > 64 * 1024) {                                                                \
       const int rc = hip_check(                                                           \
           hipFuncSetAttribute(reinterpret_cast<const void*>(run_decode_kernel<S, NT>),    \
