@@ -21,7 +21,8 @@ for f in glob.glob(sys.argv[1] + '/**/*counter_collection.csv', recursive=True):
         if 'decode_kernel' in r['Kernel_Name']:
             agg[r['Counter_Name']].append(float(r['Counter_Value']))
 m = {k: sum(v) / len(v) for k, v in agg.items()}
-miss, hit, req = (m.get(f'TCP_UTCL1_TRANSLATION_{x}_sum') for x in ('MISS', 'HIT')) + (m.get('TCP_UTCL1_REQUEST_sum'),)
+miss, hit = (m.get(f'TCP_UTCL1_TRANSLATION_{x}_sum') for x in ('MISS', 'HIT'))
+req = m.get('TCP_UTCL1_REQUEST_sum')
 print('shards', sys.argv[2], 'per launch: UTCL1 requests %.4g hits %.4g misses %.4g miss rate %.4f' % (req, hit, miss, miss / max(req, 1)))
 PY
 done
