@@ -254,7 +254,7 @@ __device__ __forceinline__ bool copy_segment(Stream& st, const lds_u8* ring, uin
 }
 
 template <int S, bool kNT>
-__global__ __launch_bounds__(kRunBlock) void run_decode_kernel(const DevArgs a) {
+__global__ __launch_bounds__(kRunBlock, 7) void run_decode_kernel(const DevArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   __shared__ DevCol s_cols[MDSX_MAX_COLUMNS];
   const int t = threadIdx.x, lane = t & 63;
