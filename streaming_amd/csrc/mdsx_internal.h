@@ -49,7 +49,7 @@ struct mdsx_plan {
   int stage_debug = 0;  // measurement only: parts of the staged decode skipped (bits)
   int stage_fill = 70;  // percent of a stage buffer a tile's samples fill on average (tile sizing)
   int run_slots = 0;    // ragged plans: KiB of the streaming decode's per-wave LDS ring (0: off)
-  int run_kb = 64;      // streaming decode: about this many KiB of samples per tile (tile sizing)
+  int run_kb = 32;      // streaming decode: about this many KiB of samples per tile (tile sizing)
   int64_t run_min = 2048;  // streaming decode for batches whose samples average >= this many bytes
   int run_nt = 0;          // streaming decode: non-temporal ring loads and stores (measured: the
                            // temporal ones let L2 merge the partial stores at run edges)

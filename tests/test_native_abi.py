@@ -113,15 +113,15 @@ def test_too_many_columns():
 
 def test_tile_rows_for_sizes_ragged_tiles_to_the_decode(monkeypatch):
     """Ragged plans: batches of long samples (>= 2 KiB on average) go to the streaming decode,
-    whose tiles hold 32-64 KiB of samples (1..32 rows); shorter samples keep the register
+    whose tiles hold 16-32 KiB of samples (1..32 rows); shorter samples keep the register
     decode's 32-row tiles; the staged decode (opt-in) sizes tiles to ~70 % of its 24 KiB stage;
     all-fixed plans: the plan's tile size whatever the batch."""
     from streaming_amd.decoder import Plan
     c = Plan(['b', 'n', 's'], ['bytes', 'int', 'str'], [None, 8, None])
     assert c.tile_rows_for(1 << 26, (1 << 26) // 100) == 32  # 100-byte samples: register decode
     assert c.tile_rows_for(1 << 26, (1 << 26) // 2000) == 32
-    assert c.tile_rows_for(1 << 26, 15_700) == 8  # ~4.3 KB samples: streaming, 8-row tiles
-    assert c.tile_rows_for(1 << 26, (1 << 26) // 2048) == 32
+    assert c.tile_rows_for(1 << 26, 15_700) == 4  # ~4.3 KB samples: streaming, 4-row tiles
+    assert c.tile_rows_for(1 << 26, (1 << 26) // 2048) == 16
     assert c.tile_rows_for(1 << 26, 10) == 1  # 6.7 MB samples: one per tile
     monkeypatch.setenv('MDSX_TUNE', 'run=4,rkb=256')
     assert Plan(['b'], ['bytes'], [None]).tile_rows_for(1 << 26, 15_700) == 32
