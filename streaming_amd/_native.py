@@ -125,7 +125,8 @@ assert ctypes.sizeof(ColumnOut) == 32
 assert ctypes.sizeof(Batch) == 56
 
 _here = os.path.dirname(os.path.abspath(__file__))
-lib_path = os.path.join(_here, 'lib', 'libmdsx.so')
+# MDSX_LIBRARY: another build of the library (measurement A/B of kernel variants in one run)
+lib_path = os.environ.get('MDSX_LIBRARY') or os.path.join(_here, 'lib', 'libmdsx.so')
 
 _lock = threading.Lock()
 _lib: Optional[ctypes.CDLL] = None
