@@ -77,6 +77,7 @@ struct DevArgs {
   uint32_t stage_tiles;  // tiles per workgroup of the staged decode
   uint32_t stage_debug;  // measurement only (MDSX_TUNE sdbg): parts of the staged decode skipped
   uint32_t run_slots;    // KiB of the streaming decode's per-wave ring (0: not the streaming decode)
+  uint32_t rows_bytes;   // LDS stage of the row-parallel decode (0: not the row-parallel decode)
   uint32_t gather_block0[MDSX_MAX_COLUMNS + 1];  // first gather workgroup of each ragged column
   DevCol cols[MDSX_MAX_COLUMNS];
 };
@@ -170,5 +171,6 @@ int launch_stage_totals(const DevArgs& a, hipStream_t s);
 int launch_stage_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s);
 uint32_t stage_tiles_per_wg(uint32_t ntiles);
 int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s);
+int launch_rows_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s);
 
 }  // namespace mdsx_kernels

@@ -53,6 +53,8 @@ struct mdsx_plan {
   int64_t run_min = 2048;  // streaming decode for batches whose samples average >= this many bytes
   int run_nt = 0;          // streaming decode: non-temporal ring loads and stores (measured: the
                            // temporal ones let L2 merge the partial stores at run edges)
+  int rows_kb = 0;         // row-parallel decode of short samples: LDS stage in KiB (0: off)
+  int rows_nt = 0;         // row-parallel decode: non-temporal loads and stores
   int gather_chunks = 2;  // 16-byte chunks per lane in the ragged gather (tile = 4 KiB x this)
   int gather_min = 256;   // ragged columns averaging fewer bytes per row use the gather kernel
   int group_max = 1024;   // ... fewer than this (and >= gather_min): four rows per wave
@@ -67,4 +69,10 @@ struct mdsx_plan {
 // register decode, measured 2x and 1.3x faster there).
 inline bool use_run_decode(const mdsx_plan* p, uint64_t bytes, uint64_t rows) {
   return p->nvar > 0 && p->run_slots > 0 && rows > 0 && bytes / rows >= uint64_t(p->run_min);
+}
+
+// Whether a ragged batch of shorter samples decodes through the row-parallel decode
+// (mdsx_rows.hip).
+inline bool use_rows_decode(const mdsx_plan* p, uint64_t bytes, uint64_t rows) {
+  return p->nvar > 0 && p->rows_kb > 0 && rows > 0 && !use_run_decode(p, bytes, rows);
 }

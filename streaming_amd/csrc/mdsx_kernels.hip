@@ -873,11 +873,13 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   a->stage_debug = uint32_t(plan->stage_debug);
   a->run_slots = use_run_decode(plan, b->bytes, b->rows) ? uint32_t(plan->run_slots) : 0u;
   if (a->run_slots) a->stage_bytes = 0;  // the streaming decode takes precedence
+  a->rows_bytes = use_rows_decode(plan, b->bytes, b->rows) ? uint32_t(plan->rows_kb) * 1024u : 0u;
+  if (a->rows_bytes) a->stage_bytes = 0;
   if (a->run_slots && tr > 32)
     return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode tiles hold at most 32 rows");
   // the staged and streaming decodes scan one total per tile; the register-copy decode one per
   // 256 rows
-  a->scan_per = (a->stage_bytes || a->run_slots) ? 1u : uint32_t(kBlock / tr);
+  a->scan_per = (a->stage_bytes || a->run_slots || a->rows_bytes) ? 1u : uint32_t(kBlock / tr);
   a->nscan = (b->ntiles + a->scan_per - 1) / a->scan_per;
   a->nchunk = (a->nscan + kScanChunk - 1) / kScanChunk;
   a->nshards = b->nshards;
@@ -1215,7 +1217,7 @@ int mdsx_scan_shards(const mdsx_plan* plan, const mdsx_batch* batch, const mdsx_
   hipStream_t s = static_cast<hipStream_t>(stream);
   rc = hip_check(hipMemsetAsync(d_workspace, 0, kStatusBlock, s), "hipMemsetAsync");
   if (rc != MDSX_OK || plan->nvar == 0) return rc;
-  if (a.ntiles > 0 && (a.stage_bytes || a.run_slots)) {
+  if (a.ntiles > 0 && (a.stage_bytes || a.run_slots || a.rows_bytes)) {
     rc = launch_stage_totals(a, s);
     if (rc != MDSX_OK) return rc;
   } else if (a.ntiles > 0) {
@@ -1243,6 +1245,7 @@ static int launch_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s,
                          const uint64_t* mode_bytes) {
   int rc = MDSX_OK;
   if (plan->nvar > 0 && !single && a.run_slots > 0) return launch_run_decode(plan, a, s);
+  if (plan->nvar > 0 && !single && a.rows_bytes > 0) return launch_rows_decode(plan, a, s);
   if (plan->nvar > 0 && !single && a.stage_bytes > 0) return launch_stage_decode(plan, a, s);
   const size_t lds =
       size_t(a.tile_rows) * (12 * size_t(plan->nvar) + 4 * size_t(plan->ncols) + 1) + 16;

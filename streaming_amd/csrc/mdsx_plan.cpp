@@ -215,6 +215,10 @@ void apply_tuning(mdsx_plan* p) {
       p->run_min = v;
     } else if (key == "rnt") {
       p->run_nt = v ? 1 : 0;
+    } else if (key == "rows" && v >= 0 && v <= 96) {
+      p->rows_kb = int(v);
+    } else if (key == "rownt") {
+      p->rows_nt = v ? 1 : 0;
     } else if (key == "rkb" && v >= 1 && v <= 4096) {
       p->run_kb = int(v);
     }
@@ -344,6 +348,13 @@ int mdsx_plan_tile_rows_for(const mdsx_plan* plan, uint64_t shard_bytes, uint64_
     const uint64_t per_row = std::max<uint64_t>(1, shard_bytes / rows);
     int tr = 1;
     while (tr < 32 && uint64_t(tr) * 2 * per_row <= uint64_t(plan->run_kb) * 1024) tr *= 2;
+    return tr;
+  }
+  if (use_rows_decode(plan, shard_bytes, rows)) {
+    // row-parallel decode: samples filling about half the LDS stage on average, 1..256 rows
+    const uint64_t per_row = std::max<uint64_t>(1, shard_bytes / rows);
+    int tr = 1;
+    while (tr < 256 && uint64_t(tr) * 4 * per_row <= uint64_t(plan->rows_kb) * 1024) tr *= 2;
     return tr;
   }
   if (plan->nvar == 0 || plan->stage_kb == 0 || rows == 0) return plan->tile_rows;

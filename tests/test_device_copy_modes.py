@@ -33,6 +33,8 @@ MODES = {
     'run': 'run=8,rmin=0',  # the streaming decode (mdsx_run.hip) whatever the sample size
     'run4': 'run=4,rmin=0,rkb=4',  # small ring, 1-2-row tiles
     'run16': 'run=16,rmin=0,rkb=1024',  # 32-row tiles
+    'rows': 'rows=32,rmin=1000000000',  # the row-parallel decode (mdsx_rows.hip) for every size
+    'rows_small': 'rows=2,rmin=1000000000',  # a 2 KiB stage: windows and HBM-direct samples
     'stage': 'stage=24,run=0',  # the staged decode (opt-in; measured slower)
     'stage_overflow': 'stage=4,fill=300,run=0',  # tiles of ~3x the stage: several row groups each
     'stage_tiny': 'stage=1,run=0',  # rows over 1 KiB go through the huge-row kernel
