@@ -41,7 +41,7 @@ struct TileRun {
   uint32_t r0;      // first sample of the run inside its shard
   uint16_t nrows;
   uint16_t fast;    // the table fits and every sample of the run passes the file checks
-  uint64_t reserved;
+  uint64_t shard_off;  // batch byte of the shard
 };
 static_assert(sizeof(TileRun) == 48, "TileRun layout");
 
@@ -172,5 +172,8 @@ int launch_stage_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s);
 uint32_t stage_tiles_per_wg(uint32_t ntiles);
 int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s);
 int launch_rows_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s);
+// The samples listed (tile << 32 | row in tile, a.src_abs; count at kHugeCountOffset) as larger
+// than an LDS stage: one workgroup each, straight from HBM (mdsx_stage.hip).
+int launch_huge_rows(const DevArgs& a, bool nt, hipStream_t s);
 
 }  // namespace mdsx_kernels

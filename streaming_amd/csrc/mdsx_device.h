@@ -216,16 +216,17 @@ __device__ __forceinline__ uint4 readlane0(const uint4 v) {
                     __builtin_amdgcn_readlane(v.z, 0), __builtin_amdgcn_readlane(v.w, 0));
 }
 
+// 0xFF in byte i of the result where bit i of the nibble x is set (the four shifted copies of x
+// that the multiply adds never overlap, so no carries).
+__device__ __forceinline__ uint32_t nibble_bytes(uint32_t x) {
+  return ((x * 0x00204081u) & 0x01010101u) * 0xFFu;
+}
+
 // Byte mask of bytes [a, b) of a 16-byte chunk (0 <= a <= b <= 16).
 __device__ __forceinline__ uint4 byte_mask(uint32_t a, uint32_t b) {
-  uint32_t m[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int lo = min(max(int(a) - 4 * j, 0), 4), hi = min(max(int(b) - 4 * j, 0), 4);
-    const uint64_t mh = (uint64_t(1) << (8 * hi)) - 1, ml = (uint64_t(1) << (8 * lo)) - 1;
-    m[j] = uint32_t(mh & ~ml);
-  }
-  return make_uint4(m[0], m[1], m[2], m[3]);
+  const uint32_t bits = ((1u << b) - 1u) & ~((1u << a) - 1u);
+  return make_uint4(nibble_bytes(bits & 15u), nibble_bytes((bits >> 4) & 15u),
+                    nibble_bytes((bits >> 8) & 15u), nibble_bytes(bits >> 12));
 }
 
 // Bytes [a, b) (0 <= a <= b <= 16) of `val` merged into `acc`.
@@ -277,6 +278,79 @@ __device__ __forceinline__ bool utf8_chunk_bad(const uint4 v, uint32_t pw, bool 
                  utf8_dword_err(v.w, v.z);
   if (last) err |= utf8_dword_err(0u, v.w);  // positions 16..18 after the segment end
   return err != 0;
+}
+
+// ---- The same check by nibble tables (the Keiser-Lemire classification), about half the
+// operations of utf8_dword_err: the error bits of a byte are the AND of three 16-entry byte-table
+// lookups -- the previous byte's high nibble, its low nibble, this byte's high nibble -- each
+// done with v_perm_b32 (an 8-entry byte select) and a blend; a byte that two / three bytes back
+// has a lead >= E0 / F0 must be a continuation, which flips bit 7 (two continuations in a row)
+// via must23. Error bits: 0 too short, 1 too long, 2 overlong 3-byte, 3 too large, 4 surrogate,
+// 5 overlong 2-byte, 6 too large / overlong 4-byte, 7 two continuations. p1: the previous byte of
+// each byte (v_alignbyte of this dword and the one before). Nonzero bytes of the result err.
+__device__ __forceinline__ uint32_t utf8_lookup_err(uint32_t x, uint32_t p1, uint32_t must23) {
+  const uint32_t sign1 = ((p1 >> 7) & 0x01010101u) * 0xFFu;  // previous byte >= 0x80
+  // previous byte, high nibble: 0..7 -> 02 (ASCII), 8..B -> 80, C 21, D 01, E 15, F 49
+  const uint32_t b1h = (__builtin_amdgcn_perm(0x49150121u, 0x80808080u, (p1 >> 4) & 0x07070707u) &
+                        sign1) | (0x02020202u & ~sign1);
+  // previous byte, low nibble: E7 A3 83 83 8B CB CB CB | CB CB CB CB CB DB CB CB
+  const uint32_t lo3 = p1 & 0x07070707u;
+  const uint32_t m8 = ((p1 >> 3) & 0x01010101u) * 0xFFu;
+  const uint32_t b1l = (__builtin_amdgcn_perm(0xCBCBDBCBu, 0xCBCBCBCBu, lo3) & m8) |
+                       (__builtin_amdgcn_perm(0xCBCBCB8Bu, 0x8383A3E7u, lo3) & ~m8);
+  // this byte, high nibble: 8 E6, 9 AE, A..B BA (continuations), else 01
+  const uint32_t cont = (((x & ~(x << 1)) >> 7) & 0x01010101u) * 0xFFu;
+  const uint32_t b2h = (__builtin_amdgcn_perm(0u, 0xBABAAEE6u, (x >> 4) & 0x03030303u) & cont) |
+                       (0x01010101u & ~cont);
+  return (b1h & b1l & b2h) ^ must23;
+}
+
+// Bytes [a, b) of v (0 <= a <= b <= 16), others zero.
+__device__ __forceinline__ uint4 keep_bytes(const uint4 v, uint32_t a, uint32_t b) {
+  const uint4 m = byte_mask(a, b);
+  return make_uint4(v.x & m.x, v.y & m.y, v.z & m.z, v.w & m.w);
+}
+
+// A sequence still open after the byte before chunk byte s (1..16) of the stream pw | X: one of
+// the bytes s-1 / s-2 / s-3 is a lead >= C0 / E0 / F0 (a lead that saw too few continuations; if
+// its sequence was already broken the check errs there anyway).
+__device__ __forceinline__ bool utf8_open_at(const uint4 X, uint32_t pw, uint32_t s) {
+  const uint32_t q = s >> 2;
+  const uint32_t lo = q == 0 ? pw : q == 1 ? X.x : q == 2 ? X.y : q == 3 ? X.z : X.w;
+  const uint32_t hi = q == 0 ? X.x : q == 1 ? X.y : q == 2 ? X.z : X.w;
+  const uint32_t w = alignbyte(hi, lo, s & 3);  // bytes s-4 .. s-1
+  const uint32_t t = w & (w << 1);
+  return ((t & 0x80000000u) | (t & (w << 2) & 0x00800000u) |
+          (t & (w << 2) & (w << 3) & 0x00008000u)) != 0;
+}
+
+// The 16 chunk bytes X (bytes outside the chunk's pieces zero) of two consecutive values: A,
+// bytes < sB, whose bytes before the chunk end in pw (bytes before A's start zero), and B, bytes
+// >= sB (1 <= sB <= 16; 16: A only), starting at sB. Every byte takes its context from its own
+// value. Returns bit 0: A errs inside the chunk, bit 1: B does (a value that ends in the chunk
+// is followed by zeros, which err after an open sequence; A's end at sB and a value ending at
+// the chunk's end are the caller's, utf8_open_at).
+__device__ __forceinline__ uint32_t utf8_chunk_err2(const uint4 X, uint32_t pw, uint32_t sB) {
+  const uint4 MB = byte_mask(sB, 16);
+  const uint32_t xs[4] = {X.x, X.y, X.z, X.w};
+  const uint32_t ms[4] = {MB.x, MB.y, MB.z, MB.w};
+  uint32_t errA = 0, errB = 0;
+  uint32_t prev = pw, prevB = 0;
+  uint32_t Ep = hi_e0(pw), Fp = hi_f0(pw), EBp = 0, FBp = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t x = xs[j], mb = ms[j];
+    const uint32_t xB = x & mb;
+    const uint32_t E = hi_e0(x), F = hi_f0(x), EB = E & mb, FB = F & mb;
+    const uint32_t p1 = (alignbyte(xB, prevB, 3) & mb) | (alignbyte(x, prev, 3) & ~mb);
+    const uint32_t m23 = ((alignbyte(EB, EBp, 2) | alignbyte(FB, FBp, 1)) & mb) |
+                         ((alignbyte(E, Ep, 2) | alignbyte(F, Fp, 1)) & ~mb);
+    const uint32_t err = utf8_lookup_err(x, p1, m23);
+    errA |= err & ~mb;
+    errB |= err & mb;
+    prev = x, prevB = xB, Ep = E, Fp = F, EBp = EB, FBp = FB;
+  }
+  return (errA != 0 ? 1u : 0u) | (errB != 0 ? 2u : 0u);
 }
 
 // Bytes of a 16-byte chunk at address D that lie in [lo, hi), others zeroed.

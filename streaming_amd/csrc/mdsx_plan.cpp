@@ -351,10 +351,18 @@ int mdsx_plan_tile_rows_for(const mdsx_plan* plan, uint64_t shard_bytes, uint64_
     return tr;
   }
   if (use_rows_decode(plan, shard_bytes, rows)) {
-    // row-parallel decode: samples filling about half the LDS stage on average, 1..256 rows
+    // row-parallel decode: samples filling at most 8/9 of the LDS stage on average (a tile of
+    // longer samples is decoded in windows), 1..256 rows
     const uint64_t per_row = std::max<uint64_t>(1, shard_bytes / rows);
     int tr = 1;
-    while (tr < 256 && uint64_t(tr) * 4 * per_row <= uint64_t(plan->rows_kb) * 1024) tr *= 2;
+    const uint64_t cap = uint64_t(plan->rows_kb) * 1024;
+    // the workgroup's LDS (mdsx_rows.hip: stage, per-column tables, marks, chunk maps) <= 160 KiB
+    auto lds = [&](uint64_t r) {
+      return 192 + cap + r * uint64_t(plan->ncols) * 16 + uint64_t(plan->ncols) * 32 +
+             uint64_t(plan->nvar) * (cap / 16 + 4);
+    };
+    while (tr < 256 && uint64_t(tr) * 2 * per_row * 9 <= cap * 8 && lds(uint64_t(tr) * 2) <= 160 * 1024)
+      tr *= 2;
     return tr;
   }
   if (plan->nvar == 0 || plan->stage_kb == 0 || rows == 0) return plan->tile_rows;

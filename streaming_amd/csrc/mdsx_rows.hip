@@ -1,29 +1,34 @@
 // Row-parallel decode of ragged plans with short samples (gfx950): a workgroup decodes one tile
 // -- up to 256 consecutive samples of one shard -- from a single LDS copy of the tile's bytes, one
-// thread per sample.
+// thread per sample for the per-sample work and one thread per 16-byte output chunk for the copy.
 //
 // The reference decodes one sample per call (MDSReader.get_sample_data, mds/reader.py:128-149;
 // decode_sample, :103-126; mds_decode, encodings.py:760-773). The samples of a tile are one
 // contiguous byte range of the shard (sample i ends where i + 1 starts), so the workgroup
 //   1. copies the range into LDS once (global_load_lds_dwordx4, 1 KiB per wave-instruction, the
-//      range started on a 128-byte line);
+//      range started on a 128-byte line). A tile the scan pass found clean and small enough
+//      (its TileRun record, stage_totals_kernel) is copied straight from that record, in flight
+//      together with the tile's offsets;
 //   2. parses each sample's size heads and column boundaries from LDS, one thread per sample
 //      (decode_sample's head loop; a sample whose offsets or columns do not fit counts zero
 //      bytes and is reported, the scan pass's rule);
-//   3. scans the ragged lengths across the tile (block scan) onto the tile's output base (from
-//      the scan pass, stage_totals_kernel + the reduce-then-scan kernels);
-//   4. writes every column: the thread of sample j owns the 16-byte-aligned output chunks whose
-//      first byte is one of its own, assembles each from LDS with unaligned ds_read_b128 (a chunk
-//      that runs past the sample's end takes the following samples' bytes), and stores it whole;
-//      only the chunks a tile shares with its neighbours are stored a byte at a time;
-//   5. checks its str values for strict UTF-8 from LDS (what bytes.decode('utf-8') accepts,
-//      encodings.py:80-81) and writes its offsets and flags.
+//   3. scans the ragged lengths across the tile (one block scan per pair of ragged columns, the
+//      two 32-bit sums packed in one 64-bit word) onto the tile's output base (from the scan
+//      pass), writes the offsets, and marks which sample holds the first byte of every output
+//      chunk (the chunk map);
+//   4. writes every column output-chunk-parallel: consecutive threads assemble consecutive
+//      16-byte chunks of the column's output from LDS (unaligned ds_read_b128; a chunk spanning
+//      several samples takes a piece of each) and store them whole; only the chunks a tile
+//      shares with its neighbours are stored a byte at a time. The pieces of str values are
+//      checked for strict UTF-8 on the way (what bytes.decode('utf-8') accepts,
+//      encodings.py:80-81; the dword before a piece comes from the same value), a failing piece
+//      marks its sample, and each sample's flag is written at the end.
 // Per-sample work is spread over lanes, not looped over by one wave: the per-sample scalar
 // control of the streaming decode (mdsx_run.hip) is what bounds short samples there.
 //
 // A tile whose range exceeds the LDS stage is decoded in windows of samples that fit, each window
-// a tile of its own for the edge chunks; a sample larger than the stage is copied straight from
-// HBM by the workgroup's four waves.
+// a tile of its own for the edge chunks; a sample larger than the stage is listed for the
+// huge-row kernel (stage_huge_kernel, straight from HBM) once its offsets are written.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -47,54 +52,48 @@ __device__ __forceinline__ uint4 lds_read16(const lds_u8* p) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// A u32 of the stage at an arbitrary byte position (unaligned ds_read_b32).
+__device__ __forceinline__ uint32_t lds_u32(const lds_u8* p) { return *(const MDSX_L uint32_t*)p; }
+
 // Bytes [from, to) (0 <= from <= to <= 16) of chunk v stored at the aligned address D.
 __device__ __forceinline__ void store_bytes(uint64_t D, const uint4 v, uint32_t from, uint32_t to) {
   for (uint32_t b = from; b < to; ++b) *gp_at<uint8_t>(D + b) = uint8_t(byte_of(v, int(b)));
 }
 
-// Per-column, per-sample tables of the window in LDS.
-struct RowsTab {
-  MDSX_L uint32_t* src;  // [ncols][TR] stage position of the column's first byte
-  MDSX_L uint32_t* len;  // [ncols][TR] bytes (0: a sample that failed a check)
-  MDSX_L uint64_t* dst;  // [ncols][TR] output byte of the column value, relative to its data
+__host__ __device__ __forceinline__ uint32_t rows_map_len(uint32_t cap) { return cap / 16 + 4; }
+
+// LDS of one workgroup: the stage, then per-column tables of the window ([ncols][TR] output
+// byte of the value inside the window's output, stage byte, length), the UTF-8 marks ([ncols]
+// [8] bits, one per sample) and the chunk maps ([nvar][map_len]: the sample holding the first
+// window byte of each output chunk).
+__host__ __device__ __forceinline__ size_t rows_lds_bytes(uint32_t cap, int TR, int ncols,
+                                                          int nvar) {
+  return kStageFront + size_t(cap) + kStageSlack + size_t(TR) * size_t(ncols) * 16 +
+         size_t(ncols) * 32 + size_t(nvar) * rows_map_len(cap);
+}
+
+// One value of the window: output byte inside the window's output of its column, bytes (0: a
+// sample that failed a check), stage position of its first byte (read with one ds_read_b128).
+struct RowsRec {
+  uint32_t dst, len, src, pad;
 };
 
-__host__ __device__ __forceinline__ size_t rows_tab_bytes(int TR, int ncols) {
-  return size_t(TR) * size_t(ncols) * 16;
-}
-
-__host__ __device__ __forceinline__ size_t rows_lds_bytes(uint32_t cap, int TR, int ncols) {
-  return kStageFront + size_t(cap) + kStageSlack + rows_tab_bytes(TR, ncols);
-}
-
-// The 16 output bytes at aligned column address D (absolute), from the window's samples r, r + 1,
-// ... (stage bytes; a sample whose value is not in the stage leaves zeros) whose values cover
-// them, starting at byte `from` of the chunk.
-__device__ __forceinline__ uint4 assemble(const lds_u8* stage, const RowsTab& T, int base, int r,
-                                          int gb, uint64_t data, uint64_t D, uint32_t from) {
-  uint4 val = make_uint4(0, 0, 0, 0);
-  uint64_t pos = D + from;
-  for (; r < gb && pos < D + 16; ++r) {
-    const uint32_t len = T.len[base + r];
-    const uint64_t ds = data + T.dst[base + r];
-    const uint64_t de = ds + len;
-    if (de <= pos || len == 0) continue;
-    const uint64_t a = max(pos, ds), b = min(D + 16, de);
-    const uint4 v = lds_read16(stage + T.src[base + r] + uint32_t(a - ds) - uint32_t(a - D));
-    val = merge_bytes(val, v, uint32_t(a - D), uint32_t(b - D));
-    pos = b;
-  }
-  return val;
-}
+struct RowsTab {
+  MDSX_L RowsRec* rec;   // [ncols][TR]
+  MDSX_L uint32_t* bad;  // [ncols][8]: UTF-8 failures of the tile's samples
+  MDSX_L uint8_t* map;   // [nvar][map_len]
+};
 
 template <bool kNT>
-__global__ __launch_bounds__(kRowsBlock) void rows_decode_kernel(const DevArgs a) {
+__global__ __launch_bounds__(kRowsBlock, 5) void rows_decode_kernel(const DevArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   __shared__ DevCol s_cols[MDSX_MAX_COLUMNS];
   __shared__ int64_t s_wsum[kRowsBlock / 64];
-  __shared__ uint64_t s_base[MDSX_MAX_COLUMNS];  // next output byte of each column (rel. data)
+  __shared__ uint64_t s_base[MDSX_MAX_COLUMNS];   // next output byte of each column (rel. data)
+  __shared__ uint64_t s_wbase[MDSX_MAX_COLUMNS];  // the window's first output byte (rel. data)
+  __shared__ uint32_t s_wlen[MDSX_MAX_COLUMNS];   // the window's output bytes
   __shared__ uint32_t s_skip[MDSX_MAX_COLUMNS];   // the tile's bytes exceed the column capacity
-  __shared__ uint32_t s_gb, s_lo, s_hi, s_bdir;
+  __shared__ uint32_t s_gb, s_lo, s_hi;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   for (int c = t; c < a.ncols; c += kRowsBlock) s_cols[c] = a.cols[c];
   const MDSX_L DevCol* cols = (const MDSX_L DevCol*)s_cols;
@@ -102,30 +101,58 @@ __global__ __launch_bounds__(kRowsBlock) void rows_decode_kernel(const DevArgs a
   const int TR = a.tile_rows;
   const int ncols = a.ncols, nvar = a.nvar;
   const uint32_t cap = a.rows_bytes;
+  const uint32_t map_len = rows_map_len(cap);
   const lds_u8* stage = (const lds_u8*)(smem + kStageFront);
   RowsTab T;
-  T.dst = (MDSX_L uint64_t*)(smem + kStageFront + cap + kStageSlack);
-  T.src = (MDSX_L uint32_t*)(T.dst + size_t(ncols) * TR);
-  T.len = T.src + size_t(ncols) * TR;
+  T.rec = (MDSX_L RowsRec*)(smem + kStageFront + cap + kStageSlack);
+  T.bad = (MDSX_L uint32_t*)(T.rec + size_t(ncols) * TR);
+  T.map = (MDSX_L uint8_t*)(T.bad + size_t(ncols) * 8);
   const uint32_t stage_lds = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(
       reinterpret_cast<uintptr_t>((const MDSX_L uint8_t*)(smem + kStageFront))));
+  for (int i = t; i < ncols * 8; i += kRowsBlock) T.bad[i] = 0;
 
-  const TileView v = tile_view(a, tile);
-  if (t == 0 && tile == v.d.tile0) {
-    // header written by encode_joint_shard (mds/writer.py:133-144): u32 N, then N + 1 offsets
-    if (!v.table_ok || *reinterpret_cast<const uint32_t*>(v.shard) != v.d.samples ||
-        v.offs[0] < v.hdr_end || v.offs[v.d.samples] > v.d.bytes)
-      report_decode(a, MDSX_E_HEADER, v.shard_idx, -1, -1);
-  }
-  if (!v.table_ok) return;  // block-uniform
-  const int n = int(v.nrows);
-  const uint64_t row0 = v.d.row0 + v.r0;
-  // this thread's sample: offsets pair and file checks (mds/reader.py:137-148)
+  // ---- the tile: its run record (scan pass) or its shard's view
+  const TileRun run = a.tile_run[tile];
+  const bool fast = run.fast && (run.stream & 127) + run.bytes <= cap;  // block-uniform
+  const uint8_t* frame;  // b / e below are byte positions relative to frame
+  int n;
+  uint64_t row0;
+  uint32_t shard_idx, r0;
   uint32_t b = 0, e = 0;
-  int rc = MDSX_OK;
-  if (t < n) rc = sample_range(v, v.r0 + uint32_t(t), &b, &e);
-  const bool in_range = t < n && rc == MDSX_OK;
-  if (t < n && rc != MDSX_OK) report_decode(a, rc, v.shard_idx, int(v.r0 + t), -1);
+  bool in_range = false;
+  if (fast) {
+    // one window: the DMA of the run's bytes goes out with the offsets loads
+    n = run.nrows;
+    row0 = run.row0;
+    shard_idx = run.shard;
+    r0 = run.r0;
+    frame = a.batch + run.shard_off;
+    const uint64_t lo_al = run.stream & ~uint64_t(127);
+    const uint32_t nq = uint32_t((run.stream + run.bytes - lo_al + 15) >> 4);
+    const uint4* src = reinterpret_cast<const uint4*>(a.batch + lo_al);
+    for (uint32_t kb = uint32_t(wave); kb * 64 < nq; kb += kRowsBlock / 64) {
+      const uint32_t k = kb * 64 + uint32_t(lane);
+      if (k < nq) glds16<kNT>(src + k, stage_lds + kb * 1024u);  // lanes past nq write nothing
+    }
+    if (t < n) {
+      const uint32_t* o = reinterpret_cast<const uint32_t*>(a.batch + run.offs);
+      b = o[t];
+      e = o[t + 1];
+      in_range = true;  // run.fast: every sample of the run passed the file checks
+    }
+  } else {
+    const TileView v = tile_view(a, tile);
+    if (!v.table_ok) return;  // block-uniform; reported by the scan pass
+    n = int(v.nrows);
+    row0 = v.d.row0 + v.r0;
+    shard_idx = v.shard_idx;
+    r0 = v.r0;
+    frame = v.shard;
+    int rc = MDSX_OK;
+    if (t < n) rc = sample_range(v, v.r0 + uint32_t(t), &b, &e);
+    in_range = t < n && rc == MDSX_OK;
+    if (t < n && rc != MDSX_OK) report_decode(a, rc, shard_idx, int(r0 + t), -1);
+  }
   if (t < ncols) {
     const MDSX_L DevCol& col = cols[t];
     const int vi = col.var_index;
@@ -134,159 +161,248 @@ __global__ __launch_bounds__(kRowsBlock) void rows_decode_kernel(const DevArgs a
       const uint64_t off = uint64_t(a.tile_prefix[uint64_t(vi) * a.nscan + tile]);
       s_base[t] = off;
       if (off + uint64_t(a.tile_total[uint64_t(vi) * a.nscan + tile]) > col.capacity) {
-        report_decode(a, MDSX_E_CAPACITY, v.shard_idx, int(v.r0), t);
+        report_decode(a, MDSX_E_CAPACITY, shard_idx, int(r0), t);
         skip = 1;
       }
-    } else {
-      s_base[t] = row0 * col.row_bytes;
     }
     s_skip[t] = skip;
   }
 
   for (int ga = 0; ga < n;) {  // block-uniform loop over windows
     // ---- the window: samples [ga, gb) whose bytes lie in [lo, lo + cap)
-    __syncthreads();  // the previous window's readers of the stage and the tables are done
-    if (t == 0) s_gb = uint32_t(n), s_lo = 0xffffffffu;
-    __syncthreads();
-    if (t >= ga && in_range) atomicMin(&s_lo, b);  // the window's first in-range byte
-    __syncthreads();
-    const uint32_t lo = s_lo;
-    if (t >= ga && in_range && !(b >= lo && e - lo <= cap)) atomicMin(&s_gb, uint32_t(t));
-    __syncthreads();
-    int gb = int(s_gb);
-    const bool direct = gb == ga;  // sample ga alone is larger than the stage: from HBM
-    if (direct) gb = ga + 1;
-    const uint32_t lo_al = lo & ~127u;
-    // ---- 1. the window's bytes [lo_al, hi) into LDS, hi the largest end of its in-range samples
-    if (t == 0) s_hi = 0;
-    __syncthreads();
-    if (t >= ga && t < gb && in_range) atomicMax(&s_hi, e);
-    if (direct && t == ga) s_bdir = b;
-    __syncthreads();
-    const uint32_t hi = s_hi;
-    if (!direct && lo != 0xffffffffu && hi > lo_al) {
-      const uint32_t nq = (hi - lo_al + 15) >> 4;
-      const uint4* src = reinterpret_cast<const uint4*>(v.shard + lo_al);
-      for (uint32_t kb = uint32_t(wave); kb * 64 < nq; kb += kRowsBlock / 64) {
-        const uint32_t k = kb * 64 + uint32_t(lane);
-        if (k < nq) glds16<kNT>(src + k, stage_lds + kb * 1024u);  // lanes past nq write nothing
-      }
+    int gb;
+    uint32_t lo_al;  // stage byte 0 = frame byte lo_al
+    bool direct = false;
+    if (fast) {
+      gb = n;
+      lo_al = uint32_t((run.stream & ~uint64_t(127)) - run.shard_off);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      __syncthreads();  // the previous window's readers of the stage and the tables are done
+      if (t == 0) s_gb = uint32_t(n), s_lo = 0xffffffffu, s_hi = 0;
+      __syncthreads();
+      if (t >= ga && in_range) atomicMin(&s_lo, b);  // the window's first in-range byte
+      __syncthreads();
+      const uint32_t lo = s_lo;
+      if (t >= ga && in_range && !(b >= lo && e - lo <= cap)) atomicMin(&s_gb, uint32_t(t));
+      __syncthreads();
+      gb = int(s_gb);
+      direct = gb == ga;  // sample ga alone is larger than the stage: the huge-row kernel's
+      if (direct) gb = ga + 1;
+      lo_al = lo & ~127u;
+      // ---- 1. the window's bytes [lo_al, hi) into LDS, hi the largest end of its samples
+      if (t >= ga && t < gb && in_range) atomicMax(&s_hi, e);
+      __syncthreads();
+      const uint32_t hi = s_hi;
+      if (!direct && lo != 0xffffffffu && hi > lo_al) {
+        const uint32_t nq = (hi - lo_al + 15) >> 4;
+        const uint4* src = reinterpret_cast<const uint4*>(frame + lo_al);
+        for (uint32_t kb = uint32_t(wave); kb * 64 < nq; kb += kRowsBlock / 64) {
+          const uint32_t k = kb * 64 + uint32_t(lane);
+          if (k < nq) glds16<kNT>(src + k, stage_lds + kb * 1024u);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
     }
     __syncthreads();
 
     // ---- 2. column boundaries of this thread's sample (mds/reader.py:111-125)
     const bool mine = t >= ga && t < gb;
+    const uint32_t sp = b - lo_al;  // stage position of the sample (not direct)
+    auto head = [&](int vi) -> uint32_t {
+      return direct ? load_u32_any(frame + b + 4u * uint32_t(vi))
+                    : lds_u32(stage + sp + 4u * uint32_t(vi));
+    };
     bool ok = mine && in_range;
-    uint32_t need = 4u * uint32_t(nvar);
+    uint64_t need = 4ull * uint64_t(nvar);
     if (ok && need > e - b) ok = false;
     if (ok) {
       for (int c = 0; c < ncols; ++c) {
         const int vi = cols[c].var_index;
-        need += vi >= 0 ? (direct ? load_u32_any(v.shard + b + 4u * uint32_t(vi))
-                                  : *(const MDSX_L uint32_t*)(stage + (b - lo_al) + 4u * vi))
-                        : cols[c].row_bytes;
+        need += vi >= 0 ? head(vi) : cols[c].row_bytes;
       }
       if (need > e - b) ok = false;
     }
-    if (mine && in_range && !ok) report_decode(a, MDSX_E_BOUNDS, v.shard_idx, int(v.r0 + t), -1);
-    // ---- 3. offsets: lengths scanned across the window onto each column's base
-    uint32_t rel = 4u * uint32_t(nvar);
-    for (int c = 0; c < ncols; ++c) {
-      const MDSX_L DevCol& col = cols[c];
-      const int vi = col.var_index;
-      uint32_t len = 0;
-      if (ok)
-        len = vi >= 0 ? (direct ? load_u32_any(v.shard + b + 4u * uint32_t(vi))
-                                : *(const MDSX_L uint32_t*)(stage + (b - lo_al) + 4u * vi))
-                      : col.row_bytes;
-      uint64_t dst;
-      if (vi >= 0) {
-        int64_t total;
-        const int64_t excl = block_exclusive_scan(mine ? int64_t(len) : 0, s_wsum, &total);
-        dst = s_base[c] + uint64_t(excl);
-        __syncthreads();  // every thread has read s_base[c]
-        if (t == 0) s_base[c] += uint64_t(total);
-        if (mine) *gp(col.offsets + row0 + t) = int64_t(dst);
-      } else {
-        dst = uint64_t(row0 + t) * col.row_bytes;
+    if (mine && in_range && !ok) report_decode(a, MDSX_E_BOUNDS, shard_idx, int(r0 + t), -1);
+    // ---- 3. value lengths and stage positions; fixed columns' window output
+    {
+      uint32_t rel = 4u * uint32_t(nvar);
+      for (int c = 0; c < ncols; ++c) {
+        const MDSX_L DevCol& col = cols[c];
+        const int vi = col.var_index;
+        const uint32_t len = ok ? (vi >= 0 ? head(vi) : col.row_bytes) : 0u;
+        if (mine) {
+          T.rec[c * TR + t].len = len;
+          T.rec[c * TR + t].src = (direct ? 0u : sp) + rel;
+          if (vi < 0) T.rec[c * TR + t].dst = uint32_t(t - ga) * col.row_bytes;
+        }
+        if (vi < 0 && t == 0) {
+          s_wbase[c] = (row0 + uint64_t(ga)) * col.row_bytes;
+          s_wlen[c] = uint32_t(gb - ga) * col.row_bytes;
+        }
+        rel += len;
       }
-      if (mine) {
-        T.dst[c * TR + t] = dst;
-        T.src[c * TR + t] = direct ? rel : (b - lo_al) + rel;  // direct: inside the sample
-        T.len[c * TR + t] = len;
+    }
+    // ragged lengths scanned across the window onto each column's base, two columns per scan;
+    // offsets; chunk maps
+    for (int c0 = 0; c0 < ncols;) {
+      int c1 = c0;
+      while (c1 < ncols && cols[c1].var_index < 0) ++c1;
+      if (c1 >= ncols) break;
+      int c2 = c1 + 1;
+      while (c2 < ncols && cols[c2].var_index < 0) ++c2;
+      const bool pair = c2 < ncols;
+      const uint64_t len1 = mine ? T.rec[c1 * TR + t].len : 0u;
+      const uint64_t len2 = (mine && pair) ? T.rec[c2 * TR + t].len : 0u;
+      const uint64_t base1 = s_base[c1], base2 = pair ? s_base[c2] : 0;
+      int64_t total;
+      // each half sums at most the window's bytes (< 2^32): no carry between the halves
+      const int64_t excl = block_exclusive_scan(int64_t(len1 | (len2 << 32)), s_wsum, &total);
+      for (int h = 0; h < (pair ? 2 : 1); ++h) {
+        const int c = h ? c2 : c1;
+        const MDSX_L DevCol& col = cols[c];
+        const uint32_t dst = uint32_t(uint64_t(excl) >> (32 * h));
+        const uint32_t len = uint32_t(h ? len2 : len1);
+        const uint64_t base = h ? base2 : base1;
+        if (mine) {
+          *gp(col.offsets + row0 + t) = int64_t(base + dst);
+          T.rec[c * TR + t].dst = dst;
+          if (len && !direct) {
+            // chunk k of the window's output begins at window byte 16 k - head (head: the
+            // window's misalignment); this sample holds the first byte of chunks [k0, k1)
+            const uint32_t hd = uint32_t((reinterpret_cast<uint64_t>(col.data) + base) & 15);
+            const uint32_t k0 = dst == 0 ? 0u : (dst + hd + 15) >> 4;
+            const uint32_t k1 = (dst + len + hd + 15) >> 4;
+            MDSX_L uint8_t* mp = T.map + size_t(col.var_index) * map_len;
+            for (uint32_t k = k0; k < k1; ++k) mp[k] = uint8_t(t);
+          }
+        }
+        if (t == 0) {
+          const uint32_t tot = uint32_t(uint64_t(total) >> (32 * h));
+          s_wbase[c] = base;
+          s_wlen[c] = tot;
+          s_base[c] = base + tot;
+        }
       }
-      rel += len;
+      c0 = pair ? c2 + 1 : c1 + 1;
+    }
+    if (direct && t == ga && ok) {  // copied by the huge-row kernel after this one
+      uint32_t* count = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(a.status) +
+                                                    kHugeCountOffset);
+      const uint32_t slot = atomicAdd(count, 1u);
+      a.src_abs[slot] = (uint64_t(tile) << 32) | uint32_t(t);
     }
     __syncthreads();
 
-    // ---- 4. every column, destination-major per sample; 5. UTF-8
-    for (int c = 0; c < ncols; ++c) {
-      const MDSX_L DevCol& col = cols[c];
-      if (s_skip[c]) continue;  // block-uniform
-      const uint64_t data = reinterpret_cast<uint64_t>(col.data);
-      const int base = c * TR;
-      const bool utf8 = col.kind == MDSX_KIND_STR && col.flags != nullptr;
-      // the window's output range of the column
-      const uint64_t wbeg = data + T.dst[base + ga];
-      const uint64_t wend = data + T.dst[base + gb - 1] + T.len[base + gb - 1];
-      if (direct) {  // one sample larger than the stage: copied from HBM by the four waves
-        const uint32_t len = T.len[base + ga];
-        if (len == 0) continue;  // block-uniform
-        const uint8_t* src = v.shard + s_bdir + T.src[base + ga];
-        uint8_t* out = reinterpret_cast<uint8_t*>(data + T.dst[base + ga]);
-        if (utf8) {  // one wave copies and validates
-          if (wave == 0) {
-            const bool bad = wave_copy<true, 2, kNT>(src, out, len, lane);
-            if (lane == 0) *gp(col.flags + row0 + ga) = bad ? 1 : 0;
+    // ---- 4. every column, output-chunk-parallel, str pieces checked on the way
+    if (!direct) {
+      for (int c = 0; c < ncols; ++c) {
+        const MDSX_L DevCol& col = cols[c];
+        if (s_skip[c]) continue;  // block-uniform
+        const int base = c * TR;
+        // (measurement only, MDSX_TUNE sdbg: 1 no UTF-8 check, 2 no copy, 16 no stores)
+        const bool utf8 = col.kind == MDSX_KIND_STR && col.flags != nullptr && !(a.stage_debug & 1);
+        const uint64_t wout = reinterpret_cast<uint64_t>(col.data) + s_wbase[c];
+        const uint32_t wlen = s_wlen[c];
+        const uint64_t D0 = wout & ~uint64_t(15);
+        const int32_t hd = int32_t(wout - D0);
+        const uint32_t nch = uint32_t((uint64_t(hd) + wlen + 15) >> 4);
+        const uint32_t rb = col.var_index >= 0 ? 0u : col.row_bytes;
+        const MDSX_L uint8_t* mp = T.map + size_t(col.var_index >= 0 ? col.var_index : 0) * map_len;
+        MDSX_L uint32_t* bad = T.bad + c * 8;
+        for (uint32_t k = uint32_t(t); k < (a.stage_debug & 2 ? 0u : nch); k += kRowsBlock) {
+          const int32_t P0 = int32_t(k * 16) - hd;  // window output byte of the chunk's byte 0
+          int32_t pos = max(P0, 0);
+          const int32_t end = min(P0 + 16, int32_t(wlen));
+          const int r = rb ? ga + int(uint32_t(pos) / rb) : int(mp[k]);
+          // the common chunk: one value (A) or two (A, then B from byte sB), straight-line
+          const RowsRec qa = T.rec[base + r];
+          const int32_t dsA = int32_t(qa.dst), deA = dsA + int32_t(qa.len);
+          const lds_u8* pa = stage + (int32_t(qa.src) - dsA + P0);
+          uint4 val = lds_read16(pa);
+          const int32_t hiA = min(end, deA);
+          bool simple = deA > pos;  // (a fixed column's failed sample: no bytes)
+          uint32_t sB = 16;
+          int32_t deL = deA;  // end of the chunk's last value
+          if (simple && hiA < end) {
+            const RowsRec qb = T.rec[base + r + 1];
+            const int32_t dsB = int32_t(qb.dst), deB = dsB + int32_t(qb.len);
+            simple = dsB == hiA && deB >= end;
+            if (simple) {
+              const uint4 vb = lds_read16(stage + (int32_t(qb.src) - dsB + P0));
+              sB = uint32_t(hiA - P0);
+              const uint4 m = byte_mask(0, sB);
+              val = make_uint4((val.x & m.x) | (vb.x & ~m.x), (val.y & m.y) | (vb.y & ~m.y),
+                               (val.z & m.z) | (vb.z & ~m.z), (val.w & m.w) | (vb.w & ~m.w));
+              deL = deB;
+            }
           }
-          continue;
-        }
-        // quarter w: output bytes [q_w, q_w+1), split at 16-byte-aligned output addresses
-        const uint64_t D0 = reinterpret_cast<uint64_t>(out);
-        const uint64_t per = (((uint64_t(len) + 3) / 4) + 15) & ~uint64_t(15);
-        uint64_t q0 = wave == 0 ? 0 : ((D0 + per * uint64_t(wave)) & ~uint64_t(15)) - D0;
-        uint64_t q1 = wave == 3 ? len : ((D0 + per * uint64_t(wave + 1)) & ~uint64_t(15)) - D0;
-        q0 = std::min<uint64_t>(q0, len);
-        q1 = std::min<uint64_t>(std::max(q1, q0), len);
-        if (q1 > q0) wave_copy<false, 4, kNT>(src + q0, out + q0, q1 - q0, lane);
-        continue;
-      }
-      if (mine && T.len[base + t]) {
-        const uint32_t len = T.len[base + t];
-        const uint64_t ds = data + T.dst[base + t];
-        const uint64_t de = ds + len;
-        const uint32_t sp = T.src[base + t];
-        // the chunk holding the window's first byte, shared with the previous window / tile
-        if ((ds & 15) && ds == wbeg) {
-          const uint64_t D = ds & ~uint64_t(15);
-          const uint4 val = assemble(stage, T, base, t, gb, data, D, uint32_t(ds - D));
-          store_bytes(D, val, uint32_t(ds - D), uint32_t(min(D + 16, wend) - D));
-        }
-        // the chunks whose first byte is one of this sample's
-        for (uint64_t D = (ds + 15) & ~uint64_t(15); D < de; D += 16) {
-          uint4 val;
-          if (D + 16 <= de) {
-            val = lds_read16(stage + sp + uint32_t(D - ds));
+          if (simple) {
+            if (utf8) {
+              // the chunk's bytes (others zero), A's dword before the chunk (bytes before A's
+              // start zero); each value checked in its own context (utf8_chunk_err2); A's end at
+              // sB and a value ending at the chunk's end checked for an open sequence
+              const uint4 X = (pos > P0 || end < P0 + 16)
+                                  ? keep_bytes(val, uint32_t(pos - P0), uint32_t(end - P0))
+                                  : val;
+              uint32_t pw = 0;
+              if (pos > dsA) {
+                pw = lds_u32(pa + (pos - P0) - 4);
+                const int32_t nv = pos - dsA;  // A's bytes before the chunk
+                if (nv < 4) pw &= ~((1u << (8 * (4 - nv))) - 1u);
+              }
+              uint32_t e = utf8_chunk_err2(X, pw, sB);
+              if (sB < 16 && utf8_open_at(X, pw, sB)) e |= 1u;
+              if (end == P0 + 16 && end == deL) {
+                if (sB < 16) e |= utf8_open_at(keep_bytes(X, sB, 16), 0, 16) ? 2u : 0u;
+                else e |= utf8_open_at(X, pw, 16) ? 1u : 0u;
+              }
+              if (e & 1u) atomicOr(&bad[r >> 5], 1u << (r & 31));
+              if (e & 2u) atomicOr(&bad[(r + 1) >> 5], 1u << ((r + 1) & 31));
+            }
           } else {
-            val = assemble(stage, T, base, t, gb, data, D, 0);
+            // three or more values, an empty value, or a gap (a fixed column's failed sample
+            // leaves zeros): piece by piece
+            val = make_uint4(0, 0, 0, 0);
+            for (int rr = r; rr < gb && pos < end; ++rr) {
+              const RowsRec q = T.rec[base + rr];
+              const int32_t ds = int32_t(q.dst);
+              const int32_t de = ds + int32_t(q.len);
+              if (de <= pos) continue;  // a sample with no bytes in this column
+              if (ds >= end) break;
+              const int32_t lo = max(pos, ds), hi = min(end, de);
+              const lds_u8* p = stage + (int32_t(q.src) - ds + P0);
+              const uint4 v = lds_read16(p);
+              const uint4 pv = keep_bytes(v, uint32_t(lo - P0), uint32_t(hi - P0));
+              val = make_uint4(val.x | pv.x, val.y | pv.y, val.z | pv.z, val.w | pv.w);
+              if (utf8) {
+                uint32_t pw = 0;
+                if (lo > ds) {
+                  pw = lds_u32(p + (lo - P0) - 4);
+                  const int32_t nv = lo - ds;
+                  if (nv < 4) pw &= ~((1u << (8 * (4 - nv))) - 1u);
+                }
+                if ((utf8_chunk_err2(pv, pw, 16) & 1u) ||
+                    (hi == de && hi == P0 + 16 && utf8_open_at(pv, pw, 16)))
+                  atomicOr(&bad[rr >> 5], 1u << (rr & 31));
+              }
+              pos = hi;
+            }
           }
-          if (D + 16 <= wend) st16<kNT>(D, val);
-          else store_bytes(D, val, 0, uint32_t(wend - D));
+          const uint64_t D = D0 + 16ull * k;
+          if ((a.stage_debug & 16) && val.x != 0x9e3779b9u) continue;
+          if (P0 >= 0 && P0 + 16 <= int32_t(wlen)) st16<kNT>(D, val);
+          else store_bytes(D, val, uint32_t(max(P0, 0) - P0), uint32_t(end - P0));
         }
       }
-      if (utf8 && mine) {
-        bool bad = false;
-        const uint32_t len = T.len[base + t];
-        const uint32_t sp = T.src[base + t];
-        uint32_t pw = 0;
-        for (uint32_t k = 0; k < len; k += 16) {
-          uint4 vv = lds_read16(stage + sp + k);
-          if (k + 16 > len) vv = keep_range(vv, 0, 0, len - k);
-          bad |= utf8_chunk_bad(vv, pw, k + 16 >= len);
-          pw = vv.w;
-        }
-        *gp(col.flags + row0 + t) = bad ? 1 : 0;
+      __syncthreads();  // every piece's UTF-8 mark is in
+    }
+    // ---- 5. flags (a sample listed for the huge-row kernel: set there when its value fails)
+    if (mine) {
+      for (int c = 0; c < ncols; ++c) {
+        const MDSX_L DevCol& col = cols[c];
+        if (col.kind == MDSX_KIND_STR && col.flags != nullptr && !s_skip[c])
+          *gp(col.flags + row0 + t) = uint8_t((T.bad[c * 8 + (t >> 5)] >> (t & 31)) & 1u);
       }
     }
     ga = gb;
@@ -300,24 +416,32 @@ uint32_t rows_tile_rows_limit() { return kRowsBlock; }
 int launch_rows_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
   if (a.tile_rows > kRowsBlock)
     return mdsx::fail(MDSX_E_ARG, "mdsx: row-parallel decode tiles hold at most 256 rows");
-  const size_t lds = rows_lds_bytes(a.rows_bytes, a.tile_rows, a.ncols);
-#define MDSX_ROWS_CASE(NT)                                                                   \
-  if (bool(plan->rows_nt) == NT) {                                                           \
-    if (lds > 64 * 1024) {                                                                   \
-      const int rc = hip_check(                                                              \
-          hipFuncSetAttribute(reinterpret_cast<const void*>(rows_decode_kernel<NT>),         \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)),         \
-          "hipFuncSetAttribute");                                                            \
-      if (rc != MDSX_OK) return rc;                                                          \
-    }                                                                                        \
-    mdsx::set_last_kernel("rows_decode_kernel<" #NT ">");                                   \
-    hipLaunchKernelGGL((rows_decode_kernel<NT>), dim3(a.ntiles), dim3(kRowsBlock), lds, s, a); \
-    return hip_check(hipGetLastError(), "rows_decode_kernel launch");                        \
+  // the huge-row list (samples larger than the stage) starts empty
+  int rc = hip_check(hipMemsetAsync(reinterpret_cast<uint8_t*>(a.status) + kHugeCountOffset, 0,
+                                    4, s),
+                     "hipMemsetAsync");
+  if (rc != MDSX_OK) return rc;
+  const size_t lds = rows_lds_bytes(a.rows_bytes, a.tile_rows, a.ncols, a.nvar);
+  if (lds > 160 * 1024)
+    return mdsx::fail(MDSX_E_ARG, "mdsx: row-parallel decode stage and tables exceed 160 KiB of LDS");
+  const bool nt = plan->rows_nt != 0;
+  const void* fn = nt ? reinterpret_cast<const void*>(rows_decode_kernel<true>)
+                      : reinterpret_cast<const void*>(rows_decode_kernel<false>);
+  if (lds > 64 * 1024) {
+    rc = hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)),
+                   "hipFuncSetAttribute");
+    if (rc != MDSX_OK) return rc;
   }
-  MDSX_ROWS_CASE(true)
-  MDSX_ROWS_CASE(false)
-#undef MDSX_ROWS_CASE
-  return MDSX_E_ARG;
+  if (nt) {
+    mdsx::set_last_kernel("rows_decode_kernel<true>");
+    hipLaunchKernelGGL((rows_decode_kernel<true>), dim3(a.ntiles), dim3(kRowsBlock), lds, s, a);
+  } else {
+    mdsx::set_last_kernel("rows_decode_kernel<false>");
+    hipLaunchKernelGGL((rows_decode_kernel<false>), dim3(a.ntiles), dim3(kRowsBlock), lds, s, a);
+  }
+  rc = hip_check(hipGetLastError(), "rows_decode_kernel launch");
+  if (rc != MDSX_OK) return rc;
+  return launch_huge_rows(a, nt, s);
 }
 
 }  // namespace mdsx_kernels

@@ -418,6 +418,7 @@ __device__ __forceinline__ void fail_row(const DevArgs& a, const TileDesc& td, c
 // fit counts zero.
 __global__ __launch_bounds__(kBlock) void stage_totals_kernel(const DevArgs a) {
   __shared__ int64_t s_part[kBlock / 64][MDSX_MAX_COLUMNS];
+  __shared__ uint32_t s_bad[kBlock / 64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int TR = a.tile_rows;
   const uint32_t tile = blockIdx.x * uint32_t(kBlock / TR) + uint32_t(t / TR);
@@ -465,12 +466,23 @@ __global__ __launch_bounds__(kBlock) void stage_totals_kernel(const DevArgs a) {
       }
     }
   }
-  if (a.run_slots && TR < 64) {  // the streaming decode's run records (its tiles: <= 32 rows)
+  // the run records of the streaming decode (tiles <= 32 rows) and the row-parallel decode
+  if ((a.run_slots && TR < 64) || a.rows_bytes) {
     const uint64_t bad = __ballot(range_bad);
-    const uint64_t seg = ((1ull << TR) - 1) << (lane & ~(TR - 1));  // this tile's lanes
+    bool tile_bad;
+    if (TR <= 64) {
+      const uint64_t seg = TR == 64 ? ~0ull : ((1ull << TR) - 1) << (lane & ~(TR - 1));
+      tile_bad = (bad & seg) != 0;  // this tile's lanes
+    } else {  // a tile spans TR / 64 waves
+      if (lane == 0) s_bad[wave] = bad != 0;
+      __syncthreads();
+      tile_bad = false;
+      for (int w = wave & ~(TR / 64 - 1); w < (wave & ~(TR / 64 - 1)) + TR / 64; ++w)
+        tile_bad = tile_bad || s_bad[w];
+    }
     if (tile_ok && t % TR == 0) {
       TileRun r;
-      const bool fast = v.table_ok && v.nrows > 0 && (bad & seg) == 0;
+      const bool fast = v.table_ok && v.nrows > 0 && !tile_bad;
       r.fast = fast ? 1 : 0;
       r.stream = v.d.offset + (fast ? v.offs[v.r0] : 0u);
       r.bytes = fast ? v.offs[v.r0 + v.nrows] - v.offs[v.r0] : 0u;
@@ -479,7 +491,7 @@ __global__ __launch_bounds__(kBlock) void stage_totals_kernel(const DevArgs a) {
       r.shard = v.shard_idx;
       r.r0 = v.r0;
       r.nrows = uint16_t(v.nrows);
-      r.reserved = 0;
+      r.shard_off = v.d.offset;
       a.tile_run[tile] = r;
       // header written by encode_joint_shard (mds/writer.py:133-144): u32 N, then N + 1 offsets
       if (tile == v.d.tile0 &&
@@ -787,22 +799,25 @@ int launch_stage_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) 
     if (rc != MDSX_OK) return rc;
   }
   const unsigned grid = (a.ntiles + a.stage_tiles - 1) / a.stage_tiles;
-  // huge rows: one workgroup each, 1024 at a time (usually none)
-  const unsigned hgrid = unsigned(std::min<uint64_t>(a.ntiles, 1024));
   if (plan->nontemporal) {
     mdsx::set_last_kernel("stage_decode_kernel<true>");
     hipLaunchKernelGGL((stage_decode_kernel<true>), dim3(grid), dim3(kStageBlock), lds, s, a);
-    rc = hip_check(hipGetLastError(), "stage_decode_kernel launch");
-    if (rc == MDSX_OK)
-      hipLaunchKernelGGL((stage_huge_kernel<true>), dim3(hgrid), dim3(kBlock), 0, s, a);
   } else {
     mdsx::set_last_kernel("stage_decode_kernel<false>");
     hipLaunchKernelGGL((stage_decode_kernel<false>), dim3(grid), dim3(kStageBlock), lds, s, a);
-    rc = hip_check(hipGetLastError(), "stage_decode_kernel launch");
-    if (rc == MDSX_OK)
-      hipLaunchKernelGGL((stage_huge_kernel<false>), dim3(hgrid), dim3(kBlock), 0, s, a);
   }
+  rc = hip_check(hipGetLastError(), "stage_decode_kernel launch");
   if (rc != MDSX_OK) return rc;
+  return launch_huge_rows(a, plan->nontemporal != 0, s);
+}
+
+int launch_huge_rows(const DevArgs& a, bool nt, hipStream_t s) {
+  // one workgroup per listed row, 1024 at a time (usually none are listed)
+  const unsigned hgrid = unsigned(std::min<uint64_t>(a.ntiles, 1024));
+  if (nt)
+    hipLaunchKernelGGL((stage_huge_kernel<true>), dim3(hgrid), dim3(kBlock), 0, s, a);
+  else
+    hipLaunchKernelGGL((stage_huge_kernel<false>), dim3(hgrid), dim3(kBlock), 0, s, a);
   return hip_check(hipGetLastError(), "stage_huge_kernel launch");
 }
 
