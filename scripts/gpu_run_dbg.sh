@@ -6,7 +6,8 @@ OUT=gpurun_out/${TAG:-rundbg}
 timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "${PYTEST_K:-run}" > "$OUT/pytest_gpu.log" 2>&1 || { tail -60 "$OUT/pytest_gpu.log"; exit 1; }
 tail -1 "$OUT/pytest_gpu.log"
 V="${V:-tile=16 run=8 run=4 run=8,sdbg=16 run=8,sdbg=1,nocheck run=8,sdbg=2,nocheck run=8,sdbg=4,nocheck}"
-for cfg in "C" "C --blob 32,256 --chars 8,64" "C --blob 256,1024 --chars 64,256"; do
+IFS=';' read -r -a CFG_LIST <<< "${CFGS:-C;C --blob 32,256 --chars 8,64;C --blob 256,1024 --chars 64,256}"
+for cfg in "${CFG_LIST[@]}"; do
 timeout -k 10 300 python3 scripts/tune_decode.py --config $cfg --shards 16 --rounds 3 --variants $V > $OUT/t.json 2> $OUT/t.err || { tail -30 $OUT/t.err; exit 1; }
 python3 -c "
 import json; d = json.load(open('$OUT/t.json'))

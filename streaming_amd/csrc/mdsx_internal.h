@@ -50,10 +50,11 @@ struct mdsx_plan {
   int stage_fill = 70;  // percent of a stage buffer a tile's samples fill on average (tile sizing)
   int run_slots = 0;    // ragged plans: KiB of the streaming decode's per-wave LDS ring (0: off)
   int run_kb = 32;      // streaming decode: about this many KiB of samples per tile (tile sizing)
-  int64_t run_min = 2048;  // streaming decode for batches whose samples average >= this many bytes
+  int64_t run_min = 3072;  // streaming decode for batches whose samples average >= this many bytes
   int run_nt = 0;          // streaming decode: non-temporal ring loads and stores (measured: the
                            // temporal ones let L2 merge the partial stores at run edges)
-  int rows_kb = 0;         // row-parallel decode of short samples: LDS stage in KiB (0: off)
+  int rows_kb = 0;         // row-parallel decode of shorter samples: LDS stage in KiB (0: off,
+                           // -1: sized per batch, rows_tile_rows / rows_stage_bytes)
   int rows_nt = 0;         // row-parallel decode: non-temporal loads and stores
   int gather_chunks = 2;  // 16-byte chunks per lane in the ragged gather (tile = 4 KiB x this)
   int gather_min = 256;   // ragged columns averaging fewer bytes per row use the gather kernel
@@ -65,8 +66,8 @@ struct mdsx_plan {
 
 // Whether a batch of `bytes` shard bytes and `rows` samples decodes through the streaming decode
 // (mdsx_run.hip): ragged plans whose samples average at least run_min bytes (config C's 4.4 KB
-// samples: 4.76 vs 4.70 TB/s, 1.02x vs 1.15x traffic; short and medium rows stay on the
-// register decode, measured 2x and 1.3x faster there).
+// samples: 4.2 TB/s there vs 3.4 through the row-parallel decode; at 1.9 KB the row-parallel
+// decode leads, 2.85 vs 2.26).
 inline bool use_run_decode(const mdsx_plan* p, uint64_t bytes, uint64_t rows) {
   return p->nvar > 0 && p->run_slots > 0 && rows > 0 && bytes / rows >= uint64_t(p->run_min);
 }
@@ -74,5 +75,43 @@ inline bool use_run_decode(const mdsx_plan* p, uint64_t bytes, uint64_t rows) {
 // Whether a ragged batch of shorter samples decodes through the row-parallel decode
 // (mdsx_rows.hip).
 inline bool use_rows_decode(const mdsx_plan* p, uint64_t bytes, uint64_t rows) {
-  return p->nvar > 0 && p->rows_kb > 0 && rows > 0 && !use_run_decode(p, bytes, rows);
+  return p->nvar > 0 && p->rows_kb != 0 && rows > 0 && !use_run_decode(p, bytes, rows);
+}
+
+// Row-parallel decode sizing. A workgroup's LDS: the stage, [ncols][tile rows] 16-byte value
+// records, UTF-8 marks, one chunk map per ragged column, and the kernel's static arrays.
+inline uint64_t rows_lds_bytes_est(const mdsx_plan* p, uint64_t stage, uint64_t tr) {
+  return 192 + stage + tr * uint64_t(p->ncols) * 16 + uint64_t(p->ncols) * 32 +
+         uint64_t(p->nvar) * (stage / 16 + 4) + 4352;
+}
+
+// The stage a tile of tr samples of per_row bytes needs: 9/8 of its average bytes plus 1 KiB
+// (4..96 KiB; a tile that does not fit is decoded in windows).
+inline uint64_t rows_auto_stage(uint64_t per_row, uint64_t tr) {
+  const uint64_t kb = (tr * per_row * 9 / 8 + 1023) / 1024 + 1;
+  return (kb < 4 ? 4 : kb > 96 ? 96 : kb) * 1024;
+}
+
+// Rows per tile: the largest power of two (<= 256) whose samples fill at most 8/9 of the target
+// stage -- rows_kb, or by default 20 KiB for samples under 512 bytes (per-sample work dominates:
+// five workgroups per CU) and 40 KiB above (three workgroups of larger tiles; measured)
+// -- with the workgroup's LDS within the CU's 160 KiB.
+inline int rows_tile_rows(const mdsx_plan* p, uint64_t per_row) {
+  if (per_row == 0) per_row = 1;
+  const uint64_t target = p->rows_kb > 0 ? uint64_t(p->rows_kb) * 1024
+                                         : (per_row < 512 ? 20 : 40) * 1024ull;
+  int tr = 1;
+  while (tr < 256) {
+    const uint64_t t2 = uint64_t(tr) * 2;
+    const uint64_t stage = p->rows_kb > 0 ? target : rows_auto_stage(per_row, t2);
+    if (t2 * per_row * 9 > target * 8 || rows_lds_bytes_est(p, stage, t2) > 160 * 1024) break;
+    tr = int(t2);
+  }
+  return tr;
+}
+
+// The stage of a batch decoded in tiles of tr rows.
+inline uint32_t rows_stage_bytes(const mdsx_plan* p, uint64_t per_row, int tr) {
+  return p->rows_kb > 0 ? uint32_t(p->rows_kb) * 1024u
+                        : uint32_t(rows_auto_stage(per_row ? per_row : 1, uint64_t(tr)));
 }

@@ -873,7 +873,13 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   a->stage_debug = uint32_t(plan->stage_debug);
   a->run_slots = use_run_decode(plan, b->bytes, b->rows) ? uint32_t(plan->run_slots) : 0u;
   if (a->run_slots) a->stage_bytes = 0;  // the streaming decode takes precedence
-  a->rows_bytes = use_rows_decode(plan, b->bytes, b->rows) ? uint32_t(plan->rows_kb) * 1024u : 0u;
+  a->rows_bytes = use_rows_decode(plan, b->bytes, b->rows)
+                      ? rows_stage_bytes(plan, b->bytes / b->rows, tr)
+                      : 0u;
+  // (a batch tiled for another decode, too wide for the row-parallel workgroup's LDS: the register
+  // decode)
+  if (a->rows_bytes && rows_lds_bytes_est(plan, a->rows_bytes, uint64_t(tr)) > 160 * 1024)
+    a->rows_bytes = 0;
   if (a->rows_bytes) a->stage_bytes = 0;
   if (a->run_slots && tr > 32)
     return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode tiles hold at most 32 rows");

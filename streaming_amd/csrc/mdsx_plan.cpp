@@ -215,7 +215,7 @@ void apply_tuning(mdsx_plan* p) {
       p->run_min = v;
     } else if (key == "rnt") {
       p->run_nt = v ? 1 : 0;
-    } else if (key == "rows" && v >= 0 && v <= 96) {
+    } else if (key == "rows" && v >= -1 && v <= 96) {
       p->rows_kb = int(v);
     } else if (key == "rownt") {
       p->rows_nt = v ? 1 : 0;
@@ -327,6 +327,9 @@ int mdsx_plan_create(const char* const* encodings, const int64_t* column_sizes, 
   // Ragged batches of long samples decode through the streaming decode (mdsx_run.hip, 4 KiB ring
   // per wave): every shard byte read once, whole-chunk stores (use_run_decode).
   p->run_slots = p->nvar > 0 ? 4 : 0;
+  // ... and shorter samples through the row-parallel decode (mdsx_rows.hip), its tiles and stage
+  // sized per batch (rows_tile_rows).
+  p->rows_kb = p->nvar > 0 ? -1 : 0;
   p->stage_fill = 70;
   apply_tuning(p);
   *out = p;
@@ -350,21 +353,7 @@ int mdsx_plan_tile_rows_for(const mdsx_plan* plan, uint64_t shard_bytes, uint64_
     while (tr < 32 && uint64_t(tr) * 2 * per_row <= uint64_t(plan->run_kb) * 1024) tr *= 2;
     return tr;
   }
-  if (use_rows_decode(plan, shard_bytes, rows)) {
-    // row-parallel decode: samples filling at most 8/9 of the LDS stage on average (a tile of
-    // longer samples is decoded in windows), 1..256 rows
-    const uint64_t per_row = std::max<uint64_t>(1, shard_bytes / rows);
-    int tr = 1;
-    const uint64_t cap = uint64_t(plan->rows_kb) * 1024;
-    // the workgroup's LDS (mdsx_rows.hip: stage, per-column tables, marks, chunk maps) <= 160 KiB
-    auto lds = [&](uint64_t r) {
-      return 192 + cap + r * uint64_t(plan->ncols) * 16 + uint64_t(plan->ncols) * 32 +
-             uint64_t(plan->nvar) * (cap / 16 + 4);
-    };
-    while (tr < 256 && uint64_t(tr) * 2 * per_row * 9 <= cap * 8 && lds(uint64_t(tr) * 2) <= 160 * 1024)
-      tr *= 2;
-    return tr;
-  }
+  if (use_rows_decode(plan, shard_bytes, rows)) return rows_tile_rows(plan, shard_bytes / rows);
   if (plan->nvar == 0 || plan->stage_kb == 0 || rows == 0) return plan->tile_rows;
   const uint64_t target = uint64_t(plan->stage_kb) * 1024 * uint64_t(plan->stage_fill) / 100;
   const uint64_t per_row = std::max<uint64_t>(1, shard_bytes / rows);

@@ -112,20 +112,28 @@ def test_too_many_columns():
 
 
 def test_tile_rows_for_sizes_ragged_tiles_to_the_decode(monkeypatch):
-    """Ragged plans: batches of long samples (>= 2 KiB on average) go to the streaming decode,
-    whose tiles hold 16-32 KiB of samples (1..32 rows); shorter samples keep the register
-    decode's 32-row tiles; the staged decode (opt-in) sizes tiles to ~70 % of its 24 KiB stage;
-    all-fixed plans: the plan's tile size whatever the batch."""
+    """Ragged plans: batches of long samples (>= 3 KiB on average) go to the streaming decode,
+    whose tiles hold 16-32 KiB of samples (1..32 rows); shorter samples to the row-parallel
+    decode, whose tiles fill at most 8/9 of a 20 KiB (samples < 512 B) or 40 KiB stage (1..256
+    rows, the workgroup's LDS within 160 KiB); the staged decode (opt-in) sizes tiles to ~70 % of
+    its 24 KiB stage; all-fixed plans: the plan's tile size whatever the batch."""
     from streaming_amd.decoder import Plan
     c = Plan(['b', 'n', 's'], ['bytes', 'int', 'str'], [None, 8, None])
-    assert c.tile_rows_for(1 << 26, (1 << 26) // 100) == 32  # 100-byte samples: register decode
-    assert c.tile_rows_for(1 << 26, (1 << 26) // 2000) == 32
+    assert c.tile_rows_for(1 << 26, (1 << 26) // 100) == 128  # 100-byte samples: row-parallel
+    assert c.tile_rows_for(1 << 26, (1 << 26) // 50) == 256
+    assert c.tile_rows_for(1 << 26, (1 << 26) // 250) == 64
+    assert c.tile_rows_for(1 << 26, (1 << 26) // 1000) == 32
+    assert c.tile_rows_for(1 << 26, (1 << 26) // 2000) == 16
     assert c.tile_rows_for(1 << 26, 15_700) == 4  # ~4.3 KB samples: streaming, 4-row tiles
     assert c.tile_rows_for(1 << 26, (1 << 26) // 2048) == 16
     assert c.tile_rows_for(1 << 26, 10) == 1  # 6.7 MB samples: one per tile
+    wide = Plan([f'c{i:02d}' for i in range(64)], ['str'] * 64, [None] * 64)
+    assert wide.tile_rows_for(1 << 26, 1 << 20) == 64  # 64 columns: the tables bound the tile
+    monkeypatch.setenv('MDSX_TUNE', 'rows=18')
+    assert Plan(['b'], ['bytes'], [None]).tile_rows_for(1 << 26, (1 << 26) // 100) == 128
     monkeypatch.setenv('MDSX_TUNE', 'run=4,rkb=256')
     assert Plan(['b'], ['bytes'], [None]).tile_rows_for(1 << 26, 15_700) == 32
-    monkeypatch.setenv('MDSX_TUNE', 'stage=24,run=0')
+    monkeypatch.setenv('MDSX_TUNE', 'stage=24,run=0,rows=0')
     c = Plan(['b', 'n', 's'], ['bytes', 'int', 'str'], [None, 8, None])
     assert c.tile_rows_for(1 << 26, 15_700) == 4  # ~4.3 KB rows: 4-row tiles (~17 KB)
     assert c.tile_rows_for(1 << 26, (1 << 26) // 100) == 128  # 100-byte rows
