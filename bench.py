@@ -282,20 +282,20 @@ def cpu_baseline(args, config, synth, tmpdir):
 
 # ---------------------------------------------------------------------------------------------
 # measurement
-def lib_sha() -> str:
-    """sha256 (16 hex digits) of the libmdsx.so this run loads: profiles match on it."""
-    import hashlib
+def src_sha() -> str:
+    """sha256 (16 hex digits) of the sources the loaded libmdsx.so was built from (compiled into
+    ``mdsx_version()`` by streaming_amd/build.py): profiles match on it."""
     from streaming_amd import _native
-    with open(_native.lib_path, 'rb') as f:
-        return hashlib.sha256(f.read()).hexdigest()[:16]
+    version = _native.lib().mdsx_version().decode()
+    return version.rsplit(' src ', 1)[1] if ' src ' in version else 'unknown'
 
 
 def committed_traffic(key, kernel):
     """Per-launch HBM bytes of ``kernel`` on workload ``key`` from a committed rocprofv3 PMC
     summary (the L2's memory-side read and write requests by size, TCC_EA0_RDREQ_{32B,64B,128B}
     and TCC_EA0_WRREQ / _64B: scripts/pmc_summary.py), or (None, None) when no summary was taken
-    on this exact workload, kernel and library build."""
-    build = lib_sha()
+    on this exact workload, kernel and library sources."""
+    build = src_sha()
     for path in sorted(glob.glob(os.path.join(HERE, 'profiles', 'r*', '**', 'pmc_*.json'),
                                  recursive=True), reverse=True):
         try:
@@ -305,7 +305,7 @@ def committed_traffic(key, kernel):
             continue
         for e in summ.get('entries', []):
             if e.get('workload_key') == key and kernel and kernel in e.get('kernel', '') and \
-                    e.get('lib_sha') == build:
+                    e.get('src_sha') == build:
                 return e.get('hbm_traffic_bytes_per_launch'), os.path.relpath(path, HERE)
     return None, None
 
@@ -408,7 +408,7 @@ def measure(args, config, world, rank, dev, tmpdir):
             'frac': achieved / HBM_PEAK_GBS,
             'traffic': traffic,
             'traffic_source': traffic_src,
-            'lib_sha': lib_sha(),
+            'src_sha': src_sha(),
             'algorithmic_bytes_per_launch': R + W,
             'algorithmic': {'R': R, 'W': W},
             'kernel_ms': kern_s * 1e3,

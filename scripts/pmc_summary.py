@@ -74,7 +74,7 @@ def main(out):
         e = {
             'workload_key': key,
             'kernel': kernel,
-            'lib_sha': cfg['roofline'].get('lib_sha'),
+            'src_sha': cfg['roofline'].get('src_sha'),
             'algorithmic_bytes_per_launch': cfg['roofline']['algorithmic_bytes_per_launch'],
             'kernel_stats': [r for r in stats if kernel in r['Name']],
         }

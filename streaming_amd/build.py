@@ -6,6 +6,7 @@ One hipcc invocation over the HIP kernels and the host plan builder; the output 
 
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -32,17 +33,37 @@ def hipcc() -> str:
 FLAGS = ['-O3', '-std=c++17', '-fPIC', '-Wall', '-Wno-unused-function', '--no-offload-compress']
 
 
+def source_sha() -> str:
+    """sha256 (16 hex digits) of every source, header, the target and the flags of the library.
+
+    Compiled into the library (``mdsx_version()``), so a measurement names the code it ran: two
+    links of the same sources need not give identical bytes, the same sources give the same code.
+    """
+    h = hashlib.sha256()
+    for path in SOURCES + HEADERS + [os.path.join(ROOT, 'include', 'mdsx.h')]:
+        h.update(os.path.basename(path).encode() + b'\0')
+        with open(path, 'rb') as f:
+            h.update(f.read())
+    h.update(' '.join([ARCH, *FLAGS]).encode())
+    return h.hexdigest()[:16]
+
+
+def _defines() -> list[str]:
+    return [f'-DMDSX_SOURCE_SHA="{source_sha()}"']
+
+
 def command(output: str = OUTPUT, extra: tuple = ()) -> list[str]:
     """One hipcc invocation building the whole library (compile + link)."""
     return [
-        hipcc(), f'--offload-arch={ARCH}', *FLAGS, '-shared', '-I', os.path.join(ROOT, 'include'),
-        '-o', output, *extra, *SOURCES
+        hipcc(), f'--offload-arch={ARCH}', *FLAGS, *_defines(), '-shared', '-I',
+        os.path.join(ROOT, 'include'), '-o', output, *extra, *SOURCES
     ]
 
 
 def _compile(src: str, obj: str, verbose: bool) -> None:
-    cmd = [hipcc(), f'--offload-arch={ARCH}', *FLAGS, '-I', os.path.join(ROOT, 'include'), '-c',
-           src, '-o', obj]
+    defs = _defines() if src.endswith('mdsx_plan.cpp') else []
+    cmd = [hipcc(), f'--offload-arch={ARCH}', *FLAGS, *defs, '-I', os.path.join(ROOT, 'include'),
+           '-c', src, '-o', obj]
     if verbose:
         print(' '.join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

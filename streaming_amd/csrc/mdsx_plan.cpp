@@ -236,7 +236,12 @@ const char* mdsx_last_error(void) { return g_last_error.c_str(); }
 
 const char* mdsx_last_kernel(void) { return g_last_kernel.c_str(); }
 
-const char* mdsx_version(void) { return "mdsx 0.1.0 (gfx950)"; }
+#ifndef MDSX_SOURCE_SHA
+#define MDSX_SOURCE_SHA "unknown"
+#endif
+// The library's version and the sha256 of the sources it was built from (streaming_amd/build.py
+// source_sha): measurements key their profiles on it.
+const char* mdsx_version(void) { return "mdsx 0.1.0 (gfx950) src " MDSX_SOURCE_SHA; }
 
 int mdsx_plan_create(const char* const* encodings, const int64_t* column_sizes, int ncols,
                      mdsx_plan** out) {

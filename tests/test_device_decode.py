@@ -161,8 +161,9 @@ def test_config_b_full_size_round_trip():
     assert output_bytes(synth.plan, out) == 1_000_000 * 4100
 
 
-def test_config_c_full_shards_round_trip():
-    """BASELINE config C schema at full 64 MiB shard size (3 shards), vs the source columns."""
+def test_config_c_full_shards_round_trip(tmp_path):
+    """BASELINE config C schema at full 64 MiB shard size (3 shards), vs the source columns and,
+    on the first shard's first samples, vs the oracle reading the shard file."""
     shards, counts, src = var_c_shards(45_000, seed=5)
     assert len(counts) == 3 and counts[0] > 14_000
     names = ['b', 'n', 's']
@@ -177,8 +178,20 @@ def test_config_c_full_shards_round_trip():
     assert np.array_equal(s.offsets.cpu().numpy(), np.concatenate([[0], np.cumsum(src['s_len'])]))
     assert np.array_equal(s.values.cpu().numpy(), src['s_pool'])
     assert int(s.flags.sum()) == 0
-    # same result against the oracle on the first shard's first samples
     assert dec.rows == 45_000
+    # same result against the oracle on the first shard's first samples
+    (tmp_path / 'shard.00000.mds').write_bytes(shards[0])
+    info = {'column_names': names, 'column_encodings': ['bytes', 'int', 'str'],
+            'column_sizes': [None, 8, None], 'samples': counts[0],
+            'raw_data': {'basename': 'shard.00000.mds'}}
+    ref = mds_oracle.OracleMDSReader(str(tmp_path), None, info)
+    bo, so = b.offsets.cpu().numpy(), s.offsets.cpu().numpy()
+    bv, sv, nv = b.values.cpu().numpy(), s.values.cpu().numpy(), dec['n'].cpu().numpy()
+    for i in list(range(300)) + [counts[0] - 1]:
+        want = ref.get_item(i)
+        assert want['n'] == int(nv[i])
+        assert want['b'] == bv[bo[i]:bo[i + 1]].tobytes()
+        assert want['s'] == sv[so[i]:so[i + 1]].tobytes().decode('utf-8')
 
 
 def _random_dataset(tmp_path, seed):

@@ -32,6 +32,16 @@ def test_library_exports_every_declared_symbol():
     assert lib.mdsx_version().startswith(b'mdsx')
 
 
+def test_library_built_from_these_sources():
+    """The loaded library names the sources it was built from (bench.py keys profiles on it); a
+    stale build (sources edited since) fails here instead of being measured."""
+    from streaming_amd import build
+    if os.environ.get('MDSX_LIBRARY'):
+        pytest.skip('another build selected by MDSX_LIBRARY')
+    version = _native.lib().mdsx_version().decode()
+    assert version.endswith(' src ' + build.source_sha()), version
+
+
 def test_struct_layouts():
     assert ctypes.sizeof(_native.ShardDesc) == 32
     assert ctypes.sizeof(_native.ColumnOut) == 32
