@@ -218,6 +218,32 @@ int mdsx_gather_ragged_copy(const uint8_t* src_values, const int64_t* src_offset
                             int64_t* dst_offsets, uint8_t* dst_flags, void* d_workspace,
                             uint64_t workspace_bytes, void* stream);
 
+/* Multi-source gather: one batch over the decoded columns of many shards in one launch sequence
+ * per column, rows in the caller's order -- StreamingDataset.__iter__'s get_item over a worker's
+ * ids (dataset.py:1430-1473, 1237-1293), whose Spanner lookup (spanner.py:40-59) gives each id's
+ * shard and row. srcs: DEVICE array of nsrc sources (one decoded column of one shard each);
+ * idx: device int64[m], each source << MDSX_GATHER_SRC_SHIFT | row. Same workspace, status,
+ * scan/copy sequence and errors as the single-source calls above (an id whose source or row is
+ * out of range reports MDSX_E_BOUNDS). As there, a ragged column's copy reads the tile prefixes
+ * its scan left in the workspace: scan another column in between only on another workspace. */
+#define MDSX_GATHER_SRC_SHIFT 40
+typedef struct mdsx_gather_src {
+  const void* values;      /* fixed: rows x row_bytes; ragged: packed values                    */
+  const int64_t* offsets;  /* ragged: rows + 1 offsets into values; NULL for fixed columns      */
+  const uint8_t* flags;    /* str: per-row invalid-UTF-8 flags, or NULL                         */
+  uint64_t rows;
+} mdsx_gather_src;
+int mdsx_gather_fixed_multi(const mdsx_gather_src* srcs, uint32_t nsrc, uint64_t row_bytes,
+                            const int64_t* idx, uint64_t m, void* dst, void* d_workspace,
+                            uint64_t workspace_bytes, void* stream);
+int mdsx_gather_ragged_scan_multi(const mdsx_gather_src* srcs, uint32_t nsrc, const int64_t* idx,
+                                  uint64_t m, int64_t* dst_offsets, void* d_workspace,
+                                  uint64_t workspace_bytes, int64_t* d_total, void* stream);
+int mdsx_gather_ragged_copy_multi(const mdsx_gather_src* srcs, uint32_t nsrc, const int64_t* idx,
+                                  uint64_t m, uint8_t* dst_values, uint64_t dst_capacity,
+                                  int64_t* dst_offsets, uint8_t* dst_flags, void* d_workspace,
+                                  uint64_t workspace_bytes, void* stream);
+
 /* ---- dynamic ndarray columns ------------------------------------------------------------------
  * Header parse of NDArray.decode (encodings.py:270-305) over a decoded MDSX_KIND_NDARRAY column
  * (values with headers + offsets): per row the value dtype id (encodings.py:131-143; dtype_id

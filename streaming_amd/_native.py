@@ -40,6 +40,7 @@ KIND_NDARRAY = 3
 
 MAX_COLUMNS = 64
 BATCH_PAD = 256
+GATHER_SRC_SHIFT = 40  # MDSX_GATHER_SRC_SHIFT: multi-source gather ids are source << 40 | row
 
 # Every function include/mdsx.h declares (checked by tests/test_native_abi.py).
 EXPORTED_SYMBOLS = (
@@ -63,6 +64,9 @@ EXPORTED_SYMBOLS = (
     'mdsx_gather_fixed',
     'mdsx_gather_ragged_scan',
     'mdsx_gather_ragged_copy',
+    'mdsx_gather_fixed_multi',
+    'mdsx_gather_ragged_scan_multi',
+    'mdsx_gather_ragged_copy_multi',
     'mdsx_ndarray_meta',
     'mdsx_ndarray_shapes',
     'mdsx_plan_encode_tile_rows',
@@ -202,6 +206,14 @@ def _declare(handle: ctypes.CDLL) -> None:
     handle.mdsx_gather_ragged_copy.restype = c_int
     handle.mdsx_gather_ragged_copy.argtypes = [
         vp, vp, vp, c_u64, vp, c_u64, vp, c_u64, vp, vp, vp, c_u64, vp
+    ]
+    handle.mdsx_gather_fixed_multi.restype = c_int
+    handle.mdsx_gather_fixed_multi.argtypes = [vp, c_u32, c_u64, vp, c_u64, vp, vp, c_u64, vp]
+    handle.mdsx_gather_ragged_scan_multi.restype = c_int
+    handle.mdsx_gather_ragged_scan_multi.argtypes = [vp, c_u32, vp, c_u64, vp, vp, c_u64, vp, vp]
+    handle.mdsx_gather_ragged_copy_multi.restype = c_int
+    handle.mdsx_gather_ragged_copy_multi.argtypes = [
+        vp, c_u32, vp, c_u64, vp, c_u64, vp, vp, vp, c_u64, vp
     ]
 
 

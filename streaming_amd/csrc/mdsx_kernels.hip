@@ -977,10 +977,40 @@ __global__ __launch_bounds__(kBlock) void copy_probe_kernel(const uint4* __restr
 
 constexpr int kGatherRowTile = 256;  // rows of the output per workgroup
 
+// Where the rows come from. OneSrc: one decoded column, ids are its rows. MultiSrc: a device
+// table of decoded columns (one per shard a batch touches), ids are source << 40 | row -- a
+// batch over many shards in ONE launch sequence per column, rows in the caller's order (the
+// reference's Spanner lookup, spanner.py:40-59, done by the caller).
+struct OneSrc {
+  const uint8_t* vals;
+  const int64_t* off;
+  const uint8_t* flags;
+  uint64_t rows;
+  __device__ __forceinline__ bool resolve(int64_t id, mdsx_gather_src* g, uint64_t* r) const {
+    if (id < 0 || uint64_t(id) >= rows) return false;
+    g->values = vals;
+    g->offsets = off;
+    g->flags = flags;
+    *r = uint64_t(id);
+    return true;
+  }
+};
+
+struct MultiSrc {
+  const mdsx_gather_src* table;
+  uint32_t n;
+  __device__ __forceinline__ bool resolve(int64_t id, mdsx_gather_src* g, uint64_t* r) const {
+    const uint64_t s = uint64_t(id) >> MDSX_GATHER_SRC_SHIFT;
+    if (id < 0 || s >= n) return false;
+    *g = table[s];
+    *r = uint64_t(id) & ((uint64_t(1) << MDSX_GATHER_SRC_SHIFT) - 1);
+    return *r < g->rows;
+  }
+};
+
 // Fixed column: one output row per wave (rows > 16 bytes) or per lane (<= 16 bytes).
-template <bool kNT>
-__global__ __launch_bounds__(kBlock) void gather_fixed_kernel(const uint8_t* src, uint64_t nsrc,
-                                                              uint32_t row_bytes,
+template <bool kNT, class Src>
+__global__ __launch_bounds__(kBlock) void gather_fixed_kernel(const Src S, uint32_t row_bytes,
                                                               const int64_t* idx, uint64_t m,
                                                               uint8_t* dst, mdsx_status* st) {
   const uint64_t k0 = uint64_t(blockIdx.x) * kGatherRowTile;
@@ -988,13 +1018,14 @@ __global__ __launch_bounds__(kBlock) void gather_fixed_kernel(const uint8_t* src
   if (row_bytes <= uint32_t(kSmallMax)) {
     const uint64_t k = k0 + threadIdx.x;
     if (k < m) {
-      const int64_t r = idx[k];
-      if (r < 0 || uint64_t(r) >= nsrc) {
+      mdsx_gather_src g;
+      uint64_t r;
+      if (!S.resolve(idx[k], &g, &r)) {
         report(st, MDSX_E_BOUNDS, -1, int(k), -1);
       } else {
-        const MDSX_G uint8_t* p = gp(src + uint64_t(r) * row_bytes);  // both rows aligned to
-        MDSX_G uint8_t* q = gp(dst + k * row_bytes);  // row_bytes' power-of-two factor
-        switch (row_bytes) {
+        const MDSX_G uint8_t* p = gp(static_cast<const uint8_t*>(g.values) + r * row_bytes);
+        MDSX_G uint8_t* q = gp(dst + k * row_bytes);  // both rows aligned to row_bytes'
+        switch (row_bytes) {                          // power-of-two factor
           case 1: *q = *p; break;
           case 2: *(MDSX_G uint16_t*)q = *(const MDSX_G uint16_t*)p; break;
           case 4: *(MDSX_G uint32_t*)q = *(const MDSX_G uint32_t*)p; break;
@@ -1011,34 +1042,35 @@ __global__ __launch_bounds__(kBlock) void gather_fixed_kernel(const uint8_t* src
   for (int i = wave; i < kGatherRowTile; i += kBlock / 64) {
     const uint64_t k = k0 + i;
     if (k >= m) break;  // wave-uniform
-    const int64_t r = idx[k];
-    if (r < 0 || uint64_t(r) >= nsrc) {
+    mdsx_gather_src g;
+    uint64_t r;
+    if (!S.resolve(idx[k], &g, &r)) {
       if (lane == 0) report(st, MDSX_E_BOUNDS, -1, int(k), -1);
       continue;
     }
+    const uint8_t* src = static_cast<const uint8_t*>(g.values) + r * row_bytes;
     if (aligned)
-      wave_copy<false, 4, kNT, false>(src + uint64_t(r) * row_bytes, dst + k * row_bytes,
-                                      row_bytes, lane);
+      wave_copy<false, 4, kNT, false>(src, dst + k * row_bytes, row_bytes, lane);
     else
-      wave_copy<false, 4, kNT, true, true>(src + uint64_t(r) * row_bytes, dst + k * row_bytes,
-                                     row_bytes, lane);
+      wave_copy<false, 4, kNT, true, true>(src, dst + k * row_bytes, row_bytes, lane);
   }
 }
 
 // Ragged column, pass 1: selected lengths -> local exclusive offsets + per-tile totals.
-__global__ __launch_bounds__(kBlock) void gather_len_kernel(const int64_t* src_off, uint64_t nsrc,
-                                                            const int64_t* idx, uint64_t m,
-                                                            int64_t* dst_off, int64_t* tile_total,
-                                                            mdsx_status* st) {
+template <class Src>
+__global__ __launch_bounds__(kBlock) void gather_len_kernel(const Src S, const int64_t* idx,
+                                                            uint64_t m, int64_t* dst_off,
+                                                            int64_t* tile_total, mdsx_status* st) {
   __shared__ int64_t s_wsum[kBlock / 64];
   const uint64_t k = uint64_t(blockIdx.x) * kGatherRowTile + threadIdx.x;
   int64_t len = 0;
   if (k < m) {
-    const int64_t r = idx[k];
-    if (r < 0 || uint64_t(r) >= nsrc)
+    mdsx_gather_src g;
+    uint64_t r;
+    if (!S.resolve(idx[k], &g, &r))
       report(st, MDSX_E_BOUNDS, -1, int(k), -1);
     else
-      len = src_off[r + 1] - src_off[r];
+      len = g.offsets[r + 1] - g.offsets[r];
   }
   int64_t total;
   const int64_t excl = block_exclusive_scan(len, s_wsum, &total);
@@ -1068,13 +1100,12 @@ __global__ __launch_bounds__(kBlock) void scan_tile_totals_kernel(const int64_t*
 
 // Ragged column, pass 2: final offsets, flags, and the rows copied: one per wave, or (kGroup,
 // rows of a few hundred bytes) four per wave, one per 16-lane group.
-template <bool kNT, bool kGroup>
+template <bool kNT, bool kGroup, class Src>
 __global__ __launch_bounds__(kBlock) void gather_copy_kernel(
-    const uint8_t* src_vals, const int64_t* src_off, const uint8_t* src_flags, uint64_t nsrc,
-    const int64_t* idx, uint64_t m, uint8_t* dst_vals, uint64_t capacity, int64_t* dst_off,
-    uint8_t* dst_flags, const int64_t* tile_prefix, mdsx_status* st) {
+    const Src S, const int64_t* idx, uint64_t m, uint8_t* dst_vals, uint64_t capacity,
+    int64_t* dst_off, uint8_t* dst_flags, const int64_t* tile_prefix, mdsx_status* st) {
+  __shared__ const uint8_t* s_src[kGatherRowTile];
   __shared__ int64_t s_dst[kGatherRowTile];
-  __shared__ int64_t s_src[kGatherRowTile];
   __shared__ int64_t s_len[kGatherRowTile];
   const uint64_t k0 = uint64_t(blockIdx.x) * kGatherRowTile;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1085,15 +1116,16 @@ __global__ __launch_bounds__(kBlock) void gather_copy_kernel(
       const int64_t off = tile_prefix[blockIdx.x] + dst_off[k];
       dst_off[k] = off;
       s_dst[threadIdx.x] = off;
-      const int64_t r = idx[k];
-      if (r >= 0 && uint64_t(r) < nsrc) {
-        s_src[threadIdx.x] = src_off[r];
-        len = src_off[r + 1] - src_off[r];
+      mdsx_gather_src g;
+      uint64_t r;
+      if (S.resolve(idx[k], &g, &r)) {
+        s_src[threadIdx.x] = static_cast<const uint8_t*>(g.values) + g.offsets[r];
+        len = g.offsets[r + 1] - g.offsets[r];
         if (uint64_t(off + len) > capacity) {
           report(st, MDSX_E_CAPACITY, -1, int(k), -1);
           len = -1;
         }
-        if (dst_flags) dst_flags[k] = src_flags ? src_flags[r] : 0;
+        if (dst_flags) dst_flags[k] = g.flags ? g.flags[r] : 0;
       }
     }
     s_len[threadIdx.x] = len;
@@ -1106,8 +1138,7 @@ __global__ __launch_bounds__(kBlock) void gather_copy_kernel(
       if (k0 + r0 >= m) break;  // wave-uniform
       const int i = r0 + g;
       const bool live = k0 + i < m && s_len[i] > 0;
-      group_copy<2, kNT, true>(live ? src_vals + s_src[i] : src_vals,
-                               live ? dst_vals + s_dst[i] : dst_vals,
+      group_copy<2, kNT, true>(live ? s_src[i] : dst_vals, live ? dst_vals + s_dst[i] : dst_vals,
                                live ? uint64_t(s_len[i]) : 0, lane);
     }
   } else {
@@ -1115,8 +1146,7 @@ __global__ __launch_bounds__(kBlock) void gather_copy_kernel(
       if (k0 + i >= m) break;
       const int64_t len = s_len[i];
       if (len <= 0) continue;  // wave-uniform
-      wave_copy<false, 4, kNT, true, true>(src_vals + s_src[i], dst_vals + s_dst[i],
-                                           uint64_t(len), lane);
+      wave_copy<false, 4, kNT, true, true>(s_src[i], dst_vals + s_dst[i], uint64_t(len), lane);
     }
   }
 }
@@ -1414,37 +1444,40 @@ static int gather_ws(void* ws, uint64_t ws_bytes, uint64_t m, mdsx_status** st, 
   return MDSX_OK;
 }
 
-int mdsx_gather_fixed(const void* src, uint64_t src_rows, uint64_t row_bytes, const int64_t* idx,
-                      uint64_t m, void* dst, void* d_workspace, uint64_t workspace_bytes,
-                      void* stream) {
+extern "C++" {
+template <class Src>
+static int gather_fixed_launch(const Src S, uint64_t row_bytes, const int64_t* idx, uint64_t m,
+                               void* dst, void* d_workspace, uint64_t workspace_bytes,
+                               void* stream) {
   mdsx_status* st;
   int64_t *tt, *tp;
   int rc = gather_ws(d_workspace, workspace_bytes, m, &st, &tt, &tp);
   if (rc != MDSX_OK) return rc;
-  if (!src || !idx || !dst || row_bytes == 0 || row_bytes >= (uint64_t(1) << 32))
+  if (!idx || !dst || row_bytes == 0 || row_bytes >= (uint64_t(1) << 32))
     return mdsx::fail(MDSX_E_ARG, "mdsx_gather_fixed: bad argument");
   if (m == 0) return MDSX_OK;
   const unsigned grid = unsigned((m + kGatherRowTile - 1) / kGatherRowTile);
-  hipLaunchKernelGGL((gather_fixed_kernel<true>), dim3(grid), dim3(kBlock), 0,
-                     static_cast<hipStream_t>(stream), static_cast<const uint8_t*>(src), src_rows,
-                     uint32_t(row_bytes), idx, m, static_cast<uint8_t*>(dst), st);
+  hipLaunchKernelGGL((gather_fixed_kernel<true, Src>), dim3(grid), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), S, uint32_t(row_bytes), idx, m,
+                     static_cast<uint8_t*>(dst), st);
   return hip_check(hipGetLastError(), "gather_fixed_kernel launch");
 }
 
-int mdsx_gather_ragged_scan(const int64_t* src_offsets, uint64_t src_rows, const int64_t* idx,
-                            uint64_t m, int64_t* dst_offsets, void* d_workspace,
-                            uint64_t workspace_bytes, int64_t* d_total, void* stream) {
+template <class Src>
+static int gather_scan_launch(const Src S, const int64_t* idx, uint64_t m, int64_t* dst_offsets,
+                              void* d_workspace, uint64_t workspace_bytes, int64_t* d_total,
+                              void* stream) {
   mdsx_status* st;
   int64_t *tt, *tp;
   int rc = gather_ws(d_workspace, workspace_bytes, m, &st, &tt, &tp);
   if (rc != MDSX_OK) return rc;
-  if (!src_offsets || !dst_offsets || (m && !idx))
+  if (!dst_offsets || (m && !idx))
     return mdsx::fail(MDSX_E_ARG, "mdsx_gather_ragged_scan: bad argument");
   hipStream_t s = static_cast<hipStream_t>(stream);
   const unsigned tiles = unsigned((m + kGatherRowTile - 1) / kGatherRowTile);
   if (tiles) {
-    hipLaunchKernelGGL(gather_len_kernel, dim3(tiles), dim3(kBlock), 0, s, src_offsets, src_rows,
-                       idx, m, dst_offsets, tt, st);
+    hipLaunchKernelGGL((gather_len_kernel<Src>), dim3(tiles), dim3(kBlock), 0, s, S, idx, m,
+                       dst_offsets, tt, st);
     rc = hip_check(hipGetLastError(), "gather_len_kernel launch");
     if (rc != MDSX_OK) return rc;
   }
@@ -1453,30 +1486,86 @@ int mdsx_gather_ragged_scan(const int64_t* src_offsets, uint64_t src_rows, const
   return hip_check(hipGetLastError(), "scan_tile_totals_kernel launch");
 }
 
-int mdsx_gather_ragged_copy(const uint8_t* src_values, const int64_t* src_offsets,
-                            const uint8_t* src_flags, uint64_t src_rows, const int64_t* idx,
-                            uint64_t m, uint8_t* dst_values, uint64_t dst_capacity,
-                            int64_t* dst_offsets, uint8_t* dst_flags, void* d_workspace,
-                            uint64_t workspace_bytes, void* stream) {
+template <class Src>
+static int gather_copy_launch(const Src S, const int64_t* idx, uint64_t m, uint8_t* dst_values,
+                              uint64_t dst_capacity, int64_t* dst_offsets, uint8_t* dst_flags,
+                              void* d_workspace, uint64_t workspace_bytes, void* stream) {
   mdsx_status* st;
   int64_t *tt, *tp;
   int rc = gather_ws(d_workspace, workspace_bytes, m, &st, &tt, &tp);
   if (rc != MDSX_OK) return rc;
-  if (!src_offsets || !dst_offsets || (m && !idx) || (dst_capacity && (!dst_values || !src_values)))
+  if (!dst_offsets || (m && !idx) || (dst_capacity && !dst_values))
     return mdsx::fail(MDSX_E_ARG, "mdsx_gather_ragged_copy: bad argument");
   if (m == 0) return MDSX_OK;
   const unsigned tiles = unsigned((m + kGatherRowTile - 1) / kGatherRowTile);
   // rows averaging under 1 KiB: four per wave (as the decode's medium rows)
   const bool group = dst_capacity < uint64_t(1024) * m;
   if (group)
-    hipLaunchKernelGGL((gather_copy_kernel<true, true>), dim3(tiles), dim3(kBlock), 0,
-                       static_cast<hipStream_t>(stream), src_values, src_offsets, src_flags,
-                       src_rows, idx, m, dst_values, dst_capacity, dst_offsets, dst_flags, tp, st);
+    hipLaunchKernelGGL((gather_copy_kernel<true, true, Src>), dim3(tiles), dim3(kBlock), 0,
+                       static_cast<hipStream_t>(stream), S, idx, m, dst_values, dst_capacity,
+                       dst_offsets, dst_flags, tp, st);
   else
-    hipLaunchKernelGGL((gather_copy_kernel<true, false>), dim3(tiles), dim3(kBlock), 0,
-                       static_cast<hipStream_t>(stream), src_values, src_offsets, src_flags,
-                       src_rows, idx, m, dst_values, dst_capacity, dst_offsets, dst_flags, tp, st);
+    hipLaunchKernelGGL((gather_copy_kernel<true, false, Src>), dim3(tiles), dim3(kBlock), 0,
+                       static_cast<hipStream_t>(stream), S, idx, m, dst_values, dst_capacity,
+                       dst_offsets, dst_flags, tp, st);
   return hip_check(hipGetLastError(), "gather_copy_kernel launch");
+}
+
+}  // extern "C++"
+
+int mdsx_gather_fixed(const void* src, uint64_t src_rows, uint64_t row_bytes, const int64_t* idx,
+                      uint64_t m, void* dst, void* d_workspace, uint64_t workspace_bytes,
+                      void* stream) {
+  if (!src) return mdsx::fail(MDSX_E_ARG, "mdsx_gather_fixed: bad argument");
+  return gather_fixed_launch(OneSrc{static_cast<const uint8_t*>(src), nullptr, nullptr, src_rows},
+                             row_bytes, idx, m, dst, d_workspace, workspace_bytes, stream);
+}
+
+int mdsx_gather_ragged_scan(const int64_t* src_offsets, uint64_t src_rows, const int64_t* idx,
+                            uint64_t m, int64_t* dst_offsets, void* d_workspace,
+                            uint64_t workspace_bytes, int64_t* d_total, void* stream) {
+  if (!src_offsets) return mdsx::fail(MDSX_E_ARG, "mdsx_gather_ragged_scan: bad argument");
+  return gather_scan_launch(OneSrc{nullptr, src_offsets, nullptr, src_rows}, idx, m, dst_offsets,
+                            d_workspace, workspace_bytes, d_total, stream);
+}
+
+int mdsx_gather_ragged_copy(const uint8_t* src_values, const int64_t* src_offsets,
+                            const uint8_t* src_flags, uint64_t src_rows, const int64_t* idx,
+                            uint64_t m, uint8_t* dst_values, uint64_t dst_capacity,
+                            int64_t* dst_offsets, uint8_t* dst_flags, void* d_workspace,
+                            uint64_t workspace_bytes, void* stream) {
+  if (!src_offsets || (dst_capacity && !src_values))
+    return mdsx::fail(MDSX_E_ARG, "mdsx_gather_ragged_copy: bad argument");
+  return gather_copy_launch(OneSrc{src_values, src_offsets, src_flags, src_rows}, idx, m,
+                            dst_values, dst_capacity, dst_offsets, dst_flags, d_workspace,
+                            workspace_bytes, stream);
+}
+
+int mdsx_gather_fixed_multi(const mdsx_gather_src* srcs, uint32_t nsrc, uint64_t row_bytes,
+                            const int64_t* idx, uint64_t m, void* dst, void* d_workspace,
+                            uint64_t workspace_bytes, void* stream) {
+  if (!srcs || nsrc == 0) return mdsx::fail(MDSX_E_ARG, "mdsx_gather_fixed_multi: no sources");
+  return gather_fixed_launch(MultiSrc{srcs, nsrc}, row_bytes, idx, m, dst, d_workspace,
+                             workspace_bytes, stream);
+}
+
+int mdsx_gather_ragged_scan_multi(const mdsx_gather_src* srcs, uint32_t nsrc, const int64_t* idx,
+                                  uint64_t m, int64_t* dst_offsets, void* d_workspace,
+                                  uint64_t workspace_bytes, int64_t* d_total, void* stream) {
+  if (!srcs || nsrc == 0)
+    return mdsx::fail(MDSX_E_ARG, "mdsx_gather_ragged_scan_multi: no sources");
+  return gather_scan_launch(MultiSrc{srcs, nsrc}, idx, m, dst_offsets, d_workspace,
+                            workspace_bytes, d_total, stream);
+}
+
+int mdsx_gather_ragged_copy_multi(const mdsx_gather_src* srcs, uint32_t nsrc, const int64_t* idx,
+                                  uint64_t m, uint8_t* dst_values, uint64_t dst_capacity,
+                                  int64_t* dst_offsets, uint8_t* dst_flags, void* d_workspace,
+                                  uint64_t workspace_bytes, void* stream) {
+  if (!srcs || nsrc == 0)
+    return mdsx::fail(MDSX_E_ARG, "mdsx_gather_ragged_copy_multi: no sources");
+  return gather_copy_launch(MultiSrc{srcs, nsrc}, idx, m, dst_values, dst_capacity, dst_offsets,
+                            dst_flags, d_workspace, workspace_bytes, stream);
 }
 
 

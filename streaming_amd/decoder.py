@@ -420,6 +420,97 @@ class DecodedBatch:
         return DecodedBatch(out, m)
 
 
+def gather_sources(sources: Sequence[DecodedBatch], src: np.ndarray, rows: np.ndarray,
+                   check: bool = True) -> DecodedBatch:
+    """Output row k = row ``rows[k]`` of ``sources[src[k]]`` (decoded shards of one schema), for
+    every column in ONE launch sequence (``mdsx_gather_*_multi``): the device side of the
+    reference's per-sample ``get_item`` over a worker's ids across shards
+    (``dataset.py:1430-1473``; ``Spanner``, ``spanner.py:40-59``, gives ``src`` / ``rows``).
+    One host sync (the ragged totals that size the value buffers, read with the status)."""
+    if not sources:
+        raise ValueError('gather_sources: no sources')
+    lib = _native.lib()
+    src = np.asarray(src, np.int64).reshape(-1)
+    rows = np.asarray(rows, np.int64).reshape(-1)
+    if src.shape != rows.shape:
+        raise ValueError('gather_sources: src and rows differ in length')
+    m, nsrc = int(src.size), len(sources)
+    names = list(sources[0].columns)
+    first = sources[0].columns[names[0]]
+    dev = first.values.device if isinstance(first, RaggedColumn) else first.device
+    # one upload: [ncols][nsrc] mdsx_gather_src records, then the packed ids
+    table = np.zeros((len(names), nsrc, 4), np.uint64)
+    for j, b in enumerate(sources):
+        for c, name in enumerate(names):
+            col = b.columns[name]
+            if isinstance(col, RaggedColumn):
+                table[c, j] = (col.values.data_ptr() if col.values.numel() else 0,
+                               col.offsets.data_ptr(),
+                               col.flags.data_ptr() if col.flags is not None else 0, b.rows)
+            else:
+                table[c, j] = (col.data_ptr(), 0, 0, b.rows)
+    if m and (src.min() < 0 or src.max() >= nsrc or rows.min() < 0 or
+              rows.max() >= (1 << _native.GATHER_SRC_SHIFT)):
+        raise IndexError('gather_sources: source or row out of range')
+    packed = (src.astype(np.uint64) << np.uint64(_native.GATHER_SRC_SHIFT)) | rows.astype(np.uint64)
+    buf = torch.from_numpy(np.concatenate([table.reshape(-1), packed]).view(np.int64)).to(dev)
+    tab = buf.data_ptr()
+    idx = tab + table.size * 8
+    ragged = [n for n in names if isinstance(sources[0].columns[n], RaggedColumn)]
+    # a workspace per ragged column (its scan's tile prefixes are read by its copy, which runs
+    # after every scan), fixed columns in the first; then the ragged totals
+    wsb = int(lib.mdsx_gather_workspace_bytes(m))
+    nws = max(len(ragged), 1)
+    ws = torch.zeros(wsb * nws + 8 * nws, dtype=torch.uint8, device=dev)
+    tot = wsb * nws
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    out: dict[str, Union[torch.Tensor, RaggedColumn]] = {}
+    offs = {}
+    for c, name in enumerate(names):
+        col = sources[0].columns[name]
+        srcs = tab + c * nsrc * 32
+        if isinstance(col, RaggedColumn):
+            r = ragged.index(name)
+            offs[name] = torch.empty(m + 1, dtype=torch.int64, device=dev)
+            _check(lib.mdsx_gather_ragged_scan_multi(srcs, nsrc, idx if m else None, m,
+                                                     offs[name].data_ptr(),
+                                                     ws.data_ptr() + r * wsb, wsb,
+                                                     ws.data_ptr() + tot + 8 * r, stream),
+                   'mdsx_gather_ragged_scan_multi')
+        else:
+            row_shape = tuple(col.shape[1:])
+            dst = torch.empty((m, ) + row_shape, dtype=col.dtype, device=dev)
+            row_bytes = int(np.prod(row_shape, dtype=np.int64)) * col.element_size()
+            if m:
+                _check(lib.mdsx_gather_fixed_multi(srcs, nsrc, row_bytes, idx, m, dst.data_ptr(),
+                                                   ws.data_ptr(), wsb, stream),
+                       'mdsx_gather_fixed_multi')
+            out[name] = dst
+    # the one sync: the status records and the ragged totals together
+    head = torch.cat([ws[r * wsb:r * wsb + 16] for r in range(nws)] +
+                     [ws[tot:tot + 8 * len(ragged)]]).cpu().numpy()
+    if check:
+        for r in range(nws):
+            st = _native.Status.from_buffer_copy(head[16 * r:16 * r + 16].tobytes())
+            if st.code != 0:
+                raise IndexError(f'sample id out of range at position {st.row} of the gather')
+    caps = head[16 * nws:].view(np.int64)
+    for c, name in enumerate(names):
+        col = sources[0].columns[name]
+        if not isinstance(col, RaggedColumn):
+            continue
+        cap = int(caps[ragged.index(name)])
+        vals = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
+        flags = torch.zeros(m, dtype=torch.uint8, device=dev) if col.flags is not None else None
+        _check(lib.mdsx_gather_ragged_copy_multi(
+            tab + c * nsrc * 32, nsrc, idx if m else None, m, vals.data_ptr() if cap else None,
+            cap, offs[name].data_ptr(), flags.data_ptr() if flags is not None else None,
+            ws.data_ptr() + ragged.index(name) * wsb, wsb, stream), 'mdsx_gather_ragged_copy_multi')
+        out[name] = RaggedColumn(vals[:cap], offs[name], flags)
+    # (a source freed after this returns is reused in stream order: these kernels come first)
+    return DecodedBatch({name: out[name] for name in names}, m)
+
+
 def _status_error(status: _native.Status, plan: Plan) -> Exception:
     code = status.code
     col = ''

@@ -32,7 +32,7 @@ from typing import Iterator, Sequence, Union
 import numpy as np
 import torch
 
-from streaming_amd.decoder import DecodedBatch, RaggedColumn
+from streaming_amd.decoder import DecodedBatch, RaggedColumn, gather_sources
 from streaming_amd.reader import MDSReader
 
 __all__ = ['worker_sample_ids', 'concat_batches', 'DeviceSampleGather']
@@ -92,35 +92,28 @@ class DeviceSampleGather:
         shard = np.searchsorted(self.starts, ids, side='right') - 1
         return shard, ids - self.starts[shard]
 
-    def _shard_rows(self, s: int, local: np.ndarray) -> DecodedBatch:
-        reader = self.shards[s]
-        os.stat(reader._filename())  # FileNotFoundError once evicted (the reference's open())
-        entry = reader._decode_entry()
-        if entry.status.code != 0:  # raise only for the bad samples this batch reads
-            for idx in np.unique(local):
-                reader._check_row(entry, int(idx))
-        return entry.decoded.gather(torch.from_numpy(np.ascontiguousarray(local)))
-
     def gather(self, sample_ids: Union[Sequence[int], np.ndarray, torch.Tensor]) -> DecodedBatch:
-        """The samples ``sample_ids`` (global ids; ``-1`` skipped), in that order."""
+        """The samples ``sample_ids`` (global ids; ``-1`` skipped), in that order: the shards
+        they touch decoded (or found in the cache), then every column gathered from all of them
+        in one launch sequence (``mdsx_gather_*_multi``), rows already in batch order."""
         ids = np.asarray(torch.as_tensor(sample_ids).cpu().numpy() if isinstance(
             sample_ids, torch.Tensor) else sample_ids, np.int64).reshape(-1)
         ids = ids[ids != -1]
         if ids.size == 0:
             raise ValueError('gather: no samples')
         shard, local = self.locate(ids)
-        order = np.argsort(shard, kind='stable')
-        sorted_shards = shard[order]
-        cuts = np.flatnonzero(np.diff(sorted_shards)) + 1
-        parts = []
-        for grp in np.split(order, cuts):
-            parts.append(self._shard_rows(int(shard[grp[0]]), local[grp]))
-        out = concat_batches(parts)
-        if np.array_equal(order, np.arange(ids.size)):
-            return out
-        inv = np.empty_like(order)
-        inv[order] = np.arange(ids.size)  # batch position i is row inv[i] of the shard-major rows
-        return out.gather(torch.from_numpy(inv))
+        touched, src = np.unique(shard, return_inverse=True)
+        src = src.reshape(-1)
+        decoded = []
+        for j, s in enumerate(touched):
+            reader = self.shards[int(s)]
+            os.stat(reader._filename())  # FileNotFoundError once evicted (the reference's open())
+            entry = reader._decode_entry()
+            if entry.status.code != 0:  # raise only for the bad samples this batch reads
+                for idx in np.unique(local[src == j]):
+                    reader._check_row(entry, int(idx))
+            decoded.append(entry.decoded)
+        return gather_sources(decoded, src, local)
 
     def iter_batches(self, sample_ids: Union[Sequence[int], np.ndarray, torch.Tensor],
                      batch_size: int) -> Iterator[DecodedBatch]:

@@ -102,3 +102,58 @@ def test_ragged_gather_reads_only_inside_the_source_tensor(row):
     src, so = values.cpu().numpy(), offsets.cpu().numpy()
     for k, r in enumerate(ids):
         assert np.array_equal(v[o[k]:o[k + 1]], src[so[r]:so[r + 1]]), k
+
+
+@pytest.mark.parametrize('name', ['config_b_small', 'config_c_small', 'config_a', 'bad_utf8',
+                                  'dynamic'])
+def test_gather_sources_matches_oracle(name):
+    """Multi-source gather (mdsx_gather_*_multi): one launch sequence over every shard's decoded
+    columns, rows in id order, against the oracle; also through DeviceSampleGather."""
+    from streaming_amd.decoder import gather_sources
+    rows = _oracle_rows(name)
+    ds = LocalDataset(os.path.join(gu.GOLDEN, name))
+    rng = np.random.default_rng(3 + len(name))
+    ids = rng.integers(0, len(rows), 2 * len(rows) + 3)
+    g = ds.sample_gather
+    shard, local = g.locate(ids)
+    sources = [ds.decode_all([s]) for s in range(len(ds.shards))]
+    for got in (gather_sources(sources, shard, local), g.gather(ids)):
+        assert got.rows == len(ids)
+        for cname, col in got.columns.items():
+            if isinstance(col, RaggedColumn):
+                vals, offs = col.values.cpu().numpy(), col.offsets.cpu().numpy()
+                flags = col.flags.cpu().numpy() if col.flags is not None else None
+                for k, r in enumerate(ids):
+                    assert vals[offs[k]:offs[k + 1]].tobytes() == rows[r][cname], (cname, k)
+                    if flags is not None:
+                        assert flags[k] == (0 if mds_oracle.utf8_is_valid(rows[r][cname]) else 1)
+            else:
+                raw = col.reshape(col.shape[0], -1).view(torch.uint8).cpu().numpy()
+                for k, r in enumerate(ids):
+                    assert raw[k].tobytes() == rows[r][cname], (cname, k)
+
+
+def test_gather_sources_rejects_bad_ids():
+    from streaming_amd.decoder import gather_sources
+    ds = LocalDataset(os.path.join(gu.GOLDEN, 'config_c_small'))
+    src = [ds.decode_all([0])]
+    with pytest.raises(IndexError):
+        gather_sources(src, np.array([0, 1]), np.array([0, 0]))  # no source 1
+    with pytest.raises(IndexError):  # row past the source: found by the kernels
+        gather_sources(src, np.array([0, 0]), np.array([0, src[0].rows]))
+
+
+def test_gather_sources_config_b_full_size_four_sources():
+    """1M config-B rows split into four sources (row-range views), permuted across them."""
+    from streaming_amd.decoder import DecodedBatch, decode_batch, gather_sources
+    synth = fixed_b_batch_on_device(1_000_000, seed=22)
+    dec = decode_batch(synth.plan, synth.batch)
+    cuts = [0, 250_000, 400_000, 999_999, 1_000_000]
+    sources = [DecodedBatch({k: v[a:b] for k, v in dec.columns.items()}, b - a)
+               for a, b in zip(cuts[:-1], cuts[1:])]
+    perm = torch.randperm(1_000_000).numpy()
+    src = np.searchsorted(np.array(cuts), perm, side='right') - 1
+    g = gather_sources(sources, src, perm - np.array(cuts)[src])
+    p = torch.from_numpy(perm).to(dec['x'].device)
+    assert torch.equal(g['id'], synth.sources['id'][p])
+    assert torch.equal(g['x'].view(torch.int32), synth.sources['x'].view(torch.int32)[p])
