@@ -7,7 +7,8 @@ directory, then, in one process:
     cache as batches first touch them;
   * warm epochs: the same ids again (every shard resident), per batch size;
 every batch checked against the fully decoded dataset gathered with the same ids (first batch of
-each run bit-exact, all batches' row counts). Prints one JSON object.
+each run bit-exact, all batches' row counts); then the per-sample ``get_item`` rate (the path
+``StreamingDataset.get_item`` takes through a device reader). Prints one JSON object.
 """
 
 import argparse
@@ -96,6 +97,16 @@ def main():
             res['runs'][str(bs)] = {'batches': m, 'ms_per_batch': dt / m * 1e3,
                                     'samples_per_s': rows / dt, 'out_GBps': nbytes / dt / 1e9,
                                     'first_batch_bit_exact': ok}
+        # the per-sample drop-in path StreamingDataset.get_item takes (shard[idx] on a device
+        # reader: the decoded shard's host copy, sliced per sample), shards already decoded
+        n_items = min(20_000, total)
+        for shard in ds.shards:  # first touch: the decoded shard's host copy (one D2H each)
+            shard[0]
+        t0 = time.perf_counter()
+        for i in ids[:n_items]:
+            ds.get_item(int(i))
+        res['get_item'] = {'samples': n_items,
+                           'samples_per_s': n_items / (time.perf_counter() - t0)}
         print(json.dumps(res, indent=1))
         assert all(r['first_batch_bit_exact'] for r in res['runs'].values())
     finally:
