@@ -160,24 +160,32 @@ def main():
         res['d2h_GBps'] = W / (time.perf_counter() - t0) / 1e9
         del dec, out, batch
         torch.cuda.empty_cache()
-        # 5. pipelined end to end
-        for d2h in (False, True):
+        # 5. pipelined end to end: device hand-off; host hand-off with a blocking to_host per
+        # batch; host hand-off with the D2H overlapped (ShardPipeline.iter_host)
+        first_col = plan.columns[0].name
+        for mode in ('device', 'd2h', 'd2h_overlap'):
             pipe = ShardPipeline(plan, files, shards_per_batch=args.per_batch, depth=2,
                                  workers=args.workers)
-            for b in pipe:  # warm-up pass (allocations, page cache)
+            for b in (pipe.iter_host() if mode == 'd2h_overlap' else pipe):  # warm-up pass
                 pass
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             n = 0
-            for b in pipe:
-                n += b.rows
-                if d2h:
-                    to_host(b)
+            if mode == 'd2h_overlap':
+                for h in pipe.iter_host():
+                    v = h[first_col]
+                    n += (len(v[1]) - 1) if isinstance(v, tuple) else len(v)
+            else:
+                for b in pipe:
+                    n += b.rows
+                    if mode == 'd2h':
+                        to_host(b)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
             pipe.close()
             assert n == rows
-            key = 'e2e_with_d2h' if d2h else 'e2e_device_handoff'
+            key = {'device': 'e2e_device_handoff', 'd2h': 'e2e_with_d2h',
+                   'd2h_overlap': 'e2e_with_d2h_overlapped'}[mode]
             res[key] = {'samples_per_s': rows / dt, 'raw_GiBps': raw_bytes / dt / 2**30,
                         'seconds': dt}
         _validate_runs(args, plan, files, raw_bytes, rows, algos, res)

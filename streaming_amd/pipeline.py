@@ -242,8 +242,61 @@ class ShardPipeline:
             slot.decoder.check()
             yield out
 
+    def iter_host(self) -> Iterator[dict[str, Union[np.ndarray, tuple]]]:
+        """Decoded batches handed to the host (numpy arrays as :func:`to_host` returns them), in
+        order. Each batch's D2H copy runs on its own stream while the next batch's H2D copy is
+        in flight (PCIe is full duplex), and the next decode waits for it (the outputs it reads
+        belong to the slot); a batch is handed out once its copy has landed."""
+        compute = torch.cuda.current_stream(self.device)
+        d2h = torch.cuda.Stream(self.device)
+        prev = None
+        for out in self:
+            host, done = _to_host_async(out, d2h, compute)
+            compute.wait_event(done)  # the slot's outputs are reused by later decodes
+            if prev is not None:
+                prev[1].synchronize()
+                yield _host_arrays(prev[0])
+            prev = (host, done)
+        if prev is not None:
+            prev[1].synchronize()
+            yield _host_arrays(prev[0])
+
     def close(self) -> None:
         self.pool.shutdown(wait=True)
+
+
+def _to_host_async(decoded: DecodedBatch, stream: torch.cuda.Stream,
+                   after: torch.cuda.Stream) -> tuple[dict, torch.cuda.Event]:
+    """Queue the D2H copies of every column of ``decoded`` (pinned host tensors) on ``stream``,
+    behind the work queued so far on ``after``; returns the host tensors and the copies' event."""
+    ready = torch.cuda.Event()
+    ready.record(after)
+    stream.wait_event(ready)
+    out = {}
+    with torch.cuda.stream(stream):
+        for name, col in decoded.columns.items():
+            parts = ([col.values, col.offsets] + ([col.flags] if col.flags is not None else [])
+                     if isinstance(col, RaggedColumn) else [col])
+            host = []
+            for t in parts:
+                h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+                h.copy_(t, non_blocking=True)
+                host.append(h)
+            out[name] = host if isinstance(col, RaggedColumn) else host[0]
+    done = torch.cuda.Event()
+    done.record(stream)
+    return out, done
+
+
+def _host_arrays(out: dict) -> dict[str, Union[np.ndarray, tuple]]:
+    res = {}
+    for name, v in out.items():
+        if isinstance(v, list):
+            res[name] = tuple(x.numpy() for x in v)
+        else:
+            res[name] = v.view(torch.uint8).numpy() if v.dtype in (torch.uint16, torch.uint32,
+                                                                   torch.uint64) else v.numpy()
+    return res
 
 
 def to_host(decoded: DecodedBatch, pin: bool = True) -> dict[str, Union[np.ndarray, tuple]]:
@@ -263,11 +316,4 @@ def to_host(decoded: DecodedBatch, pin: bool = True) -> dict[str, Union[np.ndarr
             h.copy_(col, non_blocking=True)
             out[name] = h
     torch.cuda.current_stream().synchronize()
-    res = {}
-    for name, v in out.items():
-        if isinstance(v, list):
-            res[name] = tuple(x.numpy() for x in v)
-        else:
-            res[name] = v.view(torch.uint8).numpy() if v.dtype in (torch.uint16, torch.uint32,
-                                                                   torch.uint64) else v.numpy()
-    return res
+    return _host_arrays(out)

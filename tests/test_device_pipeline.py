@@ -73,6 +73,37 @@ def test_to_host_handoff():
     assert bytes(vals[offs[0]:offs[1]]).decode() == 'hé' and flags.tolist() == [0, 0]
 
 
+@pytest.mark.parametrize('name,per,depth', [('config_a', 3, 2), ('config_c_small', 1, 2),
+                                            ('zstd', 1, 1), ('wide', 2, 3)])
+def test_iter_host_matches_reference(name, per, depth):
+    """Host hand-off with the D2H overlapped (ShardPipeline.iter_host): every batch, in order,
+    gives the reference's column digests once concatenated."""
+    d = os.path.join(gu.GOLDEN, name)
+    idx = gu.index(name)
+    info = idx['shards'][0]
+    plan = Plan(info['column_names'], info['column_encodings'], info['column_sizes'])
+    pipe = ShardPipeline(plan, shard_files_from_index(d, idx), shards_per_batch=per, depth=depth,
+                         workers=4)
+    batches = list(pipe.iter_host())
+    pipe.close()
+    assert len(batches) == len(pipe.groups)
+    m = gu.manifest()[name]['columns']
+    for cname in batches[0]:
+        if isinstance(batches[0][cname], tuple):
+            values = np.concatenate([b[cname][0] for b in batches])
+            offs, base = [np.zeros(1, np.int64)], 0
+            for b in batches:
+                offs.append(b[cname][1][1:] + base)
+                base += int(b[cname][1][-1])
+            assert hashlib.sha256(values.tobytes()).hexdigest() == m[cname]['values']
+            assert hashlib.sha256(np.concatenate(offs).tobytes()).hexdigest() == \
+                m[cname]['offsets']
+        else:
+            rows = np.concatenate([b[cname].reshape(b[cname].shape[0], -1).view(np.uint8)
+                                   for b in batches])
+            assert hashlib.sha256(rows.tobytes()).hexdigest() == m[cname]['rows']
+
+
 @pytest.mark.parametrize('name', ['kat', 'scalars', 'bad_utf8'])
 def test_plugin_stream_get_item(name):
     d = os.path.join(gu.GOLDEN, name)
