@@ -323,6 +323,12 @@ int mdsx_hash_segments(int algo, uint64_t seed, const uint8_t* data, uint64_t da
  * 16, 16-byte aligned pointers) on `stream`. Not part of the decode path: it measures what a
  * pure stream of the same bytes reaches on the device, reported beside the decode rate. */
 int mdsx_copy_probe(const void* d_src, void* d_dst, uint64_t bytes, void* stream);
+/* Host hand-off copy: the same 16-byte streaming kernel storing into PINNED host memory (a
+ * device-accessible host pointer) over PCIe, `bytes` a multiple of 16, both pointers 16-byte
+ * aligned. A DMA-engine D2H and H2D do not overlap on this platform (they serialise, measured);
+ * this copy runs beside a DMA-engine H2D at ~43 GB/s each way (scripts/pcie_duplex.py), so a
+ * decoded batch goes to the host while the next batch's shards come in. */
+int mdsx_copy_to_host(const void* d_src, void* h_dst, uint64_t bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1612,4 +1612,18 @@ int mdsx_copy_probe(const void* d_src, void* d_dst, uint64_t bytes, void* stream
   return hip_check(hipGetLastError(), "copy_probe_kernel launch");
 }
 
+int mdsx_copy_to_host(const void* d_src, void* h_dst, uint64_t bytes, void* stream) {
+  if (!d_src || !h_dst || (bytes & 15) || (reinterpret_cast<uint64_t>(d_src) & 15) ||
+      (reinterpret_cast<uint64_t>(h_dst) & 15))
+    return mdsx::fail(MDSX_E_ARG,
+                      "mdsx_copy_to_host: 16-byte aligned pointers and size required");
+  const uint64_t n = bytes / 16;
+  if (n == 0) return MDSX_OK;
+  const unsigned grid = unsigned((n + kProbeBlock - 1) / kProbeBlock);
+  hipLaunchKernelGGL(copy_probe_kernel, dim3(grid), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), static_cast<const uint4*>(d_src),
+                     static_cast<uint4*>(h_dst), n);
+  return hip_check(hipGetLastError(), "copy_probe_kernel launch (to host)");
+}
+
 }  // extern "C"

@@ -30,6 +30,7 @@ import torch
 from streaming_amd.compression import decompress, decompress_into, get_compression_extension
 from streaming_amd.decoder import (BatchDecoder, DecodedBatch, DeviceBatch, Plan, RaggedColumn,
                                    _layout, _tables)
+from streaming_amd import _native
 from streaming_amd.hashing import DeviceHasher, _status_check, get_hash, hex_digests, is_hash
 
 __all__ = ['ShardFile', 'ShardPipeline', 'shard_files_from_index', 'to_host',
@@ -272,6 +273,7 @@ def _to_host_async(decoded: DecodedBatch, stream: torch.cuda.Stream,
     ready = torch.cuda.Event()
     ready.record(after)
     stream.wait_event(ready)
+    lib = _native.lib()
     out = {}
     with torch.cuda.stream(stream):
         for name, col in decoded.columns.items():
@@ -279,8 +281,20 @@ def _to_host_async(decoded: DecodedBatch, stream: torch.cuda.Stream,
                      if isinstance(col, RaggedColumn) else [col])
             host = []
             for t in parts:
+                t = t.contiguous()
                 h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
-                h.copy_(t, non_blocking=True)
+                nbytes = t.numel() * t.element_size()
+                body = nbytes & ~15
+                if body and not (t.data_ptr() | h.data_ptr()) & 15:
+                    # a kernel storing into the pinned buffer: it overlaps the DMA-engine H2D
+                    # of the next batch, where a DMA-engine D2H would queue behind it
+                    _native.raise_for_code(lib.mdsx_copy_to_host(
+                        t.data_ptr(), h.data_ptr(), body, stream.cuda_stream), 'mdsx_copy_to_host')
+                    if nbytes > body:
+                        h.view(-1).view(torch.uint8)[body:].copy_(
+                            t.view(-1).view(torch.uint8)[body:], non_blocking=True)
+                else:
+                    h.copy_(t, non_blocking=True)
                 host.append(h)
             out[name] = host if isinstance(col, RaggedColumn) else host[0]
     done = torch.cuda.Event()
