@@ -55,7 +55,7 @@ struct mdsx_plan {
                            // temporal ones let L2 merge the partial stores at run edges)
   int rows_kb = 0;         // row-parallel decode of shorter samples: LDS stage in KiB (0: off,
                            // -1: sized per batch, rows_tile_rows / rows_stage_bytes)
-  int rows_nt = 0;         // row-parallel decode: non-temporal loads and stores
+  int rows_nt = 1;         // row-parallel decode: non-temporal loads and stores (measured faster)
   int gather_chunks = 2;  // 16-byte chunks per lane in the ragged gather (tile = 4 KiB x this)
   int gather_min = 256;   // ragged columns averaging fewer bytes per row use the gather kernel
   int group_max = 1024;   // ... fewer than this (and >= gather_min): four rows per wave

@@ -40,6 +40,7 @@ MODES = {
     'rows': 'rows=32,rmin=1000000000',  # the row-parallel decode (mdsx_rows.hip) for every size
     'rows_auto': 'rows=-1,rmin=1000000000',  # ... its tiles and stage sized per batch
     'rows_small': 'rows=2,rmin=1000000000',  # a 2 KiB stage: windows and HBM-direct samples
+    'rows_temporal': 'rows=-1,rownt=0,rmin=1000000000',  # temporal loads / stores (default: nt)
     'stage': 'stage=24,run=0,rows=0',  # the staged decode (opt-in; measured slower)
     'stage_overflow': 'stage=4,fill=300,run=0,rows=0',  # tiles of ~3x the stage: several row groups each
     'stage_tiny': 'stage=1,run=0,rows=0',  # rows over 1 KiB go through the huge-row kernel
