@@ -113,9 +113,11 @@ int mdsx_plan_num_var(const mdsx_plan* plan);
  * [(t - tile0) * tile_rows, ...) of that shard; a shard has ceil(samples / tile_rows) tiles. */
 int mdsx_plan_tile_rows(const mdsx_plan* plan);
 /* Rows per tile the decoder wants for a batch of `rows` samples in `shard_bytes` bytes of shard
- * files (set as mdsx_batch.tile_rows and used to build its tile table). Ragged plans: sized so
- * that a tile's samples fill about half of the LDS stage of the staged decode (a power of two
- * in [1, 256]); all-fixed plans: mdsx_plan_tile_rows. */
+ * files (set as mdsx_batch.tile_rows and used to build its tile table), a power of two. Ragged
+ * plans, by the decode the batch gets: samples averaging >= 3 KiB (streaming decode) about
+ * 32 KiB of samples per tile, 1..32 rows; shorter ones (row-parallel decode) up to 256 rows
+ * filling ~8/9 of a 20 KiB (samples < 512 B) or 40 KiB LDS stage; all-fixed plans:
+ * mdsx_plan_tile_rows. */
 int mdsx_plan_tile_rows_for(const mdsx_plan* plan, uint64_t shard_bytes, uint64_t rows);
 /* Rows per tile of the encoder's batches (mdsx_encode_shards): its tile table is built with
  * this, not with mdsx_plan_tile_rows. */
