@@ -374,6 +374,7 @@ class DecodedBatch:
         lib = _native.lib()
         first = next(iter(self.columns.values()))
         dev = first.values.device if isinstance(first, RaggedColumn) else first.device
+        _require_device_columns([self])
         idx = torch.as_tensor(ids, dtype=torch.int64).to(dev).reshape(-1)
         idx = idx[idx != -1].contiguous()
         m = int(idx.numel())
@@ -420,6 +421,17 @@ class DecodedBatch:
         return DecodedBatch(out, m)
 
 
+def _require_device_columns(batches: Sequence['DecodedBatch']) -> None:
+    """The gather kernels read their sources through device pointers: a host tensor's address
+    must never reach them (it would fault the GPU), so CPU columns are refused here."""
+    for b in batches:
+        for name, col in b.columns.items():
+            for t in ((col.values, col.offsets) if isinstance(col, RaggedColumn) else (col, )):
+                if t.device.type != 'cuda':
+                    raise ValueError(f'gather: column {name!r} is not on the GPU ({t.device}); '
+                                     'the device gather reads decoded device tensors only')
+
+
 def gather_sources(sources: Sequence[DecodedBatch], src: np.ndarray, rows: np.ndarray,
                    check: bool = True) -> DecodedBatch:
     """Output row k = row ``rows[k]`` of ``sources[src[k]]`` (decoded shards of one schema), for
@@ -435,6 +447,7 @@ def gather_sources(sources: Sequence[DecodedBatch], src: np.ndarray, rows: np.nd
     if src.shape != rows.shape:
         raise ValueError('gather_sources: src and rows differ in length')
     m, nsrc = int(src.size), len(sources)
+    _require_device_columns(sources)
     names = list(sources[0].columns)
     first = sources[0].columns[names[0]]
     dev = first.values.device if isinstance(first, RaggedColumn) else first.device

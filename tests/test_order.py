@@ -96,3 +96,20 @@ def test_locate_matches_spanner():
         g.locate(np.array([16]))
     with pytest.raises(IndexError):
         g.locate(np.array([-2]))
+
+
+def test_gather_sources_refuses_host_columns_and_bad_arguments():
+    """Argument checks of the multi-source gather, all before any kernel launch (CPU)."""
+    import torch
+    from streaming_amd.decoder import DecodedBatch, RaggedColumn, gather_sources
+    host = DecodedBatch({'x': torch.zeros(4, dtype=torch.int32),
+                         's': RaggedColumn(torch.zeros(8, dtype=torch.uint8),
+                                           torch.arange(5, dtype=torch.int64) * 2, None)}, 4)
+    with pytest.raises(ValueError, match='not on the GPU'):
+        gather_sources([host], np.zeros(2, np.int64), np.arange(2))
+    with pytest.raises(ValueError, match='not on the GPU'):
+        host.gather([0, 1])
+    with pytest.raises(ValueError, match='differ in length'):
+        gather_sources([host], np.zeros(2, np.int64), np.arange(3))
+    with pytest.raises(ValueError, match='no sources'):
+        gather_sources([], np.zeros(0, np.int64), np.zeros(0, np.int64))
