@@ -588,6 +588,10 @@ class BatchDecoder:
     def __init__(self, plan: Plan, batch: DeviceBatch,
                  capacities: Optional[dict[str, int]] = None, single: bool = False) -> None:
         _native.check_fork()
+        if batch.buffer.device.type != 'cuda':  # host addresses must never reach the kernels
+            _native.require_gpu()
+            raise ValueError(f'BatchDecoder: the shard batch is on {batch.buffer.device}, not '
+                             'the GPU (stage_shards / make_batch put it there)')
         self.plan = plan
         self.batch = batch
         dev = batch.device
