@@ -89,6 +89,39 @@ def _validate_runs(args, plan, files, raw_bytes, rows, algos, res):
             'hash_on': None if algo is None else where}
 
 
+def _pipelined(args, plan, files, raw_bytes, rows, res):
+    # 5. pipelined end to end: device hand-off; host hand-off with a blocking to_host per
+    # batch; host hand-off with the D2H overlapped (ShardPipeline.iter_host)
+    first_col = plan.columns[0].name
+    for depth, mode in [(d, m) for d in args.depth for m in args.modes.split(',')]:
+        pipe = ShardPipeline(plan, files, shards_per_batch=args.per_batch, depth=depth,
+                             workers=args.workers)
+        for b in (pipe.iter_host() if mode == 'd2h_overlap' else pipe):  # warm-up pass
+            pass
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        n = 0
+        if mode == 'd2h_overlap':
+            for h in pipe.iter_host():
+                v = h[first_col]
+                n += (len(v[1]) - 1) if isinstance(v, tuple) else len(v)
+        else:
+            for b in pipe:
+                n += b.rows
+                if mode == 'd2h':
+                    to_host(b)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        pipe.close()
+        assert n == rows
+        key = {'device': 'e2e_device_handoff', 'd2h': 'e2e_with_d2h',
+               'd2h_overlap': 'e2e_with_d2h_overlapped'}[mode]
+        if depth != 2:
+            key += f'_depth{depth}'
+        res[key] = {'samples_per_s': rows / dt, 'raw_GiBps': raw_bytes / dt / 2**30,
+                    'seconds': dt}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--config', default='B', choices=['B', 'C', 'E'])
@@ -101,6 +134,10 @@ def main():
                          '(ShardPipeline validate_hash; xxh3 on the device, the rest on the host '
                          'threads)')
     ap.add_argument('--skip-stages', action='store_true', help='only the pipelined runs')
+    ap.add_argument('--depth', type=int, nargs='+', default=[2],
+                    help='ShardPipeline depths of the pipelined runs')
+    ap.add_argument('--modes', default='device,d2h,d2h_overlap',
+                    help='pipelined runs: device, d2h (blocking to_host), d2h_overlap (iter_host)')
     args = ap.parse_args()
     algos = [a for a in args.validate.split(',') if a]
     torch.cuda.set_device(0)
@@ -115,6 +152,7 @@ def main():
                'raw_bytes': raw_bytes, 'file_bytes': file_bytes, 'workers': args.workers,
                'host_cpus': len(os.sched_getaffinity(0)), 'generate_s': gen_s}
         if args.skip_stages:
+            _pipelined(args, plan, files, raw_bytes, rows, res)
             _validate_runs(args, plan, files, raw_bytes, rows, algos, res)
             print(json.dumps(res, indent=1))
             return
@@ -160,34 +198,7 @@ def main():
         res['d2h_GBps'] = W / (time.perf_counter() - t0) / 1e9
         del dec, out, batch
         torch.cuda.empty_cache()
-        # 5. pipelined end to end: device hand-off; host hand-off with a blocking to_host per
-        # batch; host hand-off with the D2H overlapped (ShardPipeline.iter_host)
-        first_col = plan.columns[0].name
-        for mode in ('device', 'd2h', 'd2h_overlap'):
-            pipe = ShardPipeline(plan, files, shards_per_batch=args.per_batch, depth=2,
-                                 workers=args.workers)
-            for b in (pipe.iter_host() if mode == 'd2h_overlap' else pipe):  # warm-up pass
-                pass
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            n = 0
-            if mode == 'd2h_overlap':
-                for h in pipe.iter_host():
-                    v = h[first_col]
-                    n += (len(v[1]) - 1) if isinstance(v, tuple) else len(v)
-            else:
-                for b in pipe:
-                    n += b.rows
-                    if mode == 'd2h':
-                        to_host(b)
-            torch.cuda.synchronize()
-            dt = time.perf_counter() - t0
-            pipe.close()
-            assert n == rows
-            key = {'device': 'e2e_device_handoff', 'd2h': 'e2e_with_d2h',
-                   'd2h_overlap': 'e2e_with_d2h_overlapped'}[mode]
-            res[key] = {'samples_per_s': rows / dt, 'raw_GiBps': raw_bytes / dt / 2**30,
-                        'seconds': dt}
+        _pipelined(args, plan, files, raw_bytes, rows, res)
         _validate_runs(args, plan, files, raw_bytes, rows, algos, res)
         print(json.dumps(res, indent=1))
     finally:

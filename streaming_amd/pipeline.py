@@ -246,8 +246,11 @@ class ShardPipeline:
     def iter_host(self) -> Iterator[dict[str, Union[np.ndarray, tuple]]]:
         """Decoded batches handed to the host (numpy arrays as :func:`to_host` returns them), in
         order. Each batch's D2H copy runs on its own stream while the next batch's H2D copy is
-        in flight (PCIe is full duplex), and the next decode waits for it (the outputs it reads
-        belong to the slot); a batch is handed out once its copy has landed."""
+        in flight, and the next decode waits for it (the outputs it reads belong to the slot); a
+        batch is handed out once its copy has landed. The D2H is a kernel storing into pinned
+        memory (``mdsx_copy_to_host``): two DMA-engine copies in opposite directions serialise
+        on this platform, a kernel beside a DMA copy does not. ``depth=3`` measured best
+        (DESIGN.md §7)."""
         compute = torch.cuda.current_stream(self.device)
         d2h = torch.cuda.Stream(self.device)
         prev = None
