@@ -206,7 +206,9 @@ __device__ __forceinline__ bool copy_segment(Stream& st, const lds_u8* ring, uin
   bool bad = false;
   uint32_t prev_w = 0;
   uint4 last = make_uint4(0, 0, 0, 0);
-  constexpr uint32_t U = 2;  // chunks per lane per step (a step spans <= 4 <= S slots)
+  // chunks per lane per step: 1 (a step waits for 1 KiB of the ring, the rest stays in flight;
+  // measured 1 % faster than 2 on config C, profiles/r02/u1/)
+  constexpr uint32_t U = 1;
   for (uint32_t g = 0; g < nch; g += 64 * U) {
     ensure<S, kNT>(st, ring, ring_lds, g ? s0 + 16u * g : sp, s0 + 16u * g + 64u * 16u * U + 15u,
                    lane);
