@@ -95,7 +95,9 @@ class DeviceSampleGather:
     def gather(self, sample_ids: Union[Sequence[int], np.ndarray, torch.Tensor]) -> DecodedBatch:
         """The samples ``sample_ids`` (global ids; ``-1`` skipped), in that order: the shards
         they touch decoded (or found in the cache), then every column gathered from all of them
-        in one launch sequence (``mdsx_gather_*_multi``), rows already in batch order."""
+        in one launch sequence (``mdsx_gather_*_multi``), rows already in batch order. The
+        touched shards' decoded columns are held until the gather is queued, so a decoded-shard
+        cache smaller than one batch's shards is exceeded for that long."""
         ids = np.asarray(torch.as_tensor(sample_ids).cpu().numpy() if isinstance(
             sample_ids, torch.Tensor) else sample_ids, np.int64).reshape(-1)
         ids = ids[ids != -1]
