@@ -52,3 +52,27 @@ def test_single_rank_dry_run():
     line = json.loads(p.stdout.strip().splitlines()[-1])
     assert line['n_gpus'] == 1
     assert line['ownership']['B'][0]['shards'] == list(range(62))
+
+
+def test_committed_traffic_is_keyed_on_workload_kernel_and_sources(tmp_path, monkeypatch):
+    """bench.py reports a PMC traffic figure only from a summary taken on the same workload,
+    kernel and library sources (the sha compiled into mdsx_version); else null."""
+    import json
+
+    import bench
+    from streaming_amd import build
+    sha = build.source_sha()
+    assert bench.src_sha() == sha  # the loaded library names these sources
+    prof = tmp_path / 'profiles' / 'r99'
+    prof.mkdir(parents=True)
+    entry = {'workload_key': 'B:k', 'kernel': 'decode_kernel<4, true>', 'src_sha': sha,
+             'hbm_traffic_bytes_per_launch': 123.0}
+    stale = dict(entry, src_sha='0' * 16, hbm_traffic_bytes_per_launch=7.0)
+    (prof / 'pmc_x.json').write_text(json.dumps({'entries': [stale, entry]}))
+    monkeypatch.setattr(bench, 'HERE', str(tmp_path))
+    assert bench.committed_traffic('B:k', 'decode_kernel<4, true>') == (
+        123.0, os.path.join('profiles', 'r99', 'pmc_x.json'))
+    assert bench.committed_traffic('B:other', 'decode_kernel<4, true>') == (None, None)
+    assert bench.committed_traffic('B:k', 'run_decode_kernel<4, false>') == (None, None)
+    (prof / 'pmc_x.json').write_text(json.dumps({'entries': [stale]}))
+    assert bench.committed_traffic('B:k', 'decode_kernel<4, true>') == (None, None)
