@@ -20,6 +20,7 @@ Every decode goes through libmdsx.so; there is no CPU path.
 from __future__ import annotations
 
 import ctypes
+import os
 import math
 from dataclasses import dataclass, field
 from typing import Optional, Sequence, Union
@@ -570,6 +571,15 @@ def payload_bound(plan: Plan, batch: DeviceBatch) -> int:
     return max(0, batch.shard_bytes - heads - per_row * batch.total_rows)
 
 
+def _tune_knob(key: str) -> int:
+    """An integer MDSX_TUNE knob the Python side reads (measurement only; 0 when unset)."""
+    for kv in os.environ.get('MDSX_TUNE', '').split(','):
+        k, _, v = kv.partition('=')
+        if k.strip() == key and v.strip().isdigit():
+            return int(v)
+    return 0
+
+
 class BatchDecoder:
     """Decode a :class:`DeviceBatch` on the device, reusing outputs across calls.
 
@@ -603,9 +613,11 @@ class BatchDecoder:
         self.totals = torch.zeros(max(plan.num_var, 1), dtype=torch.int64, device=dev)
         self.outputs: dict[str, Union[torch.Tensor, RaggedColumn]] = {}
         self._fixed_raw: dict[str, torch.Tensor] = {}
+        skew = _tune_knob('skew') * 1024  # measurement only: fixed outputs start this far in
         for col in plan.columns:
             if col.is_fixed:
-                raw = torch.empty((rows, col.row_bytes), dtype=torch.uint8, device=dev)
+                raw = torch.empty(rows * col.row_bytes + skew, dtype=torch.uint8,
+                                  device=dev)[skew:].view(rows, col.row_bytes)
                 self._fixed_raw[col.name] = raw
                 dtype, shape = col.tensor_view()
                 self.outputs[col.name] = raw.view(dtype).reshape((rows,) + shape)
