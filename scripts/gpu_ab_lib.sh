@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/${TAG:-ab}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BASE=${BASE:-streaming_amd/lib/libmdsx_head.so}
+BASE=${BASE:?set BASE to the other build of libmdsx.so (e.g. one built from an earlier commit)}
 if [ -z "$NOTEST" ]; then
   timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > "$OUT/pytest_gpu.log" 2>&1 || { tail -40 "$OUT/pytest_gpu.log"; exit 1; }
   tail -2 "$OUT/pytest_gpu.log"
