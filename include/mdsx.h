@@ -325,6 +325,12 @@ int mdsx_hash_segments(int algo, uint64_t seed, const uint8_t* data, uint64_t da
  * 16, 16-byte aligned pointers) on `stream`. Not part of the decode path: it measures what a
  * pure stream of the same bytes reaches on the device, reported beside the decode rate. */
 int mdsx_copy_probe(const void* d_src, void* d_dst, uint64_t bytes, void* stream);
+/* The probe's shapes, for measurement: 0 a 256 KiB loop per workgroup (8 loads per lane in
+ * flight, non-temporal); 1 one 4 KiB piece per wave, non-temporal loads and stores (the shape of
+ * the config-B row copy; what mdsx_copy_probe runs); 2 as 1 with plain loads; 3 as 1 with 8 KiB
+ * per wave; 4 as 1 with plain loads and stores. */
+int mdsx_copy_probe_variant(const void* d_src, void* d_dst, uint64_t bytes, int variant,
+                            void* stream);
 /* Host hand-off copy: the same 16-byte streaming kernel storing into PINNED host memory (a
  * device-accessible host pointer) over PCIe, `bytes` a multiple of 16, both pointers 16-byte
  * aligned. A DMA-engine D2H and H2D do not overlap on this platform (they serialise, measured);

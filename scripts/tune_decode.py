@@ -24,7 +24,7 @@ from streaming_amd.synth import fixed_b_batch_on_device, var_c_batch_on_device  
 
 
 def retile(batch: DeviceBatch, plan: Plan) -> DeviceBatch:
-    tr = plan.tile_rows_for(batch.shard_bytes, batch.total_rows)
+    tr = plan.tile_rows_for(int(batch.buffer.numel()), batch.total_rows)
     raw, tile_shard, row0, rows, tiles = _tables(batch.sizes, batch.samples, batch.offsets, tr)
     dev = batch.device
     return DeviceBatch(batch.buffer, torch.from_numpy(raw).to(dev),
@@ -87,7 +87,10 @@ def main():
     copy_dst = torch.empty_like(base_batch.buffer)
     times = {v: [] for v in args.variants}
     times['torch_copy'] = []
+    probes = [0, 1, 2, 3, 4] if os.environ.get('MDSX_PROBES') else []
     times['mdsx_copy_probe'] = []
+    for pv in probes:
+        times[f'probe{pv}'] = []
     from streaming_amd import _native
     lib = _native.lib()
     nprobe = (base_batch.buffer.numel() // 16) * 16
@@ -113,6 +116,14 @@ def main():
         e.record()
         torch.cuda.synchronize()
         times['mdsx_copy_probe'].append(s.elapsed_time(e) / args.iters)
+        for pv in probes:
+            s.record()
+            for _ in range(args.iters):
+                lib.mdsx_copy_probe_variant(base_batch.buffer.data_ptr(), copy_dst.data_ptr(),
+                                            nprobe, pv, stream)
+            e.record()
+            torch.cuda.synchronize()
+            times[f'probe{pv}'].append(s.elapsed_time(e) / args.iters)
     phases = {}
     for v, dec in decs.items():  # sdbg bit 16: the staged decode's cycles per phase, per tile
         dbg = [int(kv[5:], 0) for kv in v.split(',') if kv.startswith('sdbg=')]
@@ -131,7 +142,8 @@ def main():
     res = {}
     for v, ts in times.items():
         ms = float(np.median(ts))
-        nbytes = 2 * base_batch.buffer.numel() if v in ('torch_copy', 'mdsx_copy_probe') else R + W
+        nbytes = 2 * base_batch.buffer.numel() if v in ('torch_copy', 'mdsx_copy_probe') or \
+            v.startswith('probe') else R + W
         res[v] = {'median_ms': ms, 'min_ms': float(np.min(ts)), 'GBps': nbytes / ms / 1e6}
     print(json.dumps({'config': args.config, 'blob': args.blob, 'chars': args.chars, 'R': R,
                       'W': W, 'rows': base_batch.total_rows, 'results': res,

@@ -60,6 +60,7 @@ EXPORTED_SYMBOLS = (
     'mdsx_decode_shards',
     'mdsx_decode_shards_single',
     'mdsx_copy_probe',
+    'mdsx_copy_probe_variant',
     'mdsx_copy_to_host',
     'mdsx_gather_workspace_bytes',
     'mdsx_gather_fixed',
@@ -180,6 +181,8 @@ def _declare(handle: ctypes.CDLL) -> None:
     ]
     handle.mdsx_copy_probe.restype = c_int
     handle.mdsx_copy_probe.argtypes = [vp, vp, c_u64, vp]
+    handle.mdsx_copy_probe_variant.restype = c_int
+    handle.mdsx_copy_probe_variant.argtypes = [vp, vp, c_u64, c_int, vp]
     handle.mdsx_copy_to_host.restype = c_int
     handle.mdsx_copy_to_host.argtypes = [vp, vp, c_u64, vp]
     handle.mdsx_ndarray_meta.restype = c_int

@@ -40,7 +40,8 @@ struct TileRun {
   uint32_t shard;   // batch shard index
   uint32_t r0;      // first sample of the run inside its shard
   uint16_t nrows;
-  uint16_t fast;    // the table fits and every sample of the run passes the file checks
+  uint16_t fast;    // bit 0: the table fits and every sample of the run passes the file checks;
+                    // bit 1: also every sample is at most seg_lim bytes (the lean path takes it)
   uint64_t shard_off;  // batch byte of the shard
 };
 static_assert(sizeof(TileRun) == 48, "TileRun layout");
@@ -78,6 +79,8 @@ struct DevArgs {
   uint32_t stage_debug;  // measurement only (MDSX_TUNE sdbg): parts of the staged decode skipped
   uint32_t run_slots;    // KiB of the streaming decode's per-wave ring (0: not the streaming decode)
   uint32_t rows_bytes;   // LDS stage of the row-parallel decode (0: not the row-parallel decode)
+  uint32_t seg_lim;      // streaming decode, lean path: largest sample it takes (0: lean path off)
+  uint32_t seg_small;    // lean path: bytes per row of the fixed columns of <= 16 bytes
   uint32_t gather_block0[MDSX_MAX_COLUMNS + 1];  // first gather workgroup of each ragged column
   DevCol cols[MDSX_MAX_COLUMNS];
 };

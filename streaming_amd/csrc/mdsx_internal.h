@@ -53,6 +53,8 @@ struct mdsx_plan {
   int64_t run_min = 3072;  // streaming decode for batches whose samples average >= this many bytes
   int run_nt = 0;          // streaming decode: non-temporal ring loads and stores (measured: the
                            // temporal ones let L2 merge the partial stores at run edges)
+  int seg = 0;             // streaming decode: the lean path for clean runs of samples that fit
+                           // the ring (seg_decode_kernel; others take the general path)
   int rows_kb = 0;         // row-parallel decode of shorter samples: LDS stage in KiB (0: off,
                            // -1: sized per batch, rows_tile_rows / rows_stage_bytes)
   int rows_nt = 1;         // row-parallel decode: non-temporal loads and stores (measured faster)

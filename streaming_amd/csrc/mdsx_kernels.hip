@@ -873,6 +873,13 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   a->stage_debug = uint32_t(plan->stage_debug);
   a->run_slots = use_run_decode(plan, b->bytes, b->rows) ? uint32_t(plan->run_slots) : 0u;
   if (a->run_slots) a->stage_bytes = 0;  // the streaming decode takes precedence
+  if (a->run_slots && plan->seg) {
+    // lean path: a sample must fit the ring with a slot to spare (seg_decode_kernel)
+    a->seg_lim = a->run_slots * 1024u - 1024u - 32u;
+    for (int c = 0; c < plan->ncols; ++c)
+      if (plan->cols[c].kind == MDSX_KIND_FIXED && plan->cols[c].row_bytes <= kSmallMax)
+        a->seg_small += uint32_t(plan->cols[c].row_bytes);
+  }
   a->rows_bytes = use_rows_decode(plan, b->bytes, b->rows)
                       ? rows_stage_bytes(plan, b->bytes / b->rows, tr)
                       : 0u;
@@ -966,6 +973,27 @@ __global__ __launch_bounds__(kBlock) void copy_probe_kernel(const uint4* __restr
       const uint64_t i = base + u * kBlock + threadIdx.x;
       if (i < b1) st16<true>(reinterpret_cast<uint64_t>(dst + i), v[u]);
     }
+  }
+}
+
+// The same stream cut per wave: each wave copies its own contiguous kU x 1 KiB (64 lanes x 16 B,
+// kU loads per lane in flight, then kU stores) -- the access shape of the config-B decode's row
+// copy (one 4 KiB row per wave), which outruns the 256 KiB-per-workgroup loop above on MI355X.
+template <int kU, bool kNTLoad, bool kNTStore>
+__global__ __launch_bounds__(kBlock) void copy_wave_kernel(const uint4* __restrict__ src,
+                                                           uint4* __restrict__ dst, uint64_t n) {
+  const uint64_t w = uint64_t(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+  const uint64_t b0 = w * (64 * kU) + (threadIdx.x & 63);
+  uint4 v[kU];
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const uint64_t i = b0 + 64 * u;
+    if (i < n) v[u] = ld16<kNTLoad>(src + i);
+  }
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const uint64_t i = b0 + 64 * u;
+    if (i < n) st16<kNTStore>(reinterpret_cast<uint64_t>(dst + i), v[u]);
   }
 }
 
@@ -1599,17 +1627,46 @@ int mdsx_ndarray_shapes(const uint8_t* values, const int64_t* offsets, uint64_t 
   return hip_check(hipGetLastError(), "ndarray_meta_kernel launch");
 }
 
-int mdsx_copy_probe(const void* d_src, void* d_dst, uint64_t bytes, void* stream) {
+int mdsx_copy_probe_variant(const void* d_src, void* d_dst, uint64_t bytes, int variant,
+                            void* stream) {
   if (!d_src || !d_dst || (bytes & 15) || (reinterpret_cast<uint64_t>(d_src) & 15) ||
       (reinterpret_cast<uint64_t>(d_dst) & 15))
     return mdsx::fail(MDSX_E_ARG, "mdsx_copy_probe: 16-byte aligned pointers and size required");
   const uint64_t n = bytes / 16;
   if (n == 0) return MDSX_OK;
-  const unsigned grid = unsigned((n + kProbeBlock - 1) / kProbeBlock);
-  hipLaunchKernelGGL(copy_probe_kernel, dim3(grid), dim3(kBlock), 0,
-                     static_cast<hipStream_t>(stream), static_cast<const uint4*>(d_src),
-                     static_cast<uint4*>(d_dst), n);
-  return hip_check(hipGetLastError(), "copy_probe_kernel launch");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const uint4* src = static_cast<const uint4*>(d_src);
+  uint4* dst = static_cast<uint4*>(d_dst);
+  const uint64_t per4 = uint64_t(kBlock / 64) * 64 * 4, per8 = per4 * 2;
+  switch (variant) {
+    case 0:
+      hipLaunchKernelGGL(copy_probe_kernel, dim3(unsigned((n + kProbeBlock - 1) / kProbeBlock)),
+                         dim3(kBlock), 0, s, src, dst, n);
+      break;
+    case 1:
+      hipLaunchKernelGGL((copy_wave_kernel<4, true, true>), dim3(unsigned((n + per4 - 1) / per4)),
+                         dim3(kBlock), 0, s, src, dst, n);
+      break;
+    case 2:
+      hipLaunchKernelGGL((copy_wave_kernel<4, false, true>), dim3(unsigned((n + per4 - 1) / per4)),
+                         dim3(kBlock), 0, s, src, dst, n);
+      break;
+    case 3:
+      hipLaunchKernelGGL((copy_wave_kernel<8, true, true>), dim3(unsigned((n + per8 - 1) / per8)),
+                         dim3(kBlock), 0, s, src, dst, n);
+      break;
+    case 4:
+      hipLaunchKernelGGL((copy_wave_kernel<4, false, false>),
+                         dim3(unsigned((n + per4 - 1) / per4)), dim3(kBlock), 0, s, src, dst, n);
+      break;
+    default:
+      return mdsx::fail(MDSX_E_ARG, "mdsx_copy_probe_variant: variant 0..4");
+  }
+  return hip_check(hipGetLastError(), "copy probe launch");
+}
+
+int mdsx_copy_probe(const void* d_src, void* d_dst, uint64_t bytes, void* stream) {
+  return mdsx_copy_probe_variant(d_src, d_dst, bytes, 1, stream);
 }
 
 int mdsx_copy_to_host(const void* d_src, void* h_dst, uint64_t bytes, void* stream) {

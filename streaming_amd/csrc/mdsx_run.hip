@@ -255,32 +255,22 @@ __device__ __forceinline__ bool copy_segment(Stream& st, const lds_u8* ring, uin
   return utf8 ? __any(bad) : false;
 }
 
+// The general path of a wave's run: any run the scan pass described (a sample failing the file
+// checks, or larger than the ring). `wl`: the wave's LDS (ring, mirror, offsets, flags).
 template <int S, bool kNT>
-__global__ __launch_bounds__(kRunBlock, 7) void run_decode_kernel(const DevArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  __shared__ DevCol s_cols[MDSX_MAX_COLUMNS];
-  const int t = threadIdx.x, lane = t & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  // the column table in LDS: kernel-argument fields indexed by a loop variable compile to vector
-  // loads, whose waits would also wait for the ring's loads and the stores in flight
-  for (int c = t; c < a.ncols; c += kRunBlock) s_cols[c] = a.cols[c];
-  __syncthreads();
-  const MDSX_L DevCol* cols = (const MDSX_L DevCol*)s_cols;
-  const uint32_t tile = blockIdx.x * kRunWaves + uint32_t(wave);
-  if (tile >= a.ntiles) return;  // wave-uniform; no barrier below
+__device__ __forceinline__ void run_body(const DevArgs& a, const MDSX_L DevCol* cols,
+                                         uint32_t tile, const TileRun& r, uint8_t* wl, int lane) {
   const int TR = a.tile_rows;
   const int ncols = a.ncols, nvar = a.nvar;
-  uint8_t* wl = smem + size_t(wave) * run_wave_lds(S, TR, nvar);
   const lds_u8* ring = (const lds_u8*)wl;
   MDSX_L uint32_t* obuf = (MDSX_L uint32_t*)(wl + S * 1024 + kMirror);  // [nvar][TR]
   MDSX_L uint8_t* fbuf = (MDSX_L uint8_t*)(wl + S * 1024 + kMirror + nvar * TR * 4);  // [nvar][TR]
   const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(
       static_cast<uint32_t>(reinterpret_cast<uintptr_t>((const MDSX_L uint8_t*)wl)));
 
-  // the run as the scan pass described it (its header check too): one load, then the run's
-  // first S KiB in flight at once, its offsets-table slice and output bases loaded meanwhile
-  const TileRun r = a.tile_run[tile];
-  const bool fast = r.fast != 0;
+  // the run as the scan pass described it (its header check too): the run's first S KiB in
+  // flight at once, its offsets-table slice and output bases loaded meanwhile
+  const bool fast = (r.fast & 1) != 0;
   const uint64_t batch = reinterpret_cast<uint64_t>(a.batch);
   const uint64_t shard = batch + (r.offs - 4ull - 4ull * r.r0);  // the shard file's first byte
   Stream st;
@@ -425,6 +415,301 @@ __global__ __launch_bounds__(kRunBlock, 7) void run_decode_kernel(const DevArgs 
   }
 }
 
+template <int S, bool kNT>
+__global__ __launch_bounds__(kRunBlock, 7) void run_decode_kernel(const DevArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  __shared__ DevCol s_cols[MDSX_MAX_COLUMNS];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  // the column table in LDS: kernel-argument fields indexed by a loop variable compile to vector
+  // loads, whose waits would also wait for the ring's loads and the stores in flight
+  for (int c = t; c < a.ncols; c += kRunBlock) s_cols[c] = a.cols[c];
+  __syncthreads();
+  const MDSX_L DevCol* cols = (const MDSX_L DevCol*)s_cols;
+  const uint32_t tile = blockIdx.x * kRunWaves + uint32_t(wave);
+  if (tile >= a.ntiles) return;  // wave-uniform; no barrier below
+  uint8_t* wl = smem + size_t(wave) * run_wave_lds(S, a.tile_rows, a.nvar);
+  run_body<S, kNT>(a, cols, tile, a.tile_run[tile], wl, lane);
+}
+
+// ---------------------------------------------------------------------------------------------
+// The lean path (seg_decode_kernel) for the common run: every sample passes the file checks and
+// fits the ring with a slot to spare (TileRun.fast bit 1, set by the scan pass). Per sample the
+// wave waits ONCE, for all of the sample's bytes, and then has nothing left to wait for:
+//   * the column geometry is lane-parallel -- lane c reads column c's size head from the ring,
+//     a wave prefix sum places every column in the sample, one ballot checks the boundaries
+//     (MDSReader.decode_sample, mds/reader.py:111-125);
+//   * fixed columns of <= 16 bytes (the `int` / scalar columns) go to an LDS stage, one lane per
+//     column, and leave the wave once per run, one row per lane;
+//   * every wider column is copied destination-major (lane k: 16-byte output chunk k, one
+//     unaligned ds_read_b128 from the ring, one whole-chunk store), the partly filled last chunk
+//     carried into the next sample's first chunk; str values checked for strict UTF-8 on the same
+//     registers (bytes.decode('utf-8'), encodings.py:80-81).
+// Other runs take the general path (run_body). A sample failing the boundary check is reported
+// (MDSX_E_BOUNDS) and decodes as empty ragged values and zeroed fixed values, the scan pass's
+// zero-length rule.
+
+// per-wave LDS of the lean path: the general path's, then the staged small fixed columns
+__host__ __device__ __forceinline__ uint32_t seg_wave_lds(int S, int TR, int nvar,
+                                                          uint32_t small) {
+  return run_wave_lds(S, TR, nvar) + ((small * uint32_t(TR) + 15u) & ~15u);
+}
+
+// u32 inclusive prefix sum over lanes [0, n) (n <= 64 wave-uniform; other lanes: garbage)
+__device__ __forceinline__ uint32_t wave_incl_u32(uint32_t x, int lane, int n) {
+  for (int o = 1; o < n; o <<= 1) {
+    const uint32_t y = uint32_t(__shfl_up(int(x), o));
+    if (lane >= o) x += y;
+  }
+  return x;
+}
+
+// bytes [0, h) of `lo` and [h, 16) of `hi` (h wave-uniform, 0..16)
+__device__ __forceinline__ uint4 splice_lo(const uint4 lo, const uint4 hi, uint32_t h) {
+  const uint64_t m0 = h >= 8 ? ~0ull : (1ull << (8 * h)) - 1ull;
+  const uint64_t m1 = h <= 8 ? 0ull : h >= 16 ? ~0ull : (1ull << (8 * (h - 8))) - 1ull;
+  const uint32_t w0 = uint32_t(m0), w1 = uint32_t(m0 >> 32), w2 = uint32_t(m1),
+                 w3 = uint32_t(m1 >> 32);
+  return make_uint4((lo.x & w0) | (hi.x & ~w0), (lo.y & w1) | (hi.y & ~w1),
+                    (lo.z & w2) | (hi.z & ~w2), (lo.w & w3) | (hi.w & ~w3));
+}
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+// n (1..16) bytes of `v` to LDS at p (p aligned to the largest power of two dividing n)
+__device__ __forceinline__ void lds_put(MDSX_L uint8_t* p, const uint4 v, uint32_t n) {
+  if (n == 8) {
+    *(MDSX_L u32x2*)p = u32x2{v.x, v.y};
+  } else if (n == 4) {
+    *(MDSX_L uint32_t*)p = v.x;
+  } else if (n == 16) {
+    *(MDSX_L u32x4*)p = u32x4{v.x, v.y, v.z, v.w};
+  } else {
+    for (uint32_t k = 0; k < n; ++k) p[k] = uint8_t(byte_of(v, int(k)));
+  }
+}
+
+// n (1..16) bytes from LDS at p to global memory at q (both aligned as in lds_put)
+__device__ __forceinline__ void lds_out(const MDSX_L uint8_t* p, uint8_t* q, uint32_t n) {
+  if (n == 8) {
+    *(MDSX_G u32x2*)gp((u32x2*)q) = *(const MDSX_L u32x2*)p;
+  } else if (n == 4) {
+    *gp((uint32_t*)q) = *(const MDSX_L uint32_t*)p;
+  } else if (n == 16) {
+    const u32x4 v = *(const MDSX_L u32x4*)p;
+    *(MDSX_G u32x4*)gp((u32x4*)q) = v;
+  } else {
+    for (uint32_t k = 0; k < n; ++k) *gp(q + k) = p[k];
+  }
+}
+
+// One value of a wide column, all of its stream bytes landed: output bytes [d, d + len) (relative
+// to `base`) from stream bytes [p, p + len) (zeros when `zero`). `cst`: the run's first output
+// byte of the column (bytes below it belong to the run before). `carry` (uniform): in, the partly
+// filled chunk at d & ~15; out, the one at (d + len) & ~15. Returns (utf8) whether the value is
+// not well-formed UTF-8 (wave-uniform).
+template <int S, bool kNT>
+__device__ __forceinline__ bool seg_copy(const lds_u8* ring, uint64_t base, uint32_t cst,
+                                         uint32_t d, uint32_t len, uint32_t p, bool utf8,
+                                         bool zero, uint4& carry, uint32_t& ops, int lane) {
+  const uint32_t head = d & 15u, dbeg = d - head, dend = d + len;
+  const uint32_t nch = (dend - dbeg + 15u) >> 4;  // chunks touched
+  const uint32_t nfull = (dend - dbeg) >> 4;      // chunks completed by this value
+  const uint32_t tail = dend & 15u;
+  const bool shared0 = dbeg < cst;  // the run's first chunk of the column, shared with the run before
+  const uint32_t s0 = p - head;     // stream byte of chunk 0's byte 0 (bytes below p: the carry's)
+  const uint64_t out = base + dbeg;
+  const uint4 z4 = make_uint4(0, 0, 0, 0);
+  bool bad = false;
+  uint32_t prev_w = 0;
+  uint4 last = carry;
+  for (uint32_t g = 0; g < nch; g += 64) {  // wave-uniform
+    const uint32_t kk = g + uint32_t(lane);
+    uint4 val = zero ? z4 : ring16<S>(ring, s0 + 16u * kk);
+    if (g == 0 && head && lane == 0) val = splice_lo(carry, val, head);
+    const bool skip0 = shared0 && g == 0;
+    if (kk < nfull && !(skip0 && lane == 0)) st16<kNT>(out + 16ull * kk, val);
+    if (min(nfull, g + 64u) > g + (skip0 ? 1u : 0u)) ++ops;  // that store was issued
+    if (skip0 && nfull > 0) wave_edge_store(val, 0, out, base + cst, out + 16, lane);
+    if (utf8) {
+      // this value's bytes only: the carried ones and those past its end zeroed
+      uint4 vout = kk < nch ? val : z4;
+      if (g == 0 && head && lane == 0) vout = splice_lo(z4, vout, head);
+      if (tail && kk == nch - 1) vout = splice_lo(vout, z4, tail);
+      const uint32_t any8 = (vout.x | vout.y | vout.z | vout.w) & 0x80808080u;
+      if (__any(any8 != 0) || hi_c0(prev_w)) {  // a byte >= 0x80 (or a sequence open before)
+        uint32_t pw = uint32_t(__shfl_up(int(vout.w), 1));
+        if (lane == 0) pw = prev_w;
+        if (kk < nch) bad |= utf8_chunk_bad(vout, pw, kk == nch - 1);
+      }
+      prev_w = __builtin_amdgcn_readlane(vout.w, 63);
+    }
+    if (tail && nch - 1 - g < 64u) last = readlane4(val, int(nch - 1 - g));
+  }
+  carry = last;
+  return utf8 ? __any(bad) != 0 : false;
+}
+
+template <int S, bool kNT>
+__global__ __launch_bounds__(kRunBlock, 4) void seg_decode_kernel(const DevArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  __shared__ DevCol s_cols[MDSX_MAX_COLUMNS];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  for (int c = t; c < a.ncols; c += kRunBlock) s_cols[c] = a.cols[c];
+  __syncthreads();
+  const MDSX_L DevCol* cols = (const MDSX_L DevCol*)s_cols;
+  const uint32_t tile = blockIdx.x * kRunWaves + uint32_t(wave);
+  if (tile >= a.ntiles) return;  // wave-uniform; no barrier below
+  const int TR = a.tile_rows;
+  const int ncols = a.ncols, nvar = a.nvar;
+  uint8_t* wl = smem + size_t(wave) * seg_wave_lds(S, TR, nvar, a.seg_small);
+  const TileRun r = a.tile_run[tile];
+  if (!(r.fast & 2)) {
+    run_body<S, kNT>(a, cols, tile, r, wl, lane);
+    return;
+  }
+  const lds_u8* ring = (const lds_u8*)wl;
+  MDSX_L uint32_t* obuf = (MDSX_L uint32_t*)(wl + S * 1024 + kMirror);  // [nvar][TR]
+  MDSX_L uint8_t* fbuf = (MDSX_L uint8_t*)(wl + S * 1024 + kMirror + nvar * TR * 4);  // [nvar][TR]
+  MDSX_L uint8_t* sbuf = (MDSX_L uint8_t*)(wl + run_wave_lds(S, TR, nvar));  // small columns
+  const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((const MDSX_L uint8_t*)wl)));
+
+  // the run's bytes: one range starting on a 128-byte line, its first S KiB in flight at once
+  const uint64_t batch = reinterpret_cast<uint64_t>(a.batch);
+  const uint64_t shard = batch + (r.offs - 4ull - 4ull * r.r0);  // the shard file's first byte
+  const uint64_t sbase = (batch + r.stream) & ~uint64_t(127);
+  Stream st;
+  st.base = reinterpret_cast<const uint4*>(sbase);
+  st.nq = uint32_t((batch + r.stream + r.bytes - sbase + 15) >> 4);
+  st.nslots = (st.nq + 63) >> 6;
+  st.issued = 0;
+  st.ops = 0;
+  st.op_at = 0;
+  st.mirrored = 0xffffffffu;
+  st.landed = 0;
+  pump<S, kNT>(st, ring_lds, 0, lane);
+  const int n = int(r.nrows);
+  const uint64_t row0 = r.row0;
+  // lane j holds offsets[r0 + j] (j <= n)
+  const uint32_t ob = lane <= n ? *reinterpret_cast<const uint32_t*>(a.batch + r.offs + 4u * lane)
+                                : 0u;
+
+  // column facts and cursors, lane-distributed (lane c: column c)
+  int vi = -1;
+  uint32_t rb = 0, meta = 0, cur = 0;
+  uint64_t base = 0;
+  bool small = false, wide = false;
+  if (lane < ncols) {
+    const MDSX_L DevCol& col = cols[lane];
+    vi = col.var_index;
+    rb = col.row_bytes;
+    const uint64_t data = reinterpret_cast<uint64_t>(col.data);
+    uint64_t first = data + row0 * rb;
+    bool skip = false;
+    if (vi >= 0) {
+      const uint64_t off = uint64_t(a.tile_prefix[uint64_t(vi) * a.nscan + tile]);
+      first = data + off;
+      if (off + uint64_t(a.tile_total[uint64_t(vi) * a.nscan + tile]) > col.capacity) {
+        report_decode(a, MDSX_E_CAPACITY, int(r.shard), int(r.r0), lane);
+        skip = true;  // this run writes nothing of the column
+      }
+      meta = uint32_t(vi + 1) & 255u;
+      if (col.kind == MDSX_KIND_STR && col.flags != nullptr) meta |= 1u << 8;
+    }
+    small = vi < 0 && rb <= uint32_t(kSmallMax);
+    wide = !small && !skip;
+    base = first & ~uint64_t(15);
+    cur = uint32_t(first & 15);
+  }
+  const uint32_t cst = cur;
+  uint4 carry = make_uint4(0, 0, 0, 0);
+  const uint32_t ssz = small ? rb * uint32_t(TR) : 0u;
+  const uint32_t soff = ((wave_incl_u32(ssz, lane, ncols) - ssz));  // stage offset of the column
+  const uint64_t wide_mask = __ballot(wide);
+  const uint64_t small_mask = __ballot(small);
+  const uint32_t hv = 4u * uint32_t(nvar);
+
+  for (int j = 0; j < n; ++j) {  // wave-uniform
+    const uint32_t b = uint32_t(__builtin_amdgcn_readlane(int(ob), j));
+    const uint32_t e = uint32_t(__builtin_amdgcn_readlane(int(ob), j + 1));
+    const uint32_t size = e - b;
+    const uint32_t sp = uint32_t(shard + b - sbase);  // stream position of the sample
+    ensure<S, kNT>(st, ring, ring_lds, sp, sp + size + 15u, lane);  // ALL of the sample's bytes
+    // column geometry, lane c: size head (ragged) or row size (fixed), place by prefix sum
+    uint32_t len = 0;
+    if (lane < ncols) len = vi >= 0 ? ring_u32<S>(ring, sp + 4u * uint32_t(vi)) : rb;
+    const bool over = lane < ncols && len > size;
+    const uint32_t lc = over ? 0u : len;
+    const uint32_t incl = wave_incl_u32(lc, lane, ncols);
+    const uint32_t total = uint32_t(__builtin_amdgcn_readlane(int(incl), ncols - 1));
+    const bool ok = !__any(over) && hv <= size && total <= size - hv;
+    if (!ok && lane == 0) report_decode(a, MDSX_E_BOUNDS, int(r.shard), int(r.r0 + j), -1);
+    const uint32_t pos = sp + hv + incl - lc;  // stream position of the column's value
+    const uint32_t clen = ok ? len : (vi >= 0 ? 0u : rb);
+    if (small) lds_put(sbuf + soff + uint32_t(j) * rb, ok ? ring16<S>(ring, pos) : make_uint4(0, 0, 0, 0), rb);
+    if (vi >= 0) {
+      obuf[vi * TR + j] = cur;
+      if ((meta >> 8) & 1u) fbuf[vi * TR + j] = 0;
+    }
+    // the wide columns, in column order = stream order
+    uint64_t m = wide_mask;
+    while (m) {
+      const int c = __builtin_ctzll(m);
+      m &= m - 1;
+      const uint32_t l = uint32_t(__builtin_amdgcn_readlane(int(clen), c));
+      if (l == 0) continue;
+      const uint32_t d = uint32_t(__builtin_amdgcn_readlane(int(cur), c));
+      const uint32_t p = uint32_t(__builtin_amdgcn_readlane(int(pos), c));
+      const uint32_t mc = uint32_t(__builtin_amdgcn_readlane(int(meta), c));
+      const uint32_t cs = uint32_t(__builtin_amdgcn_readlane(int(cst), c));
+      uint4 cy = (d & 15u) ? readlane4(carry, c) : make_uint4(0, 0, 0, 0);
+      const bool utf8 = (mc >> 8) & 1u;
+      const bool bad = seg_copy<S, kNT>(ring, readlane64(base, c), cs, d, l, p, utf8, !ok, cy,
+                                        st.ops, lane);
+      if (lane == c) {
+        cur = d + l;
+        carry = cy;
+      }
+      if (bad && lane == 0) fbuf[(int(mc & 255u) - 1) * TR + j] = 1;
+      pump<S, kNT>(st, ring_lds, (p + l) >> 10, lane);  // the bytes before p + l are done
+    }
+  }
+  // the partly filled last chunk of every wide column (bytes [max(cst, chunk), cur))
+  for (uint64_t m = wide_mask; m; m &= m - 1) {
+    const int c = __builtin_ctzll(m);
+    const uint32_t cu = uint32_t(__builtin_amdgcn_readlane(int(cur), c));
+    const uint32_t cs = uint32_t(__builtin_amdgcn_readlane(int(cst), c));
+    if ((cu & 15u) == 0) continue;
+    const uint32_t C = cu & ~15u;
+    const uint32_t lo = max(cs, C);
+    if (lo >= cu) continue;
+    const uint64_t bs = readlane64(base, c);
+    wave_edge_store(carry, c, bs + C, bs + lo, bs + cu, lane);
+  }
+  // the staged small fixed columns, one row per lane
+  for (uint64_t m = small_mask; m; m &= m - 1) {
+    const int c = __builtin_ctzll(m);
+    const uint32_t w = cols[c].row_bytes;
+    const uint32_t so = uint32_t(__builtin_amdgcn_readlane(int(soff), c));
+    if (lane < n)
+      lds_out(sbuf + so + uint32_t(lane) * w,
+              static_cast<uint8_t*>(cols[c].data) + (row0 + uint64_t(lane)) * w, w);
+  }
+  // the run's ragged offsets and str flags
+  for (int c = 0; c < ncols; ++c) {
+    const MDSX_L DevCol& col = cols[c];
+    const int v = col.var_index;
+    if (v < 0) continue;
+    // offsets[row] = (base - data) + the row's position relative to base
+    const int64_t obase = int64_t(readlane64(base, c) - reinterpret_cast<uint64_t>(col.data));
+    if (lane < n) *gp(col.offsets + row0 + lane) = obase + int64_t(obuf[v * TR + lane]);
+    if (col.kind == MDSX_KIND_STR && col.flags && lane < n)
+      *gp(col.flags + row0 + lane) = fbuf[v * TR + lane];
+  }
+}
+
 }  // namespace
 
 int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
@@ -432,6 +717,33 @@ int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
   const size_t lds = size_t(kRunWaves) * run_wave_lds(a.run_slots, a.tile_rows, a.nvar);
   if (a.tile_rows > kRunMaxRows)
     return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode tiles hold at most 32 rows");
+  if (a.seg_lim) {
+    const size_t slds =
+        size_t(kRunWaves) * seg_wave_lds(a.run_slots, a.tile_rows, a.nvar, a.seg_small);
+    if (slds > 160 * 1024)
+      return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode LDS exceeds 160 KiB");
+#define MDSX_SEG_CASE(S, NT)                                                              \
+  if (a.run_slots == S && bool(plan->run_nt) == NT) {                                     \
+    if (slds > 64 * 1024) {                                                               \
+      const int rc = hip_check(                                                           \
+          hipFuncSetAttribute(reinterpret_cast<const void*>(seg_decode_kernel<S, NT>),    \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, int(slds)),     \
+          "hipFuncSetAttribute");                                                         \
+      if (rc != MDSX_OK) return rc;                                                       \
+    }                                                                                     \
+    mdsx::set_last_kernel("seg_decode_kernel<" #S ", " #NT ">");                         \
+    hipLaunchKernelGGL((seg_decode_kernel<S, NT>), dim3(grid), dim3(kRunBlock), slds, s, a); \
+    return hip_check(hipGetLastError(), "seg_decode_kernel launch");                      \
+  }
+    MDSX_SEG_CASE(4, true)
+    MDSX_SEG_CASE(4, false)
+    MDSX_SEG_CASE(8, true)
+    MDSX_SEG_CASE(8, false)
+    MDSX_SEG_CASE(16, true)
+    MDSX_SEG_CASE(16, false)
+#undef MDSX_SEG_CASE
+    return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode ring of 4, 8 or 16 KiB");
+  }
 #define MDSX_RUN_CASE(S, NT)                                                              \
   if (a.run_slots == S && bool(plan->run_nt) == NT) {                                     \
     if (lds > 64 * 1024) {                                                                \

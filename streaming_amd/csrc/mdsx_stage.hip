@@ -469,10 +469,13 @@ __global__ __launch_bounds__(kBlock) void stage_totals_kernel(const DevArgs a) {
   // the run records of the streaming decode (tiles <= 32 rows) and the row-parallel decode
   if ((a.run_slots && TR < 64) || a.rows_bytes) {
     const uint64_t bad = __ballot(range_bad);
-    bool tile_bad;
+    // samples too large for the streaming decode's lean path (its ring holds a whole sample)
+    const uint64_t big = __ballot(in_tile && !range_bad && a.seg_lim && e - b > a.seg_lim);
+    bool tile_bad, tile_big = false;
     if (TR <= 64) {
       const uint64_t seg = TR == 64 ? ~0ull : ((1ull << TR) - 1) << (lane & ~(TR - 1));
       tile_bad = (bad & seg) != 0;  // this tile's lanes
+      tile_big = (big & seg) != 0;
     } else {  // a tile spans TR / 64 waves
       if (lane == 0) s_bad[wave] = bad != 0;
       __syncthreads();
@@ -483,7 +486,7 @@ __global__ __launch_bounds__(kBlock) void stage_totals_kernel(const DevArgs a) {
     if (tile_ok && t % TR == 0) {
       TileRun r;
       const bool fast = v.table_ok && v.nrows > 0 && !tile_bad;
-      r.fast = fast ? 1 : 0;
+      r.fast = fast ? (a.seg_lim && !tile_big ? 3 : 1) : 0;
       r.stream = v.d.offset + (fast ? v.offs[v.r0] : 0u);
       r.bytes = fast ? v.offs[v.r0 + v.nrows] - v.offs[v.r0] : 0u;
       r.offs = v.d.offset + 4ull + 4ull * v.r0;

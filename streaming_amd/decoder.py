@@ -243,7 +243,8 @@ def make_batch(plan: Plan,
     sizes = [int(x) for x in sizes]
     offsets, total = _layout(sizes)
     buffer = torch.zeros(total, dtype=torch.uint8, device=device)
-    tr = plan.tile_rows_for(sum(sizes), sum(int(n) for n in samples))
+    # tiles sized from the buffer's bytes, the batch->bytes the C side picks the decode from
+    tr = plan.tile_rows_for(total, sum(int(n) for n in samples))
     raw, tile_shard, row0, rows, tiles = _tables(sizes, samples, offsets, tr)
     descs = torch.from_numpy(raw).to(device)
     tiles_t = torch.from_numpy(tile_shard).to(device) if tiles else torch.zeros(
@@ -359,10 +360,21 @@ def ndarray_meta(col: 'RaggedColumn', dtype_id: int = 0) -> NdarrayMeta:
 
 @dataclass
 class DecodedBatch:
-    """Decoded columns of a :class:`DeviceBatch` (device tensors)."""
+    """Decoded columns of a :class:`DeviceBatch` (device tensors). ``stream``: the stream the
+    decode ran on (None: the gathers' own stream, e.g. a gather's output)."""
     columns: dict[str, Union[torch.Tensor, RaggedColumn]]
     rows: int
     row0: list[int] = field(default_factory=list)
+    stream: Optional[torch.cuda.Stream] = None
+
+    def tensors(self) -> list[torch.Tensor]:
+        out = []
+        for col in self.columns.values():
+            if isinstance(col, RaggedColumn):
+                out += [t for t in (col.values, col.offsets, col.flags) if t is not None]
+            else:
+                out.append(col)
+        return out
 
     def __getitem__(self, name: str) -> Union[torch.Tensor, RaggedColumn]:
         return self.columns[name]
@@ -376,6 +388,7 @@ class DecodedBatch:
         first = next(iter(self.columns.values()))
         dev = first.values.device if isinstance(first, RaggedColumn) else first.device
         _require_device_columns([self])
+        _on_current_stream([self], dev)
         idx = torch.as_tensor(ids, dtype=torch.int64).to(dev).reshape(-1)
         idx = idx[idx != -1].contiguous()
         m = int(idx.numel())
@@ -433,6 +446,22 @@ def _require_device_columns(batches: Sequence['DecodedBatch']) -> None:
                                      'the device gather reads decoded device tensors only')
 
 
+def _on_current_stream(batches: Sequence['DecodedBatch'], dev: torch.device) -> None:
+    """A gather reads its sources on the current stream. A source decoded on another stream:
+    the current stream first waits for that stream's work (the decode), and its tensors are
+    marked in use by the current stream (``record_stream``), so that freeing them -- a cache
+    eviction -- cannot hand their memory to a new allocation on the decode's stream while the
+    gather still reads it."""
+    cur = torch.cuda.current_stream(dev)
+    for b in batches:
+        s = b.stream
+        if s is None or s == cur:
+            continue
+        cur.wait_stream(s)
+        for t in b.tensors():
+            t.record_stream(cur)
+
+
 def gather_sources(sources: Sequence[DecodedBatch], src: np.ndarray, rows: np.ndarray,
                    check: bool = True) -> DecodedBatch:
     """Output row k = row ``rows[k]`` of ``sources[src[k]]`` (decoded shards of one schema), for
@@ -452,6 +481,7 @@ def gather_sources(sources: Sequence[DecodedBatch], src: np.ndarray, rows: np.nd
     names = list(sources[0].columns)
     first = sources[0].columns[names[0]]
     dev = first.values.device if isinstance(first, RaggedColumn) else first.device
+    _on_current_stream(sources, dev)
     # one upload: [ncols][nsrc] mdsx_gather_src records, then the packed ids
     table = np.zeros((len(names), nsrc, 4), np.uint64)
     for j, b in enumerate(sources):
@@ -521,7 +551,8 @@ def gather_sources(sources: Sequence[DecodedBatch], src: np.ndarray, rows: np.nd
             cap, offs[name].data_ptr(), flags.data_ptr() if flags is not None else None,
             ws.data_ptr() + ragged.index(name) * wsb, wsb, stream), 'mdsx_gather_ragged_copy_multi')
         out[name] = RaggedColumn(vals[:cap], offs[name], flags)
-    # (a source freed after this returns is reused in stream order: these kernels come first)
+    # (a source freed after this returns is reused in stream order: these kernels come first;
+    # sources of another stream were marked in use by this one, _on_current_stream)
     return DecodedBatch({name: out[name] for name in names}, m)
 
 
@@ -716,7 +747,8 @@ class BatchDecoder:
         between the scan and the decode kernel, and after the decode kernel (kernel timing; a
         single-pass decode records the first two together).
         """
-        stream = torch.cuda.current_stream(self.device).cuda_stream
+        self._stream = torch.cuda.current_stream(self.device)
+        stream = self._stream.cuda_stream
         self._fill_outs()
         if self.single and self.plan.num_var:
             return self._run_single(stream, events)
@@ -758,7 +790,8 @@ class BatchDecoder:
                 cap = self._capacities.get(col.name, 0)
                 out = RaggedColumn(out.values[:cap], out.offsets, out.flags)
             cols[col.name] = out
-        return DecodedBatch(cols, self.batch.total_rows, list(self.batch.row0))
+        return DecodedBatch(cols, self.batch.total_rows, list(self.batch.row0),
+                            getattr(self, '_stream', None))
 
     @property
     def capacities(self) -> dict[str, int]:

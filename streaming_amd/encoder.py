@@ -94,7 +94,7 @@ class EncodedBatch:
         """The encoded shards as a decode batch of ``plan`` (same buffer, the tile table rebuilt
         for the decoder's tile size)."""
         b = self.batch
-        tr = plan.tile_rows_for(sum(b.sizes), sum(b.samples))
+        tr = plan.tile_rows_for(int(b.buffer.numel()), sum(b.samples))  # C: batch->bytes
         if b.tile_rows == tr:
             return b
         raw, tile_shard, row0, rows, tiles = _tables(b.sizes, b.samples, b.offsets, tr)

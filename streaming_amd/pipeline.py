@@ -181,7 +181,7 @@ class ShardPipeline:
 
     def _batch(self, slot: _Slot, group, sizes, offsets, total) -> DeviceBatch:
         samples = [s.samples for s in group]
-        tr = self.plan.tile_rows_for(sum(sizes), sum(samples))
+        tr = self.plan.tile_rows_for(total, sum(samples))  # = the C side's batch->bytes
         raw, tile_shard, row0, rows, tiles = _tables(sizes, samples, offsets, tr)
         dev = self.device
         # small tables: pinned + async on the compute stream (no host wait on the device)

@@ -460,7 +460,7 @@ class MDSReader(JointReader):
             with self._lock:
                 if entry.host is None:
                     entry.host = _HostShard(self.plan, entry.decoded)
-                    self.cache.update(self._key, entry, entry.nbytes + entry.host.nbytes)
+                    self.cache.set_host_bytes(self._key, entry.host.nbytes)
                 host = entry.host
         return self._materialize(host, idx)
 

@@ -344,6 +344,21 @@ def gen_zstd():
     }
 
 
+def gen_zstd_xxh3():
+    # ragged columns, zstd, and the xxh3 digests the pipeline validates on the device
+    rng = np.random.default_rng(6)
+    samples = []
+    for _ in range(120):
+        blob = rng.integers(0, 8, int(rng.integers(500, 3000))).astype(np.uint8).tobytes()
+        samples.append({'n': int(rng.integers(-2**62, 2**62)), 'b': blob,
+                        's': random_text(rng, 5, 40)})
+    return {'n': 'int', 'b': 'bytes', 's': 'str'}, samples, {
+        'size_limit': 1 << 17,
+        'compression': 'zstd',
+        'hashes': ['xxh128', 'xxh3_64']
+    }
+
+
 def gen_wide():
     rng = np.random.default_rng(6)
     cols = {}
@@ -425,6 +440,7 @@ def main() -> None:
         'images': (gen_images, True),
         'bad_utf8': (gen_bad_utf8, True),
         'zstd': (gen_zstd, False),
+        'zstd_xxh3': (gen_zstd_xxh3, False),
         'wide': (gen_wide, False),
     }
     manifest_path = os.path.join(HERE, 'manifest.json')

@@ -37,6 +37,12 @@ MODES = {
     'run': 'run=8,rmin=0',  # the streaming decode (mdsx_run.hip) whatever the sample size
     'run4': 'run=4,rmin=0,rkb=4',  # small ring, 1-2-row tiles
     'run16': 'run=16,rmin=0,rkb=1024',  # 32-row tiles
+    # the streaming decode's lean path (seg_decode_kernel) for runs whose samples fit its ring,
+    # the general path for the others, in the same launch
+    'seg4': 'run=4,seg=1,rmin=0,rkb=4',
+    'seg8': 'run=8,seg=1,rmin=0',
+    'seg16': 'run=16,seg=1,rmin=0,rkb=1024',
+    'seg8_nt': 'run=8,seg=1,rmin=0,rnt=1',
     'rows': 'rows=32,rmin=1000000000',  # the row-parallel decode (mdsx_rows.hip) for every size
     'rows_auto': 'rows=-1,rmin=1000000000',  # ... its tiles and stage sized per batch
     'rows_small': 'rows=2,rmin=1000000000',  # a 2 KiB stage: windows and HBM-direct samples

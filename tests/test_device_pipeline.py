@@ -129,20 +129,37 @@ def test_plugin_stream_get_item(name):
     assert k == len(expected)
 
 
-@pytest.mark.parametrize('algo', ['xxh64', 'sha1'])
-def test_pipeline_validate_hash(algo):
-    """validate_hash as Stream._prepare_shard_part (stream.py:401-411): xxh64 on the device over
-    the resident batch, sha1 on the host threads; the reference writer's digests pass, a wrong
-    one raises 'Checksum failure'."""
-    d = os.path.join(gu.GOLDEN, 'zstd')
-    idx = gu.index('zstd')
+@pytest.mark.parametrize('name,algo', [('zstd', 'xxh64'), ('zstd', 'sha1'),
+                                       ('zstd_xxh3', 'xxh3_64'), ('zstd_xxh3', 'xxh128')])
+def test_pipeline_validate_hash(name, algo):
+    """validate_hash as Stream._prepare_shard_part (stream.py:401-411; hashing.py:24-26): xxh3_64
+    and xxh128 on the device over the resident batch (PIPELINE_DEVICE_HASHES), xxh64 and sha1 on
+    the pipeline's host threads, in place in the pinned staging. The digests the reference writer
+    recorded in index.json (tests/golden/make_golden.py) pass; a wrong one raises 'Checksum
+    failure' before the batch is handed out."""
+    from streaming_amd.pipeline import PIPELINE_DEVICE_HASHES
+    d = os.path.join(gu.GOLDEN, name)
+    idx = gu.index(name)
     info = idx['shards'][0]
     plan = Plan(info['column_names'], info['column_encodings'], info['column_sizes'])
     files = shard_files_from_index(d, idx)
+    assert all(f.hashes.get(algo) for f in files)  # the reference's own digests
     pipe = ShardPipeline(plan, files, shards_per_batch=1, workers=2, validate_hash=algo)
-    assert sum(b.rows for b in pipe) == sum(s['samples'] for s in idx['shards'])
+    assert pipe._device_hash == (algo in PIPELINE_DEVICE_HASHES)
+    parts = []
+    for b in pipe:
+        parts.append({k: (RaggedColumn(v.values.clone(), v.offsets.clone()) if isinstance(
+            v, RaggedColumn) else v.clone()) for k, v in b.columns.items()})
     pipe.close()
-    files[-1].hashes = dict(files[-1].hashes, **{algo: '00' * 8})
+    m = gu.manifest()[name]['columns']
+    for cname, v in _merge(parts).items():
+        if isinstance(v, tuple):
+            assert hashlib.sha256(v[0].tobytes()).hexdigest() == m[cname]['values']
+        else:
+            assert hashlib.sha256(v.tobytes()).hexdigest() == m[cname]['rows']
+    digest = files[-1].hashes[algo]
+    files[-1].hashes = dict(files[-1].hashes, **{algo: digest[:-1] + ('0' if digest[-1] != '0'
+                                                                      else '1')})
     pipe = ShardPipeline(plan, files, shards_per_batch=1, workers=2, validate_hash=algo)
     with pytest.raises(ValueError, match='Checksum failure'):
         for _ in pipe:

@@ -38,6 +38,21 @@ def test_golden_index_digests():
     assert checked == len(idx['shards'])
 
 
+def test_golden_index_xxh3_digests():
+    """The xxh3_64 / xxh128 digests the reference writer recorded for the zstd_xxh3 set (zip
+    files and, decompressed, raw shards): what the pipeline's device validation compares with."""
+    from streaming_amd.compression import decompress
+    d = os.path.join(gu.GOLDEN, 'zstd_xxh3')
+    idx = json.load(open(os.path.join(d, 'index.json')))
+    for shard in idx['shards']:
+        zdata = open(os.path.join(d, shard['zip_data']['basename']), 'rb').read()
+        raw = decompress(shard['compression'], zdata)
+        assert len(raw) == shard['raw_data']['bytes']
+        for algo in ('xxh3_64', 'xxh128'):
+            assert X.hexdigest(algo, zdata) == shard['zip_data']['hashes'][algo]
+            assert X.hexdigest(algo, raw) == shard['raw_data']['hashes'][algo]
+
+
 @pytest.mark.parametrize('algo', ALGOS)
 def test_every_short_length_vs_xxhash(algo):
     rng = random.Random(7)

@@ -151,3 +151,16 @@ def test_tile_rows_for_sizes_ragged_tiles_to_the_decode(monkeypatch):
     assert c.tile_rows_for(1 << 26, 1 << 26) == 256  # 1-byte rows: capped
     b = Plan(['id', 'x'], ['int32', 'ndarray:float32:1024'], [4, 4096])
     assert b.tile_rows_for(1 << 26, 16_352) == b.tile_rows
+
+
+def test_batch_tiles_from_the_buffer_bytes_the_decode_choice_reads():
+    """The C side picks the decode (streaming vs row-parallel) and the stage from batch->bytes,
+    the padded buffer size; the batch's tile table must be sized from the same count (ADVICE
+    round 2). Small shards whose samples average just under the streaming threshold unpadded
+    (3000 bytes) and above it padded (each shard rounded up to 256 bytes)."""
+    from streaming_amd.decoder import Plan, make_batch
+    c = Plan(['b', 'n', 's'], ['bytes', 'int', 'str'], [None, 8, None])
+    sizes, samples = [3000] * 64, [1] * 64
+    b = make_batch(c, sizes, samples, device='cpu')
+    assert sum(sizes) // sum(samples) < 3072 <= b.buffer.numel() // sum(samples)
+    assert b.tile_rows == c.tile_rows_for(b.buffer.numel(), sum(samples))

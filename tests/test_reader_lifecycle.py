@@ -26,11 +26,12 @@ def test_lru_bounds_bytes_and_evicts_oldest():
     c.put(3, 'c', 40)  # evicts 2 (least recently used)
     assert 2 not in c and 1 in c and 3 in c
     assert c.resident_bytes == 80 and c.evictions == 1
-    c.put(4, 'd', 150)  # larger than the limit: not kept, nothing else dropped
-    assert 4 not in c and c.resident_bytes == 80
-    c.update(1, 'a2', 90)  # grows: evicts the others to fit
+    c.put(1, 'a2', 90)  # replaced and grown: evicts the others to fit
     assert c.get(1) == 'a2' and c.resident_bytes == 90 and len(c) == 1
-    c.discard(1)
+    with pytest.warns(UserWarning):
+        c.put(4, 'd', 150)  # larger than the limit: kept as the only (most recent) entry
+    assert 4 in c and 1 not in c and c.resident_bytes == 150
+    c.discard(4)
     assert c.resident_bytes == 0 and len(c) == 0
 
 
