@@ -421,7 +421,9 @@ def measure(args, config, world, rank, dev, tmpdir):
         },
         'cpu_baseline': None,
     }
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+    # the reference reader restated, timed on rank 0's host cores at every N, after the GPU legs
+    # (the other ranks wait for it at the next config's barrier, outside any timed region)
+    if rank == 0 and args.cpu_seconds > 0:
         result['cpu_baseline'] = cpu_baseline(args, config, synth, tmpdir)
     del dec, out, synth
     torch.cuda.empty_cache()

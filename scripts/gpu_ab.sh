@@ -17,6 +17,14 @@ if [ -n "$VC" ]; then
 import json; d = json.load(open('$OUT/C.json'))
 print('C', d['rows'], {k: (round(v['GBps']), round(v['median_ms'], 4)) for k, v in d['results'].items()})"
 fi
+for spec in "short:32,256:8,64:$VS" "medium:256,1024:64,256:$VM"; do
+  IFS=: read -r nm blob chars vars <<< "$spec"
+  [ -z "$vars" ] && continue
+  timeout -k 10 400 python3 scripts/tune_decode.py --config C --shards ${SHARDS_S:-16} --blob $blob --chars $chars --rounds ${ROUNDS:-3} --variants $vars > "$OUT/$nm.json" 2> "$OUT/$nm.err" || { tail -30 "$OUT/$nm.err"; exit 1; }
+  python3 -c "
+import json; d = json.load(open('$OUT/$nm.json'))
+print('$nm', d['rows'], {k: (round(v['GBps']), round(v['median_ms'], 4)) for k, v in d['results'].items()})"
+done
 if [ -n "$VB" ]; then
   timeout -k 10 400 python3 scripts/tune_decode.py --config B --rounds ${ROUNDS:-3} --variants $VB > "$OUT/B.json" 2> "$OUT/B.err" || { tail -30 "$OUT/B.err"; exit 1; }
   python3 -c "

@@ -19,7 +19,7 @@ SOURCES = [
                  'mdsx_plan.cpp')
 ]
 HEADERS = [os.path.join(HERE, 'csrc', name)
-           for name in ('mdsx_internal.h', 'mdsx_device.h', 'mdsx_decode.h')]
+           for name in ('mdsx_internal.h', 'mdsx_device.h', 'mdsx_decode.h', 'mdsx_ring.h')]
 OUTPUT = os.path.join(HERE, 'lib', 'libmdsx.so')
 ARCH = os.environ.get('MDSX_OFFLOAD_ARCH', 'gfx950')
 

@@ -219,6 +219,8 @@ void apply_tuning(mdsx_plan* p) {
       p->rows_kb = int(v);
     } else if (key == "rownt") {
       p->rows_nt = v ? 1 : 0;
+    } else if (key == "swin" && v >= 1 && v <= 32) {
+      p->seg_win = int(v);
     } else if (key == "seg") {
       p->seg = v ? 1 : 0;
     } else if (key == "rkb" && v >= 1 && v <= 4096) {

@@ -42,6 +42,7 @@
 #include "mdsx_decode.h"
 #include "mdsx_device.h"
 #include "mdsx_internal.h"
+#include "mdsx_ring.h"
 
 namespace mdsx_kernels {
 namespace {
@@ -52,93 +53,8 @@ constexpr int kRunMaxRows = 32;  // rows of a tile: one offsets-table entry per 
 
 // A wave's LDS: its ring (S KiB, stream byte p at p % S KiB), a 64-byte mirror of the ring's
 // first bytes behind it (so a read that wraps is one contiguous read), offsets and flags of its run.
-constexpr uint32_t kMirror = 64;
 __host__ __device__ __forceinline__ uint32_t run_wave_lds(int S, int TR, int nvar) {
   return (uint32_t(S) * 1024u + kMirror + uint32_t(nvar) * uint32_t(TR) * 5u + 15u) & ~15u;
-}
-
-// 16 stream bytes at stream byte p: one ds_read_b128 at any byte address (gfx950 reads LDS
-// unaligned; the 16-byte realignment costs no instructions).
-template <int S>
-__device__ __forceinline__ uint4 ring16(const lds_u8* ring, uint32_t p) {
-  const u32x4 v = *(const MDSX_L u32x4*)(ring + (p & (S * 1024u - 1u)));
-  return make_uint4(v.x, v.y, v.z, v.w);
-}
-
-// u32 at stream byte p (any alignment).
-template <int S>
-__device__ __forceinline__ uint32_t ring_u32(const lds_u8* ring, uint32_t p) {
-  return *(const MDSX_L uint32_t*)(ring + (p & (S * 1024u - 1u)));
-}
-
-// s_waitcnt vmcnt(m), m the largest of 0, 1, 2, 4, 8, 16, 32 not above n (three compares).
-__device__ __forceinline__ void wait_vm_coarse(uint32_t n) {
-  if (n >= 16) {
-    if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  } else if (n >= 4) {
-    if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  } else if (n >= 2) {
-    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  } else if (n == 1) {
-    asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-}
-
-// The wave's stream: chunks [0, nq) from base, in slots of 64 chunks.
-struct Stream {
-  const uint4* base;
-  uint32_t nq, nslots;
-  uint32_t issued;  // slots issued
-  uint32_t ops;     // vector-memory operations issued by this wave (loads; stores certain to issue)
-  uint32_t op_at;   // lane r: `ops` when the slot now in ring position r was issued
-  uint32_t mirrored;  // the last slot at ring position 0 copied to the mirror
-  uint32_t landed;    // slots [0, landed) have landed (waited for)
-};
-
-// Issue slots while they fit in the ring above slot `low`: the stream bytes still to be read
-// all lie in slots >= low (callers pass a non-decreasing low).
-template <int S, bool kNT>
-__device__ __forceinline__ void pump(Stream& st, uint32_t ring_lds, uint32_t low, int lane) {
-  while (st.issued < st.nslots && st.issued < low + S) {
-    const uint32_t k = st.issued * 64u + uint32_t(lane);
-    glds16<kNT>(st.base + min(k, st.nq - 1), ring_lds + ((st.issued & (S - 1)) << 10));
-    if (lane == int(st.issued & (S - 1))) st.op_at = st.ops;
-    ++st.ops;
-    ++st.issued;
-  }
-}
-
-// pump, then wait until stream bytes [lo, hi] (hi - lo < (S - 1) KiB) have landed; a slot at ring
-// position 0 that has landed is mirrored behind the ring for the reads that wrap.
-template <int S, bool kNT>
-__device__ __forceinline__ void ensure(Stream& st, const lds_u8* ring, uint32_t ring_lds,
-                                       uint32_t lo, uint32_t hi, int lane) {
-  pump<S, kNT>(st, ring_lds, lo >> 10, lane);
-  const uint32_t upto = min(hi >> 10, st.nslots - 1);
-  if (upto < st.landed) return;  // waited for already
-  st.landed = upto + 1;
-  wait_vm_coarse(st.ops - uint32_t(__builtin_amdgcn_readlane(int(st.op_at), int(upto & (S - 1)))) -
-                 1u);
-  const uint32_t j0 = upto & ~uint32_t(S - 1);
-  if (j0 != st.mirrored) {
-    st.mirrored = j0;
-    if (lane < int(kMirror / 4))
-      *(MDSX_L uint32_t*)(ring + S * 1024 + 4 * lane) = *(const MDSX_L uint32_t*)(ring + 4 * lane);
-  }
-}
-
-__device__ __forceinline__ uint4 readlane4(const uint4 v, int l) {
-  return make_uint4(__builtin_amdgcn_readlane(v.x, l), __builtin_amdgcn_readlane(v.y, l),
-                    __builtin_amdgcn_readlane(v.z, l), __builtin_amdgcn_readlane(v.w, l));
-}
-
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
-  return uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v)), l))) |
-         (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v >> 32)), l))) << 32);
 }
 
 // The per-column state of a wave, lane-distributed (lane c: column c). Output positions are
@@ -450,57 +366,21 @@ __global__ __launch_bounds__(kRunBlock, 7) void run_decode_kernel(const DevArgs 
 // zero-length rule.
 
 // per-wave LDS of the lean path: the general path's, then the staged small fixed columns
-__host__ __device__ __forceinline__ uint32_t seg_wave_lds(int S, int TR, int nvar,
-                                                          uint32_t small) {
-  return run_wave_lds(S, TR, nvar) + ((small * uint32_t(TR) + 15u) & ~15u);
+constexpr int kWinMax = kRunMaxRows;  // samples of a window: one per lane
+
+__host__ __device__ __forceinline__ uint32_t seg_small_off(int S, int TR, int nvar) {
+  return run_wave_lds(S, TR, nvar);
 }
-
-// u32 inclusive prefix sum over lanes [0, n) (n <= 64 wave-uniform; other lanes: garbage)
-__device__ __forceinline__ uint32_t wave_incl_u32(uint32_t x, int lane, int n) {
-  for (int o = 1; o < n; o <<= 1) {
-    const uint32_t y = uint32_t(__shfl_up(int(x), o));
-    if (lane >= o) x += y;
-  }
-  return x;
+// window records after the small stage: [ncols][kWinMax] output position, stream position, length
+// (u32 each), then [ncols] UTF-8 failure bits
+__host__ __device__ __forceinline__ uint32_t seg_rec_off(int S, int TR, int nvar,
+                                                         uint32_t small) {
+  return seg_small_off(S, TR, nvar) + ((small * uint32_t(TR) + 15u) & ~15u);
 }
-
-// bytes [0, h) of `lo` and [h, 16) of `hi` (h wave-uniform, 0..16)
-__device__ __forceinline__ uint4 splice_lo(const uint4 lo, const uint4 hi, uint32_t h) {
-  const uint64_t m0 = h >= 8 ? ~0ull : (1ull << (8 * h)) - 1ull;
-  const uint64_t m1 = h <= 8 ? 0ull : h >= 16 ? ~0ull : (1ull << (8 * (h - 8))) - 1ull;
-  const uint32_t w0 = uint32_t(m0), w1 = uint32_t(m0 >> 32), w2 = uint32_t(m1),
-                 w3 = uint32_t(m1 >> 32);
-  return make_uint4((lo.x & w0) | (hi.x & ~w0), (lo.y & w1) | (hi.y & ~w1),
-                    (lo.z & w2) | (hi.z & ~w2), (lo.w & w3) | (hi.w & ~w3));
-}
-
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-
-// n (1..16) bytes of `v` to LDS at p (p aligned to the largest power of two dividing n)
-__device__ __forceinline__ void lds_put(MDSX_L uint8_t* p, const uint4 v, uint32_t n) {
-  if (n == 8) {
-    *(MDSX_L u32x2*)p = u32x2{v.x, v.y};
-  } else if (n == 4) {
-    *(MDSX_L uint32_t*)p = v.x;
-  } else if (n == 16) {
-    *(MDSX_L u32x4*)p = u32x4{v.x, v.y, v.z, v.w};
-  } else {
-    for (uint32_t k = 0; k < n; ++k) p[k] = uint8_t(byte_of(v, int(k)));
-  }
-}
-
-// n (1..16) bytes from LDS at p to global memory at q (both aligned as in lds_put)
-__device__ __forceinline__ void lds_out(const MDSX_L uint8_t* p, uint8_t* q, uint32_t n) {
-  if (n == 8) {
-    *(MDSX_G u32x2*)gp((u32x2*)q) = *(const MDSX_L u32x2*)p;
-  } else if (n == 4) {
-    *gp((uint32_t*)q) = *(const MDSX_L uint32_t*)p;
-  } else if (n == 16) {
-    const u32x4 v = *(const MDSX_L u32x4*)p;
-    *(MDSX_G u32x4*)gp((u32x4*)q) = v;
-  } else {
-    for (uint32_t k = 0; k < n; ++k) *gp(q + k) = p[k];
-  }
+__host__ __device__ __forceinline__ uint32_t seg_wave_lds(int S, int TR, int nvar, int ncols,
+                                                          uint32_t small, bool windows) {
+  return seg_rec_off(S, TR, nvar, small) +
+         (windows ? uint32_t(ncols) * (3u * kWinMax * 4u + 4u) : 0u);
 }
 
 // One value of a wide column, all of its stream bytes landed: output bytes [d, d + len) (relative
@@ -550,6 +430,159 @@ __device__ __forceinline__ bool seg_copy(const lds_u8* ring, uint64_t base, uint
   return utf8 ? __any(bad) != 0 : false;
 }
 
+// One wide column of a window of m samples, all of their stream bytes landed: output bytes
+// [D, D + T) (relative to `base`), value i at window output bytes [wd[i], wd[i] + wl[i]) from
+// stream bytes [wp[i], ...) (wp[i] = ~0: zeros, a sample that failed its checks). Lane k of a
+// step assembles 16-byte output chunk k from the value(s) it covers (the first by binary search
+// over wd, one unaligned ring read per value piece), checks str pieces for strict UTF-8 (each
+// value in its own context, a failing value's bit set in *bad) and stores the chunk whole; the
+// window's first chunk takes the carried bytes, its partly filled last chunk is carried.
+template <int S, bool kNT>
+__device__ __forceinline__ void win_copy(const lds_u8* ring, const MDSX_L uint32_t* wd,
+                                         const MDSX_L uint32_t* wp, const MDSX_L uint32_t* wl,
+                                         int m, uint64_t base, uint32_t cst, uint32_t D,
+                                         uint32_t T, bool utf8, MDSX_L uint32_t* bad,
+                                         uint4& carry, uint32_t& ops, int lane) {
+  const uint32_t head = D & 15u, dbeg = D - head, dend = D + T;
+  const uint32_t nch = (dend - dbeg + 15u) >> 4;
+  const uint32_t nfull = (dend - dbeg) >> 4;
+  const uint32_t tail = dend & 15u;
+  const bool shared0 = dbeg < cst;
+  const uint64_t out = base + dbeg;
+  uint4 last = carry;
+  for (uint32_t g = 0; g < nch; g += 64) {  // wave-uniform
+    const uint32_t q = g + uint32_t(lane);
+    const int32_t x0 = int32_t(16u * q) - int32_t(head);  // window output byte of chunk byte 0
+    uint4 val = make_uint4(0, 0, 0, 0);
+    if (q < nch) {
+      int32_t x = max(x0, 0);
+      const int32_t hi = min(x0 + 16, int32_t(T));
+      // the value holding byte x: the last i with wd[i] <= x
+      int i = 0;
+      for (int w = 16; w > 0; w >>= 1)
+        if (i + w < m && int32_t(wd[i + w]) <= x) i += w;
+      while (x < hi) {  // the chunk's pieces, one value each
+        const int32_t ds = int32_t(wd[i]), de = ds + int32_t(wl[i]);
+        const int32_t pe = min(hi, de);
+        if (pe > x) {
+          const uint32_t sp = wp[i];
+          const uint4 v = sp == 0xffffffffu ? make_uint4(0, 0, 0, 0)
+                                            : ring16<S>(ring, sp - uint32_t(ds) + uint32_t(x0));
+          const uint4 piece = keep_bytes(v, uint32_t(x - x0), uint32_t(pe - x0));
+          val = make_uint4(val.x | piece.x, val.y | piece.y, val.z | piece.z, val.w | piece.w);
+          if (utf8) {
+            // the value's dword before the chunk, when the value started before it
+            uint32_t pw = 0;
+            if (x == x0 && x > ds) {
+              pw = ring_u32<S>(ring, sp - uint32_t(ds) + uint32_t(x0) - 4u);
+              const int32_t nv = x0 - ds;  // the value's bytes before the chunk
+              if (nv < 4) pw &= ~((1u << (8 * (4 - nv))) - 1u);
+            }
+            if (utf8_chunk_bad(piece, pw, pe == de)) atomicOr(bad, 1u << i);
+          }
+          x = pe;
+        }
+        ++i;
+      }
+    }
+    if (g == 0 && head && lane == 0) val = splice_lo(carry, val, head);
+    const bool skip0 = shared0 && g == 0;
+    if (q < nfull && !(skip0 && lane == 0)) st16<kNT>(out + 16ull * q, val);
+    if (min(nfull, g + 64u) > g + (skip0 ? 1u : 0u)) ++ops;  // that store was issued
+    if (skip0 && nfull > 0) wave_edge_store(val, 0, out, base + cst, out + 16, lane);
+    if (tail && nch - 1 - g < 64u) last = readlane4(val, int(nch - 1 - g));
+  }
+  carry = last;
+}
+
+// A window of m >= 2 consecutive samples (j .. j + m - 1; lane i: sample j + i), its bytes in
+// the ring together: each sample's size heads and column boundaries lane-parallel, every
+// column's window output by a wave prefix sum, the small fixed columns staged, each wide column
+// copied by win_copy over the window's whole output range.
+template <int S, bool kNT>
+__device__ __forceinline__ void seg_window(
+    const DevArgs& a, const MDSX_L DevCol* cols, Stream& st, const lds_u8* ring,
+    uint32_t ring_lds, uint32_t ob, uint64_t shard, uint64_t sbase, int j, int m, int TR,
+    const TileRun& r, int vi, uint32_t rb, uint32_t meta, bool small, uint64_t small_mask,
+    uint64_t wide_mask, uint32_t soff, uint32_t cst, uint64_t base, uint32_t& cur, uint4& carry,
+    MDSX_L uint32_t* obuf, MDSX_L uint8_t* fbuf, MDSX_L uint8_t* sbuf, MDSX_L uint32_t* wrec,
+    MDSX_L uint32_t* wbad, int lane) {
+  const int ncols = a.ncols;
+  const uint32_t hv = 4u * uint32_t(a.nvar);
+  const bool live = lane < m;
+  const int li = j + min(lane, m - 1);
+  const uint32_t wb = uint32_t(__shfl(int(ob), li)), we = uint32_t(__shfl(int(ob), li + 1));
+  const uint32_t w0 = uint32_t(__builtin_amdgcn_readlane(int(ob), j));
+  const uint32_t w1 = uint32_t(__builtin_amdgcn_readlane(int(ob), j + m));
+  const uint32_t sp0 = uint32_t(shard + w0 - sbase);
+  ensure<S, kNT>(st, ring, ring_lds, sp0, sp0 + (w1 - w0) + 15u, lane);  // the whole window
+  const uint32_t size = we - wb;
+  const uint32_t spi = uint32_t(shard + wb - sbase);  // stream position of this lane's sample
+  // the boundary check (mds/reader.py:111-125): heads and columns inside the sample
+  bool ok = live && hv <= size;
+  {
+    uint64_t need = hv;
+    for (int c = 0; c < ncols && ok; ++c) {
+      const int v = cols[c].var_index;
+      need += v >= 0 ? ring_u32<S>(ring, spi + 4u * uint32_t(v)) : cols[c].row_bytes;
+    }
+    ok = ok && need <= size;
+  }
+  if (live && !ok) report_decode(a, MDSX_E_BOUNDS, int(r.shard), int(r.r0) + j + lane, -1);
+  // every column: the window's output by a prefix sum over the samples
+  uint32_t rel = hv;
+  uint32_t Tw = 0;  // lane c: the window's output bytes of column c
+  for (int c = 0; c < ncols; ++c) {  // wave-uniform
+    const int v = cols[c].var_index;
+    const uint32_t w = cols[c].row_bytes;
+    uint32_t len = 0;
+    if (live) len = ok ? (v >= 0 ? ring_u32<S>(ring, spi + 4u * uint32_t(v)) : w) : (v >= 0 ? 0u : w);
+    const uint32_t incl = wave_incl_u32(len, lane, m);
+    const uint32_t T = uint32_t(__builtin_amdgcn_readlane(int(incl), m - 1));
+    if (lane == c) Tw = T;
+    const uint32_t d = incl - len;
+    const uint32_t pos = spi + rel;
+    if (live) {
+      wrec[(3 * c) * kWinMax + lane] = d;
+      wrec[(3 * c + 1) * kWinMax + lane] = ok ? pos : 0xffffffffu;
+      wrec[(3 * c + 2) * kWinMax + lane] = len;
+    }
+    if (v >= 0) {
+      const uint32_t cu = uint32_t(__builtin_amdgcn_readlane(int(cur), c));
+      if (live) {
+        obuf[v * TR + j + lane] = cu + d;
+        fbuf[v * TR + j + lane] = 0;
+      }
+    } else if (w <= uint32_t(kSmallMax)) {
+      const uint32_t so = uint32_t(__builtin_amdgcn_readlane(int(soff), c));
+      if (live)
+        lds_put(sbuf + so + uint32_t(j + lane) * w,
+                ok ? ring16<S>(ring, pos) : make_uint4(0, 0, 0, 0), w);
+    }
+    if (ok) rel += len;
+  }
+  // the wide columns, one window-wide copy each
+  for (uint64_t mk = wide_mask; mk; mk &= mk - 1) {
+    const int c = __builtin_ctzll(mk);
+    const uint32_t T = uint32_t(__builtin_amdgcn_readlane(int(Tw), c));
+    if (T == 0) continue;
+    const uint32_t D = uint32_t(__builtin_amdgcn_readlane(int(cur), c));
+    const uint32_t mc = uint32_t(__builtin_amdgcn_readlane(int(meta), c));
+    const bool utf8 = (mc >> 8) & 1u;
+    if (utf8 && lane == 0) wbad[c] = 0;
+    uint4 cy = (D & 15u) ? readlane4(carry, c) : make_uint4(0, 0, 0, 0);
+    win_copy<S, kNT>(ring, wrec + (3 * c) * kWinMax, wrec + (3 * c + 1) * kWinMax,
+                     wrec + (3 * c + 2) * kWinMax, m, readlane64(base, c),
+                     uint32_t(__builtin_amdgcn_readlane(int(cst), c)), D, T, utf8, wbad + c, cy,
+                     st.ops, lane);
+    if (lane == c) {
+      cur = D + T;
+      carry = cy;
+    }
+    if (utf8 && live && ((wbad[c] >> lane) & 1u)) fbuf[(int(mc & 255u) - 1) * TR + j + lane] = 1;
+  }
+}
+
 template <int S, bool kNT>
 __global__ __launch_bounds__(kRunBlock, 4) void seg_decode_kernel(const DevArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -563,7 +596,8 @@ __global__ __launch_bounds__(kRunBlock, 4) void seg_decode_kernel(const DevArgs 
   if (tile >= a.ntiles) return;  // wave-uniform; no barrier below
   const int TR = a.tile_rows;
   const int ncols = a.ncols, nvar = a.nvar;
-  uint8_t* wl = smem + size_t(wave) * seg_wave_lds(S, TR, nvar, a.seg_small);
+  uint8_t* wl =
+      smem + size_t(wave) * seg_wave_lds(S, TR, nvar, ncols, a.seg_small, a.seg_win > 1);
   const TileRun r = a.tile_run[tile];
   if (!(r.fast & 2)) {
     run_body<S, kNT>(a, cols, tile, r, wl, lane);
@@ -572,7 +606,9 @@ __global__ __launch_bounds__(kRunBlock, 4) void seg_decode_kernel(const DevArgs 
   const lds_u8* ring = (const lds_u8*)wl;
   MDSX_L uint32_t* obuf = (MDSX_L uint32_t*)(wl + S * 1024 + kMirror);  // [nvar][TR]
   MDSX_L uint8_t* fbuf = (MDSX_L uint8_t*)(wl + S * 1024 + kMirror + nvar * TR * 4);  // [nvar][TR]
-  MDSX_L uint8_t* sbuf = (MDSX_L uint8_t*)(wl + run_wave_lds(S, TR, nvar));  // small columns
+  MDSX_L uint8_t* sbuf = (MDSX_L uint8_t*)(wl + seg_small_off(S, TR, nvar));  // small columns
+  MDSX_L uint32_t* wrec = (MDSX_L uint32_t*)(wl + seg_rec_off(S, TR, nvar, a.seg_small));
+  MDSX_L uint32_t* wbad = wrec + 3 * kWinMax * ncols;
   const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(
       static_cast<uint32_t>(reinterpret_cast<uintptr_t>((const MDSX_L uint8_t*)wl)));
 
@@ -631,8 +667,23 @@ __global__ __launch_bounds__(kRunBlock, 4) void seg_decode_kernel(const DevArgs 
   const uint64_t small_mask = __ballot(small);
   const uint32_t hv = 4u * uint32_t(nvar);
 
-  for (int j = 0; j < n; ++j) {  // wave-uniform
+  // lane l: offsets[r0 + l + 1] (the end of sample l)
+  const uint32_t ob_next = uint32_t(__shfl_down(int(ob), 1));
+  for (int j = 0; j < n;) {  // wave-uniform
     const uint32_t b = uint32_t(__builtin_amdgcn_readlane(int(ob), j));
+    // a window: the samples j .. j + m - 1 whose bytes fit the ring together (seg_win > 1)
+    int m = 1;
+    if (a.seg_win > 1) {
+      const bool fits = lane >= j && lane < min(n, j + int(a.seg_win)) && ob_next - b <= a.seg_lim;
+      m = __builtin_ctzll(~(__ballot(fits) >> j));
+    }
+    if (m > 1) {
+      seg_window<S, kNT>(a, cols, st, ring, ring_lds, ob, shard, sbase, j, m, TR, r, vi, rb, meta,
+                         small, small_mask, wide_mask, soff, cst, base, cur, carry, obuf, fbuf,
+                         sbuf, wrec, wbad, lane);
+      j += m;
+      continue;
+    }
     const uint32_t e = uint32_t(__builtin_amdgcn_readlane(int(ob), j + 1));
     const uint32_t size = e - b;
     const uint32_t sp = uint32_t(shard + b - sbase);  // stream position of the sample
@@ -648,16 +699,18 @@ __global__ __launch_bounds__(kRunBlock, 4) void seg_decode_kernel(const DevArgs 
     if (!ok && lane == 0) report_decode(a, MDSX_E_BOUNDS, int(r.shard), int(r.r0 + j), -1);
     const uint32_t pos = sp + hv + incl - lc;  // stream position of the column's value
     const uint32_t clen = ok ? len : (vi >= 0 ? 0u : rb);
-    if (small) lds_put(sbuf + soff + uint32_t(j) * rb, ok ? ring16<S>(ring, pos) : make_uint4(0, 0, 0, 0), rb);
+    if (small)
+      lds_put(sbuf + soff + uint32_t(j) * rb, ok ? ring16<S>(ring, pos) : make_uint4(0, 0, 0, 0),
+              rb);
     if (vi >= 0) {
       obuf[vi * TR + j] = cur;
       if ((meta >> 8) & 1u) fbuf[vi * TR + j] = 0;
     }
     // the wide columns, in column order = stream order
-    uint64_t m = wide_mask;
-    while (m) {
-      const int c = __builtin_ctzll(m);
-      m &= m - 1;
+    uint64_t wm = wide_mask;
+    while (wm) {
+      const int c = __builtin_ctzll(wm);
+      wm &= wm - 1;
       const uint32_t l = uint32_t(__builtin_amdgcn_readlane(int(clen), c));
       if (l == 0) continue;
       const uint32_t d = uint32_t(__builtin_amdgcn_readlane(int(cur), c));
@@ -675,6 +728,7 @@ __global__ __launch_bounds__(kRunBlock, 4) void seg_decode_kernel(const DevArgs 
       if (bad && lane == 0) fbuf[(int(mc & 255u) - 1) * TR + j] = 1;
       pump<S, kNT>(st, ring_lds, (p + l) >> 10, lane);  // the bytes before p + l are done
     }
+    ++j;
   }
   // the partly filled last chunk of every wide column (bytes [max(cst, chunk), cur))
   for (uint64_t m = wide_mask; m; m &= m - 1) {
@@ -718,8 +772,8 @@ int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
   if (a.tile_rows > kRunMaxRows)
     return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode tiles hold at most 32 rows");
   if (a.seg_lim) {
-    const size_t slds =
-        size_t(kRunWaves) * seg_wave_lds(a.run_slots, a.tile_rows, a.nvar, a.seg_small);
+    const size_t slds = size_t(kRunWaves) * seg_wave_lds(a.run_slots, a.tile_rows, a.nvar,
+                                                         a.ncols, a.seg_small, a.seg_win > 1);
     if (slds > 160 * 1024)
       return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode LDS exceeds 160 KiB");
 #define MDSX_SEG_CASE(S, NT)                                                              \

@@ -366,6 +366,10 @@ class DecodedBatch:
     rows: int
     row0: list[int] = field(default_factory=list)
     stream: Optional[torch.cuda.Stream] = None
+    sample_ids: Optional[np.ndarray] = None  # the global ids of the rows (device_iter batches)
+
+    def __len__(self) -> int:
+        return int(self.rows)
 
     def tensors(self) -> list[torch.Tensor]:
         out = []

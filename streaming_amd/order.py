@@ -11,8 +11,9 @@ of the epoch's sample-id array that ``generate_work`` lays out (``batching/__ini
 :class:`DeviceSampleGather` is the device side of that loop: the same ids, in the same order, as
 device batches. For each batch the touched shards are decoded on demand through the readers'
 bounded decoded-shard cache (:mod:`streaming_amd.cache`; a shard decoded once stays resident while
-the cache holds it), each shard's rows are gathered on the device (``mdsx_gather_*``), and the
-per-shard parts are put back in batch order by one more device gather. Resumption is the
+the cache holds it), then every column is gathered from all of them in one launch sequence
+(``mdsx_gather_*_multi``: each id names its source shard and row), rows already in batch order.
+:func:`streaming_amd.plugin.device_iter` drives it from the reference's own iteration. Resumption is the
 reference's: ``state_dict`` / ``load_state_dict`` move ``sample_in_epoch``, and ``generate_work``
 then hands out the rest of the epoch (``dataset.py:778-856``); this module takes those ids as they
 come.

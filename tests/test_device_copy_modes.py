@@ -43,6 +43,8 @@ MODES = {
     'seg8': 'run=8,seg=1,rmin=0',
     'seg16': 'run=16,seg=1,rmin=0,rkb=1024',
     'seg8_nt': 'run=8,seg=1,rmin=0,rnt=1',
+    'seg8_1': 'run=8,seg=1,rmin=0,swin=1',  # one sample at a time (no windows of several)
+    'seg16_w4': 'run=16,seg=1,rmin=0,swin=4,rkb=64',
     'rows': 'rows=32,rmin=1000000000',  # the row-parallel decode (mdsx_rows.hip) for every size
     'rows_auto': 'rows=-1,rmin=1000000000',  # ... its tiles and stage sized per batch
     'rows_small': 'rows=2,rmin=1000000000',  # a 2 KiB stage: windows and HBM-direct samples

@@ -113,3 +113,37 @@ def test_pipeline_raises_on_malformed_first_batch(tmp_path):
     with pytest.raises(IndexError):
         next(it)  # the first batch holds shard 1: raised before it is handed out
     pipe.close()
+
+
+class _CacheProbe(torch.utils.data.Dataset):
+    """A dataset reporting, with each sample, its worker's decoded-shard cache occupancy."""
+
+    def __init__(self, ds):
+        self.ds = ds
+
+    def __len__(self):
+        return len(self.ds)
+
+    def __getitem__(self, i):
+        c = self.ds.cache
+        sample = self.ds[i]
+        return os.getpid(), c.resident_bytes, c.device_limit(), sample
+
+
+def test_dataloader_workers_share_the_device_bound():
+    """Spawned workers each hold an equal share of the decoded-shard bound, so the loader's
+    workers together never keep more device bytes than the bound."""
+    bound = 24 << 10  # a few decoded shards of config A
+    ds = LocalDataset(A, decoded_cache_bytes=bound)
+    loader = torch.utils.data.DataLoader(_CacheProbe(ds), batch_size=50, num_workers=2,
+                                         collate_fn=list, multiprocessing_context='spawn')
+    peak, limits, got = {}, set(), []
+    for batch in loader:
+        for pid, resident, limit, sample in batch:
+            peak[pid] = max(peak.get(pid, 0), resident)
+            limits.add(limit)
+            got.append(sample)
+    idx = gu.index('config_a')['shards']
+    assert got == [_oracle_item(A, info, i) for info in idx for i in range(info['samples'])]
+    assert len(peak) == 2 and limits == {bound // 2}
+    assert sum(peak.values()) <= bound, peak

@@ -30,3 +30,17 @@ def test_streaming_dataset_with_device_stream(tmp_path):
     assert out['shards'] == 64 and out['num_samples'] == 10_000
     assert out['ids_match_fixture']
     assert out['get_item'].startswith('RuntimeError') and 'GPU' in out['get_item']
+
+
+def test_device_iter_follows_the_reference_iteration(tmp_path):
+    """device_iter / DeviceBatches over the real StreamingDataset: the reference's order from the
+    epoch start and resumed from a checkpoint of the samples handed out (rows read by the oracle
+    here; on the GPU by the device gather, tests/test_device_plugin_iter.py)."""
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE='1', HIP_VISIBLE_DEVICES='')
+    res = subprocess.run([sys.executable, os.path.join(HERE, 'integration',
+                                                       'device_iter_ref_check.py'), REF,
+                          str(tmp_path)], capture_output=True, text=True, timeout=600, env=env)
+    assert res.returncode == 0, res.stderr[-3000:]
+    out = json.loads(res.stdout.strip().splitlines()[-1])
+    for name, r in out.items():
+        assert all(r.values()), (name, r)
