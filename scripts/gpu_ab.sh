@@ -8,7 +8,7 @@ OUT=gpurun_out/${TAG:-ab}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 if [ -n "$PYTEST_ARGS" ]; then
-  timeout -k 10 900 python3 -u -m pytest $PYTEST_ARGS -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 || { tail -60 "$OUT/pytest_gpu.log"; exit 1; }
+  timeout -k 10 900 python3 -u -m pytest $PYTEST_ARGS ${PYTEST_K:+-k "$PYTEST_K"} -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 || { tail -60 "$OUT/pytest_gpu.log"; exit 1; }
   tail -3 "$OUT/pytest_gpu.log"
 fi
 if [ -n "$VC" ]; then

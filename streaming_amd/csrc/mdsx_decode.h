@@ -59,7 +59,8 @@ struct DevArgs {
   uint64_t* src_abs;     // [nvar][rows]  byte index into the batch of each row's ragged value
   uint32_t* row_map;     // [nvar][map_len] first row of every gather tile
   uint64_t* lookback;    // [nvar][ntiles] single-pass look-back status words
-  uint32_t* ticket;      // single-pass tile ticket counter
+  uint32_t* ticket;      // single-pass tile ticket counter (also the chained totals' blocks)
+  uint64_t* chain;       // [nvar][blocks] chained totals look-back status words (run decodes)
   uint64_t map_len;
   uint64_t rows;
   uint32_t ntiles;
@@ -171,7 +172,7 @@ constexpr uint64_t kStatusBlock = 256;
 // The LDS-staged decode of ragged plans (mdsx_stage.hip). Pass 1: the ragged bytes of every tile
 // (then scan_totals_kernel, one entry per tile: a.scan_per == 1). Pass 2: every column of every
 // row from each tile's shard bytes staged once in LDS. Return MDSX_OK or a launch error.
-int launch_stage_totals(const DevArgs& a, hipStream_t s);
+int launch_stage_totals(const DevArgs& a, hipStream_t s, bool chained);
 int launch_stage_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s);
 uint32_t stage_tiles_per_wg(uint32_t ntiles);
 int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s);

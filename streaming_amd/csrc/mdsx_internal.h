@@ -55,6 +55,8 @@ struct mdsx_plan {
                            // temporal ones let L2 merge the partial stores at run edges)
   int seg = 0;             // streaming decode: the lean path for clean runs of samples that fit
                            // the ring (seg_decode_kernel; others take the general path)
+  int chain = 0;            // streaming decodes: totals scan chained into the totals pass
+  int seg_waves = 4;        // lean path: waves (runs) per workgroup (1, 2 or 4)
   int seg_win = 32;         // lean path: samples per window at most (1..32; 1: one at a time)
   int rows_kb = 0;         // row-parallel decode of shorter samples: LDS stage in KiB (0: off,
                            // -1: sized per batch, rows_tile_rows / rows_stage_bytes)

@@ -811,7 +811,7 @@ __global__ __launch_bounds__(kBlock) void gather_ragged_kernel(const DevArgs a) 
 
 // ---------------------------------------------------------------------------------------------
 struct Layout {
-  uint64_t tile_total, tile_prefix, chunk_sum, tile_run, src_abs, row_map, map_len, total;
+  uint64_t tile_total, tile_prefix, chunk_sum, tile_run, src_abs, row_map, chain, map_len, total;
 };
 
 __host__ uint64_t round256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
@@ -830,7 +830,8 @@ Layout workspace_layout(const mdsx_plan* plan, const mdsx_batch* b) {
   L.tile_run = L.chunk_sum + round256(nv * (b->ntiles / kScanChunk + 1) * 8);
   L.src_abs = L.tile_run + round256(nv ? uint64_t(b->ntiles) * sizeof(TileRun) : 0);
   L.row_map = L.src_abs + round256(nv * b->rows * 8);
-  L.total = L.row_map + round256(nv * L.map_len * 4);
+  L.chain = L.row_map + round256(nv * L.map_len * 4);
+  L.total = L.chain + round256(nv * (uint64_t(b->ntiles) + 1) * 8);
   return L;
 }
 
@@ -861,6 +862,7 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   a->row_map = reinterpret_cast<uint32_t*>(ws + L.row_map);
   a->lookback = reinterpret_cast<uint64_t*>(ws + L.tile_total);  // single pass: no tile totals
   a->ticket = reinterpret_cast<uint32_t*>(ws + kTicketOffset);
+  a->chain = reinterpret_cast<uint64_t*>(ws + L.chain);
   a->map_len = L.map_len;
   a->totals = d_totals;
   a->rows = b->rows;
@@ -1282,8 +1284,18 @@ int mdsx_scan_shards(const mdsx_plan* plan, const mdsx_batch* batch, const mdsx_
   hipStream_t s = static_cast<hipStream_t>(stream);
   rc = hip_check(hipMemsetAsync(d_workspace, 0, kStatusBlock, s), "hipMemsetAsync");
   if (rc != MDSX_OK || plan->nvar == 0) return rc;
+  // streaming decodes (tiles of <= 32 rows): the totals scan chained into the totals pass
+  const bool chained = plan->chain && a.run_slots && a.ntiles > 0;
+  if (chained) {
+    const uint32_t per = uint32_t(kBlock / a.tile_rows);
+    const uint64_t blocks = (uint64_t(a.ntiles) + per - 1) / per;
+    rc = hip_check(hipMemsetAsync(a.chain, 0, size_t(plan->nvar) * blocks * 8, s),
+                   "hipMemsetAsync");
+    if (rc != MDSX_OK) return rc;
+    return launch_stage_totals(a, s, true);
+  }
   if (a.ntiles > 0 && (a.stage_bytes || a.run_slots || a.rows_bytes)) {
-    rc = launch_stage_totals(a, s);
+    rc = launch_stage_totals(a, s, false);
     if (rc != MDSX_OK) return rc;
   } else if (a.ntiles > 0) {
     hipLaunchKernelGGL(scan_tiles_kernel, dim3(a.nscan), dim3(kBlock), 0, s, a);

@@ -219,6 +219,10 @@ void apply_tuning(mdsx_plan* p) {
       p->rows_kb = int(v);
     } else if (key == "rownt") {
       p->rows_nt = v ? 1 : 0;
+    } else if (key == "chain") {
+      p->chain = v ? 1 : 0;
+    } else if (key == "swg" && (v == 1 || v == 2 || v == 4)) {
+      p->seg_waves = int(v);
     } else if (key == "swin" && v >= 1 && v <= 32) {
       p->seg_win = int(v);
     } else if (key == "seg") {

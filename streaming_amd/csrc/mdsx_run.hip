@@ -583,21 +583,27 @@ __device__ __forceinline__ void seg_window(
   }
 }
 
-template <int S, bool kNT>
-__global__ __launch_bounds__(kRunBlock, 4) void seg_decode_kernel(const DevArgs a) {
+// The column table of a lean-path workgroup, ahead of the waves' LDS (dynamic, ncols entries).
+__host__ __device__ __forceinline__ uint32_t seg_cols_lds(int ncols) {
+  return (uint32_t(ncols) * uint32_t(sizeof(DevCol)) + 15u) & ~15u;
+}
+
+// W waves per workgroup (one run each): fewer waves per workgroup waste less LDS per CU.
+template <int S, bool kNT, int W>
+__global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  __shared__ DevCol s_cols[MDSX_MAX_COLUMNS];
   const int t = threadIdx.x, lane = t & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  for (int c = t; c < a.ncols; c += kRunBlock) s_cols[c] = a.cols[c];
+  const int wave = W == 1 ? 0 : __builtin_amdgcn_readfirstlane(t >> 6);
+  MDSX_L DevCol* s_cols = (MDSX_L DevCol*)smem;
+  for (int c = t; c < a.ncols; c += 64 * W) s_cols[c] = a.cols[c];
   __syncthreads();
   const MDSX_L DevCol* cols = (const MDSX_L DevCol*)s_cols;
-  const uint32_t tile = blockIdx.x * kRunWaves + uint32_t(wave);
+  const uint32_t tile = blockIdx.x * W + uint32_t(wave);
   if (tile >= a.ntiles) return;  // wave-uniform; no barrier below
   const int TR = a.tile_rows;
   const int ncols = a.ncols, nvar = a.nvar;
-  uint8_t* wl =
-      smem + size_t(wave) * seg_wave_lds(S, TR, nvar, ncols, a.seg_small, a.seg_win > 1);
+  uint8_t* wl = smem + seg_cols_lds(ncols) +
+                size_t(wave) * seg_wave_lds(S, TR, nvar, ncols, a.seg_small, a.seg_win > 1);
   const TileRun r = a.tile_run[tile];
   if (!(r.fast & 2)) {
     run_body<S, kNT>(a, cols, tile, r, wl, lane);
@@ -772,29 +778,38 @@ int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
   if (a.tile_rows > kRunMaxRows)
     return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode tiles hold at most 32 rows");
   if (a.seg_lim) {
-    const size_t slds = size_t(kRunWaves) * seg_wave_lds(a.run_slots, a.tile_rows, a.nvar,
-                                                         a.ncols, a.seg_small, a.seg_win > 1);
+    const int W = plan->seg_waves;
+    const size_t slds = seg_cols_lds(a.ncols) + size_t(W) * seg_wave_lds(a.run_slots, a.tile_rows,
+                                                                          a.nvar, a.ncols,
+                                                                          a.seg_small,
+                                                                          a.seg_win > 1);
     if (slds > 160 * 1024)
       return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode LDS exceeds 160 KiB");
-#define MDSX_SEG_CASE(S, NT)                                                              \
-  if (a.run_slots == S && bool(plan->run_nt) == NT) {                                     \
-    if (slds > 64 * 1024) {                                                               \
-      const int rc = hip_check(                                                           \
-          hipFuncSetAttribute(reinterpret_cast<const void*>(seg_decode_kernel<S, NT>),    \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, int(slds)),     \
-          "hipFuncSetAttribute");                                                         \
-      if (rc != MDSX_OK) return rc;                                                       \
-    }                                                                                     \
-    mdsx::set_last_kernel("seg_decode_kernel<" #S ", " #NT ">");                         \
-    hipLaunchKernelGGL((seg_decode_kernel<S, NT>), dim3(grid), dim3(kRunBlock), slds, s, a); \
-    return hip_check(hipGetLastError(), "seg_decode_kernel launch");                      \
+    const unsigned sgrid = (a.ntiles + unsigned(W) - 1) / unsigned(W);
+#define MDSX_SEG_CASE(S, NT, WV)                                                               \
+  if (a.run_slots == S && bool(plan->run_nt) == NT && W == WV) {                               \
+    if (slds > 64 * 1024) {                                                                    \
+      const int rc = hip_check(                                                                \
+          hipFuncSetAttribute(reinterpret_cast<const void*>(seg_decode_kernel<S, NT, WV>),     \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, int(slds)),          \
+          "hipFuncSetAttribute");                                                              \
+      if (rc != MDSX_OK) return rc;                                                            \
+    }                                                                                          \
+    mdsx::set_last_kernel("seg_decode_kernel<" #S ", " #NT ", " #WV ">");                     \
+    hipLaunchKernelGGL((seg_decode_kernel<S, NT, WV>), dim3(sgrid), dim3(64 * WV), slds, s, a); \
+    return hip_check(hipGetLastError(), "seg_decode_kernel launch");                           \
   }
-    MDSX_SEG_CASE(4, true)
-    MDSX_SEG_CASE(4, false)
-    MDSX_SEG_CASE(8, true)
-    MDSX_SEG_CASE(8, false)
-    MDSX_SEG_CASE(16, true)
-    MDSX_SEG_CASE(16, false)
+#define MDSX_SEG_W(WV)         \
+  MDSX_SEG_CASE(4, true, WV)   \
+  MDSX_SEG_CASE(4, false, WV)  \
+  MDSX_SEG_CASE(8, true, WV)   \
+  MDSX_SEG_CASE(8, false, WV)  \
+  MDSX_SEG_CASE(16, true, WV)  \
+  MDSX_SEG_CASE(16, false, WV)
+    MDSX_SEG_W(1)
+    MDSX_SEG_W(2)
+    MDSX_SEG_W(4)
+#undef MDSX_SEG_W
 #undef MDSX_SEG_CASE
     return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode ring of 4, 8 or 16 KiB");
   }
