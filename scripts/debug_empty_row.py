@@ -12,7 +12,7 @@ from oracle import mds_oracle  # noqa: E402
 from tests import golden_util as gu  # noqa: E402
 
 MODES = {'default': '', 'gather': 'gmin=1000000000', 'group': 'gmin=0,gmax=1000000000',
-         'wave': 'gmin=0,gmax=0,ring=0', 'run': 'run=8', 'stage': 'stage=24'}
+         'wave': 'gmin=0,gmax=0,ring=0', 'run': 'run=8'}
 
 d = tempfile.mkdtemp()
 shutil.copytree(os.path.join(gu.GOLDEN, 'config_a'), d + '/a')

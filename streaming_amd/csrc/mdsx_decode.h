@@ -75,9 +75,7 @@ struct DevArgs {
   int16_t any_wave_str;  // some str column is copied by decode_kernel (validated there)
   int16_t any_wave_ragged;  // some ragged column is copied one row per wave
   int16_t str_cached;  // plan->str_cached
-  uint32_t stage_bytes;  // each of the two LDS stage buffers of the staged decode (bytes, 1 KiB multiple)
-  uint32_t stage_tiles;  // tiles per workgroup of the staged decode
-  uint32_t stage_debug;  // measurement only (MDSX_TUNE sdbg): parts of the staged decode skipped
+  uint32_t stage_debug;  // measurement only (MDSX_TUNE sdbg): parts of the row-parallel decode skipped
   uint32_t run_slots;    // KiB of the streaming decode's per-wave ring (0: not the streaming decode)
   uint32_t rows_bytes;   // LDS stage of the row-parallel decode (0: not the row-parallel decode)
   uint32_t seg_lim;      // streaming decode, lean path: largest sample it takes (0: lean path off)
@@ -165,16 +163,12 @@ __device__ __forceinline__ void report_decode(const DevArgs& a, int code, int sh
            1u << ((-code) & 31));
 }
 
-// measurement only (stage_debug & 16): 7 u64 cycle sums of the staged decode's phases
-constexpr uint64_t kStageTimeOffset = 200;
 constexpr uint64_t kStatusBlock = 256;
 
 // The LDS-staged decode of ragged plans (mdsx_stage.hip). Pass 1: the ragged bytes of every tile
 // (then scan_totals_kernel, one entry per tile: a.scan_per == 1). Pass 2: every column of every
 // row from each tile's shard bytes staged once in LDS. Return MDSX_OK or a launch error.
 int launch_stage_totals(const DevArgs& a, hipStream_t s, bool chained);
-int launch_stage_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s);
-uint32_t stage_tiles_per_wg(uint32_t ntiles);
 int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s);
 int launch_rows_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s);
 // The samples listed (tile << 32 | row in tile, a.src_abs; count at kHugeCountOffset) as larger

@@ -44,10 +44,7 @@ struct mdsx_plan {
   int nontemporal = 0;  // non-temporal loads/stores in the row copy
   int str_cached = 0;   // medium str rows stored temporally (the UTF-8 re-read then hits L2)
   int ring_slots = 0;   // long ragged rows through a per-wave LDS-DMA ring of this many KiB (0: off)
-  int stage_kb = 0;     // ragged plans: LDS stage of the staged decode in KiB (0: register copy)
-  int stage_tiles = 0;  // tiles per workgroup of the staged decode (0: per launch)
-  int stage_debug = 0;  // measurement only: parts of the staged decode skipped (bits)
-  int stage_fill = 70;  // percent of a stage buffer a tile's samples fill on average (tile sizing)
+  int stage_debug = 0;  // measurement only: parts of the row-parallel decode skipped (bits)
   int run_slots = 0;    // ragged plans: KiB of the streaming decode's per-wave LDS ring (0: off)
   int run_kb = 32;      // streaming decode: about this many KiB of samples per tile (tile sizing)
   int64_t run_min = 3072;  // streaming decode for batches whose samples average >= this many bytes

@@ -870,11 +870,8 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   const int tr = b->tile_rows ? int(b->tile_rows) : plan->tile_rows;
   if (tr < 1 || tr > kBlock || (tr & (tr - 1)))
     return mdsx::fail(MDSX_E_ARG, "mdsx: batch tile_rows must be a power of two in [1, 256]");
-  a->stage_bytes = plan->nvar > 0 ? uint32_t(plan->stage_kb) * 1024u : 0u;
-  a->stage_tiles = plan->stage_tiles ? uint32_t(plan->stage_tiles) : stage_tiles_per_wg(b->ntiles);
   a->stage_debug = uint32_t(plan->stage_debug);
   a->run_slots = use_run_decode(plan, b->bytes, b->rows) ? uint32_t(plan->run_slots) : 0u;
-  if (a->run_slots) a->stage_bytes = 0;  // the streaming decode takes precedence
   if (a->run_slots && plan->seg) {
     // lean path: a sample must fit the ring with a slot to spare (seg_decode_kernel)
     a->seg_lim = a->run_slots * 1024u - 1024u - 32u;
@@ -890,12 +887,11 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   // decode)
   if (a->rows_bytes && rows_lds_bytes_est(plan, a->rows_bytes, uint64_t(tr)) > 160 * 1024)
     a->rows_bytes = 0;
-  if (a->rows_bytes) a->stage_bytes = 0;
   if (a->run_slots && tr > 32)
     return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode tiles hold at most 32 rows");
   // the staged and streaming decodes scan one total per tile; the register-copy decode one per
   // 256 rows
-  a->scan_per = (a->stage_bytes || a->run_slots || a->rows_bytes) ? 1u : uint32_t(kBlock / tr);
+  a->scan_per = (a->run_slots || a->rows_bytes) ? 1u : uint32_t(kBlock / tr);
   a->nscan = (b->ntiles + a->scan_per - 1) / a->scan_per;
   a->nchunk = (a->nscan + kScanChunk - 1) / kScanChunk;
   a->nshards = b->nshards;
@@ -1294,7 +1290,7 @@ int mdsx_scan_shards(const mdsx_plan* plan, const mdsx_batch* batch, const mdsx_
     if (rc != MDSX_OK) return rc;
     return launch_stage_totals(a, s, true);
   }
-  if (a.ntiles > 0 && (a.stage_bytes || a.run_slots || a.rows_bytes)) {
+  if (a.ntiles > 0 && (a.run_slots || a.rows_bytes)) {
     rc = launch_stage_totals(a, s, false);
     if (rc != MDSX_OK) return rc;
   } else if (a.ntiles > 0) {
@@ -1323,7 +1319,6 @@ static int launch_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s,
   int rc = MDSX_OK;
   if (plan->nvar > 0 && !single && a.run_slots > 0) return launch_run_decode(plan, a, s);
   if (plan->nvar > 0 && !single && a.rows_bytes > 0) return launch_rows_decode(plan, a, s);
-  if (plan->nvar > 0 && !single && a.stage_bytes > 0) return launch_stage_decode(plan, a, s);
   const size_t lds =
       size_t(a.tile_rows) * (12 * size_t(plan->nvar) + 4 * size_t(plan->ncols) + 1) + 16;
   const bool nt = plan->nontemporal != 0, ragged = plan->nvar > 0;

@@ -201,14 +201,8 @@ void apply_tuning(mdsx_plan* p) {
       p->str_cached = v ? 1 : 0;
     } else if (key == "ring" && (v == 0 || v == 4 || v == 6 || v == 8)) {
       p->ring_slots = int(v);
-    } else if (key == "stiles" && v >= 0 && v <= 1024) {
-      p->stage_tiles = int(v);
     } else if (key == "sdbg" && v >= 0) {
       p->stage_debug = int(v);
-    } else if (key == "stage" && v >= 0 && v <= 96) {
-      p->stage_kb = int(v);
-    } else if (key == "fill" && v >= 10 && v <= 400) {  // > 100: tiles overflow the stage
-      p->stage_fill = int(v);
     } else if (key == "run" && (v == 0 || v == 4 || v == 8 || v == 16)) {
       p->run_slots = int(v);
     } else if (key == "rmin" && v >= 0) {
@@ -331,12 +325,6 @@ int mdsx_plan_create(const char* const* encodings, const int64_t* column_sizes, 
   // output hits L2 instead of HBM: config C 1.94-2.01 vs 2.06-2.10 ms; 1-3 KiB blobs + 200-400-
   // code-point strings 1.51 vs 1.56 ms (tune/strc_*.json).
   p->str_cached = 1;
-  // The staged decode (mdsx_stage.hip: each tile's shard bytes read once into LDS, every column
-  // written from there) is opt-in (MDSX_TUNE=stage=24): its per-tile phases are chains of
-  // dependent LDS round trips behind block barriers, measured at 0.6-0.9 TB/s on config C against
-  // 4.3 TB/s for the register/ring decode, and 0.56-0.71 vs 0.89 TB/s on short rows
-  // (scripts/gpu_stage_dbg.sh, profiles/r02/stage_phases.txt).
-  p->stage_kb = 0;
   // Ragged batches of long samples decode through the streaming decode (mdsx_run.hip, 4 KiB ring
   // per wave): every shard byte read once, whole-chunk stores (use_run_decode).
   p->run_slots = p->nvar > 0 ? 4 : 0;
@@ -346,7 +334,6 @@ int mdsx_plan_create(const char* const* encodings, const int64_t* column_sizes, 
   // Its shard loads and output stores non-temporal: 1-3 % faster on 0.25-2.5 KB samples
   // (profiles/r02/rows_nt_crossover.jsonl).
   p->rows_nt = 1;
-  p->stage_fill = 70;
   apply_tuning(p);
   *out = p;
   return MDSX_OK;
@@ -370,12 +357,7 @@ int mdsx_plan_tile_rows_for(const mdsx_plan* plan, uint64_t shard_bytes, uint64_
     return tr;
   }
   if (use_rows_decode(plan, shard_bytes, rows)) return rows_tile_rows(plan, shard_bytes / rows);
-  if (plan->nvar == 0 || plan->stage_kb == 0 || rows == 0) return plan->tile_rows;
-  const uint64_t target = uint64_t(plan->stage_kb) * 1024 * uint64_t(plan->stage_fill) / 100;
-  const uint64_t per_row = std::max<uint64_t>(1, shard_bytes / rows);
-  int tr = 1;
-  while (tr < 256 && uint64_t(tr) * 2 * per_row <= target) tr *= 2;
-  return tr;
+  return plan->tile_rows;
 }
 
 int mdsx_plan_encode_tile_rows(const mdsx_plan* plan) {

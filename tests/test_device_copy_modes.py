@@ -6,8 +6,6 @@ measurement knobs (MDSX_TUNE, read at plan creation).
 * The streaming decode for every sample size, with small, default and large rings / tiles.
 * The row-parallel decode for every sample size: a fixed 32 KiB stage, the per-batch sizing, and
   a 2 KiB stage (tiles in several windows, samples over 2 KiB through the huge-row kernel).
-* The LDS-staged decode (opt-in, mdsx_stage.hip) at its default stage, with tiles overflowing a
-  small stage, a 1 KiB stage (the huge-row kernel) and a large stage.
 * The register-copy decode (run=0,rows=0): destination-major gather kernel (short rows), four rows
   per wave in 16-lane groups (medium rows), one row per wave (long rows), the last either from
   registers or through the per-wave LDS-DMA ring (8 or 4 slots).
@@ -52,16 +50,12 @@ MODES = {
     'rows_auto': 'rows=-1,rmin=1000000000',  # ... its tiles and stage sized per batch
     'rows_small': 'rows=2,rmin=1000000000',  # a 2 KiB stage: windows and HBM-direct samples
     'rows_temporal': 'rows=-1,rownt=0,rmin=1000000000',  # temporal loads / stores (default: nt)
-    'stage': 'stage=24,run=0,rows=0',  # the staged decode (opt-in; measured slower)
-    'stage_overflow': 'stage=4,fill=300,run=0,rows=0',  # tiles of ~3x the stage: several row groups each
-    'stage_tiny': 'stage=1,run=0,rows=0',  # rows over 1 KiB go through the huge-row kernel
-    'stage_big': 'stage=64,fill=90,run=0,rows=0',
-    'gather': 'stage=0,run=0,rows=0,gmin=1000000000',
-    'group': 'stage=0,run=0,rows=0,gmin=0,gmax=1000000000',
-    'group_nt': 'stage=0,run=0,rows=0,gmin=0,gmax=1000000000,strc=0',  # str rows streamed (non-temporal) too
-    'wave': 'stage=0,run=0,rows=0,gmin=0,gmax=0,ring=0',
-    'ring': 'stage=0,run=0,rows=0,gmin=0,gmax=0,ring=8',   # one row per wave through the LDS-DMA ring
-    'ring4': 'stage=0,run=0,rows=0,gmin=0,gmax=0,ring=4',
+    'gather': 'run=0,rows=0,gmin=1000000000',
+    'group': 'run=0,rows=0,gmin=0,gmax=1000000000',
+    'group_nt': 'run=0,rows=0,gmin=0,gmax=1000000000,strc=0',  # str rows streamed (non-temporal) too
+    'wave': 'run=0,rows=0,gmin=0,gmax=0,ring=0',
+    'ring': 'run=0,rows=0,gmin=0,gmax=0,ring=8',   # one row per wave through the LDS-DMA ring
+    'ring4': 'run=0,rows=0,gmin=0,gmax=0,ring=4',
 }
 
 

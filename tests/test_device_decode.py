@@ -162,8 +162,8 @@ def test_config_b_full_size_round_trip():
 
 
 def test_config_c_full_shards_round_trip(tmp_path):
-    """BASELINE config C schema at full 64 MiB shard size (3 shards), vs the source columns and,
-    on the first shard's first samples, vs the oracle reading the shard file."""
+    """BASELINE config C schema at full 64 MiB shard size (3 shards), vs the source columns and vs
+    the oracle reading the shard files (every sample)."""
     shards, counts, src = var_c_shards(45_000, seed=5)
     assert len(counts) == 3 and counts[0] > 14_000
     names = ['b', 'n', 's']
@@ -179,19 +179,34 @@ def test_config_c_full_shards_round_trip(tmp_path):
     assert np.array_equal(s.values.cpu().numpy(), src['s_pool'])
     assert int(s.flags.sum()) == 0
     assert dec.rows == 45_000
-    # same result against the oracle on the first shard's first samples
-    (tmp_path / 'shard.00000.mds').write_bytes(shards[0])
+    # the same decode against the oracle reading the three shard files, every sample
+    want = {c: [] for c in names}
+    for k, (data, n) in enumerate(zip(shards, counts)):
+        (tmp_path / f'shard.{k:05d}.mds').write_bytes(data)
+        info = {'column_names': names, 'column_encodings': ['bytes', 'int', 'str'],
+                'column_sizes': [None, 8, None], 'samples': n,
+                'raw_data': {'basename': f'shard.{k:05d}.mds'}}
+        for c, v in mds_oracle.decode_shard_columns(str(tmp_path), None, info).items():
+            want[c].append(v)
+    assert np.array_equal(dec['n'].cpu().numpy().view(np.uint8).reshape(-1, 8),
+                          np.concatenate([v[1] for v in want['n']]))
+    for c, col in (('b', b), ('s', s)):
+        assert np.array_equal(col.values.cpu().numpy(), np.concatenate([v[1] for v in want[c]]))
+        assert np.array_equal(np.diff(col.offsets.cpu().numpy()),
+                              np.concatenate([np.diff(v[2]) for v in want[c]]))
+    assert np.array_equal(s.flags.cpu().numpy(), np.concatenate([v[3] for v in want['s']]))
+    # and the oracle's per-sample reader (reference value types) at both ends of the first shard
     info = {'column_names': names, 'column_encodings': ['bytes', 'int', 'str'],
             'column_sizes': [None, 8, None], 'samples': counts[0],
             'raw_data': {'basename': 'shard.00000.mds'}}
     ref = mds_oracle.OracleMDSReader(str(tmp_path), None, info)
     bo, so = b.offsets.cpu().numpy(), s.offsets.cpu().numpy()
     bv, sv, nv = b.values.cpu().numpy(), s.values.cpu().numpy(), dec['n'].cpu().numpy()
-    for i in list(range(300)) + [counts[0] - 1]:
-        want = ref.get_item(i)
-        assert want['n'] == int(nv[i])
-        assert want['b'] == bv[bo[i]:bo[i + 1]].tobytes()
-        assert want['s'] == sv[so[i]:so[i + 1]].tobytes().decode('utf-8')
+    for i in list(range(50)) + [counts[0] - 1]:
+        item = ref.get_item(i)
+        assert item['n'] == int(nv[i])
+        assert item['b'] == bv[bo[i]:bo[i + 1]].tobytes()
+        assert item['s'] == sv[so[i]:so[i + 1]].tobytes().decode('utf-8')
 
 
 def _random_dataset(tmp_path, seed):

@@ -29,7 +29,7 @@ MODES = {
     'seg_1': 'run=8,seg=1,rmin=0,swin=1',
     'seg_chain': 'run=8,seg=1,rmin=0,chain=1,swg=2',
     'rows_small': 'rows=2,rmin=1000000000',  # row-parallel, 2 KiB stage (windows, huge rows)
-    'register': 'stage=0,run=0,rows=0',  # the register decode (+ gather / groups per column)
+    'register': 'run=0,rows=0',  # the register decode (+ gather / groups per column)
 }
 
 

@@ -125,8 +125,8 @@ def test_tile_rows_for_sizes_ragged_tiles_to_the_decode(monkeypatch):
     """Ragged plans: batches of long samples (>= 3 KiB on average) go to the streaming decode,
     whose tiles hold 16-32 KiB of samples (1..32 rows); shorter samples to the row-parallel
     decode, whose tiles fill at most 8/9 of a 20 KiB (samples < 512 B) or 40 KiB stage (1..256
-    rows, the workgroup's LDS within 160 KiB); the staged decode (opt-in) sizes tiles to ~70 % of
-    its 24 KiB stage; all-fixed plans: the plan's tile size whatever the batch."""
+    rows, the workgroup's LDS within 160 KiB); the register decode and all-fixed plans: the plan's
+    tile size whatever the batch."""
     from streaming_amd.decoder import Plan
     c = Plan(['b', 'n', 's'], ['bytes', 'int', 'str'], [None, 8, None])
     assert c.tile_rows_for(1 << 26, (1 << 26) // 100) == 128  # 100-byte samples: row-parallel
@@ -143,12 +143,10 @@ def test_tile_rows_for_sizes_ragged_tiles_to_the_decode(monkeypatch):
     assert Plan(['b'], ['bytes'], [None]).tile_rows_for(1 << 26, (1 << 26) // 100) == 128
     monkeypatch.setenv('MDSX_TUNE', 'run=4,rkb=256')
     assert Plan(['b'], ['bytes'], [None]).tile_rows_for(1 << 26, 15_700) == 32
-    monkeypatch.setenv('MDSX_TUNE', 'stage=24,run=0,rows=0')
+    monkeypatch.setenv('MDSX_TUNE', 'run=0,rows=0')  # the register decode: the plan's tiles
     c = Plan(['b', 'n', 's'], ['bytes', 'int', 'str'], [None, 8, None])
-    assert c.tile_rows_for(1 << 26, 15_700) == 4  # ~4.3 KB rows: 4-row tiles (~17 KB)
-    assert c.tile_rows_for(1 << 26, (1 << 26) // 100) == 128  # 100-byte rows
-    assert c.tile_rows_for(1 << 26, 10) == 1  # 6.7 MB rows: one per tile (huge-row kernel)
-    assert c.tile_rows_for(1 << 26, 1 << 26) == 256  # 1-byte rows: capped
+    assert c.tile_rows_for(1 << 26, 15_700) == c.tile_rows == 32
+    assert c.tile_rows_for(1 << 26, (1 << 26) // 100) == 32
     b = Plan(['id', 'x'], ['int32', 'ndarray:float32:1024'], [4, 4096])
     assert b.tile_rows_for(1 << 26, 16_352) == b.tile_rows
 
