@@ -94,8 +94,12 @@ def main():
     from streaming_amd import _native
     lib = _native.lib()
     nprobe = (base_batch.buffer.numel() // 16) * 16
-    for _ in range(args.rounds):
-        for v, dec in decs.items():
+    for rnd in range(args.rounds):
+        # the variants' order rotates every round: a variant's rate depends on its position in a
+        # round (the GPU's state after the previous one), so each one takes every position
+        order = list(decs.items())
+        order = order[rnd % len(order):] + order[:rnd % len(order)]
+        for v, dec in order:
             evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)]
                    for _ in range(args.iters)]
             for e in evs:

@@ -59,8 +59,7 @@ struct DevArgs {
   uint64_t* src_abs;     // [nvar][rows]  byte index into the batch of each row's ragged value
   uint32_t* row_map;     // [nvar][map_len] first row of every gather tile
   uint64_t* lookback;    // [nvar][ntiles] single-pass look-back status words
-  uint32_t* ticket;      // single-pass tile ticket counter (also the chained totals' blocks)
-  uint64_t* chain;       // [nvar][blocks] chained totals look-back status words (run decodes)
+  uint32_t* ticket;      // single-pass tile ticket counter
   uint64_t map_len;
   uint64_t rows;
   uint32_t ntiles;
@@ -80,7 +79,6 @@ struct DevArgs {
   uint32_t rows_bytes;   // LDS stage of the row-parallel decode (0: not the row-parallel decode)
   uint32_t seg_lim;      // streaming decode, lean path: largest sample it takes (0: lean path off)
   uint32_t seg_small;    // lean path: bytes per row of the fixed columns of <= 16 bytes
-  uint32_t seg_win;      // lean path: samples per window at most (1: one sample at a time)
   uint32_t gather_block0[MDSX_MAX_COLUMNS + 1];  // first gather workgroup of each ragged column
   DevCol cols[MDSX_MAX_COLUMNS];
 };
@@ -168,7 +166,7 @@ constexpr uint64_t kStatusBlock = 256;
 // The LDS-staged decode of ragged plans (mdsx_stage.hip). Pass 1: the ragged bytes of every tile
 // (then scan_totals_kernel, one entry per tile: a.scan_per == 1). Pass 2: every column of every
 // row from each tile's shard bytes staged once in LDS. Return MDSX_OK or a launch error.
-int launch_stage_totals(const DevArgs& a, hipStream_t s, bool chained);
+int launch_stage_totals(const DevArgs& a, hipStream_t s);
 int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s);
 int launch_rows_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s);
 // The samples listed (tile << 32 | row in tile, a.src_abs; count at kHugeCountOffset) as larger

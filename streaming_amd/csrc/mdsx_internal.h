@@ -48,13 +48,11 @@ struct mdsx_plan {
   int run_slots = 0;    // ragged plans: KiB of the streaming decode's per-wave LDS ring (0: off)
   int run_kb = 32;      // streaming decode: about this many KiB of samples per tile (tile sizing)
   int64_t run_min = 3072;  // streaming decode for batches whose samples average >= this many bytes
-  int run_nt = 0;          // streaming decode: non-temporal ring loads and stores (measured: the
-                           // temporal ones let L2 merge the partial stores at run edges)
+  int run_nt = 0;          // streaming decode: non-temporal ring loads and stores (the lean path
+                           // is faster with them; the general one alone was slower)
   int seg = 0;             // streaming decode: the lean path for clean runs of samples that fit
                            // the ring (seg_decode_kernel; others take the general path)
-  int chain = 0;            // streaming decodes: totals scan chained into the totals pass
   int seg_waves = 4;        // lean path: waves (runs) per workgroup (1, 2 or 4)
-  int seg_win = 32;         // lean path: samples per window at most (1..32; 1: one at a time)
   int rows_kb = 0;         // row-parallel decode of shorter samples: LDS stage in KiB (0: off,
                            // -1: sized per batch, rows_tile_rows / rows_stage_bytes)
   int rows_nt = 1;         // row-parallel decode: non-temporal loads and stores (measured faster)

@@ -811,7 +811,7 @@ __global__ __launch_bounds__(kBlock) void gather_ragged_kernel(const DevArgs a) 
 
 // ---------------------------------------------------------------------------------------------
 struct Layout {
-  uint64_t tile_total, tile_prefix, chunk_sum, tile_run, src_abs, row_map, chain, map_len, total;
+  uint64_t tile_total, tile_prefix, chunk_sum, tile_run, src_abs, row_map, map_len, total;
 };
 
 __host__ uint64_t round256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
@@ -830,8 +830,7 @@ Layout workspace_layout(const mdsx_plan* plan, const mdsx_batch* b) {
   L.tile_run = L.chunk_sum + round256(nv * (b->ntiles / kScanChunk + 1) * 8);
   L.src_abs = L.tile_run + round256(nv ? uint64_t(b->ntiles) * sizeof(TileRun) : 0);
   L.row_map = L.src_abs + round256(nv * b->rows * 8);
-  L.chain = L.row_map + round256(nv * L.map_len * 4);
-  L.total = L.chain + round256(nv * (uint64_t(b->ntiles) + 1) * 8);
+  L.total = L.row_map + round256(nv * L.map_len * 4);
   return L;
 }
 
@@ -862,7 +861,6 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   a->row_map = reinterpret_cast<uint32_t*>(ws + L.row_map);
   a->lookback = reinterpret_cast<uint64_t*>(ws + L.tile_total);  // single pass: no tile totals
   a->ticket = reinterpret_cast<uint32_t*>(ws + kTicketOffset);
-  a->chain = reinterpret_cast<uint64_t*>(ws + L.chain);
   a->map_len = L.map_len;
   a->totals = d_totals;
   a->rows = b->rows;
@@ -875,7 +873,6 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   if (a->run_slots && plan->seg) {
     // lean path: a sample must fit the ring with a slot to spare (seg_decode_kernel)
     a->seg_lim = a->run_slots * 1024u - 1024u - 32u;
-    a->seg_win = plan->seg_win > 0 ? uint32_t(plan->seg_win) : 1u;
     for (int c = 0; c < plan->ncols; ++c)
       if (plan->cols[c].kind == MDSX_KIND_FIXED && plan->cols[c].row_bytes <= kSmallMax)
         a->seg_small += uint32_t(plan->cols[c].row_bytes);
@@ -1280,18 +1277,8 @@ int mdsx_scan_shards(const mdsx_plan* plan, const mdsx_batch* batch, const mdsx_
   hipStream_t s = static_cast<hipStream_t>(stream);
   rc = hip_check(hipMemsetAsync(d_workspace, 0, kStatusBlock, s), "hipMemsetAsync");
   if (rc != MDSX_OK || plan->nvar == 0) return rc;
-  // streaming decodes (tiles of <= 32 rows): the totals scan chained into the totals pass
-  const bool chained = plan->chain && a.run_slots && a.ntiles > 0;
-  if (chained) {
-    const uint32_t per = uint32_t(kBlock / a.tile_rows);
-    const uint64_t blocks = (uint64_t(a.ntiles) + per - 1) / per;
-    rc = hip_check(hipMemsetAsync(a.chain, 0, size_t(plan->nvar) * blocks * 8, s),
-                   "hipMemsetAsync");
-    if (rc != MDSX_OK) return rc;
-    return launch_stage_totals(a, s, true);
-  }
   if (a.ntiles > 0 && (a.run_slots || a.rows_bytes)) {
-    rc = launch_stage_totals(a, s, false);
+    rc = launch_stage_totals(a, s);
     if (rc != MDSX_OK) return rc;
   } else if (a.ntiles > 0) {
     hipLaunchKernelGGL(scan_tiles_kernel, dim3(a.nscan), dim3(kBlock), 0, s, a);

@@ -213,12 +213,8 @@ void apply_tuning(mdsx_plan* p) {
       p->rows_kb = int(v);
     } else if (key == "rownt") {
       p->rows_nt = v ? 1 : 0;
-    } else if (key == "chain") {
-      p->chain = v ? 1 : 0;
     } else if (key == "swg" && (v == 1 || v == 2 || v == 4)) {
       p->seg_waves = int(v);
-    } else if (key == "swin" && v >= 1 && v <= 32) {
-      p->seg_win = int(v);
     } else if (key == "seg") {
       p->seg = v ? 1 : 0;
     } else if (key == "rkb" && v >= 1 && v <= 4096) {
@@ -325,9 +321,16 @@ int mdsx_plan_create(const char* const* encodings, const int64_t* column_sizes, 
   // output hits L2 instead of HBM: config C 1.94-2.01 vs 2.06-2.10 ms; 1-3 KiB blobs + 200-400-
   // code-point strings 1.51 vs 1.56 ms (tune/strc_*.json).
   p->str_cached = 1;
-  // Ragged batches of long samples decode through the streaming decode (mdsx_run.hip, 4 KiB ring
-  // per wave): every shard byte read once, whole-chunk stores (use_run_decode).
-  p->run_slots = p->nvar > 0 ? 4 : 0;
+  // Ragged batches of long samples decode through the streaming decode (mdsx_run.hip): every
+  // shard byte read once, whole-chunk stores (use_run_decode). Its lean path (seg_decode_kernel:
+  // one wait per sample, lane-parallel column geometry) needs a sample to fit the per-wave ring
+  // with a slot to spare, so the ring is 8 KiB; non-temporal ring loads and stores. Config C
+  // (scan + decode, three boxes, interleaved in one process each): 5.37 / 4.94 / 4.88 TB/s
+  // against 4.69 / 4.62 / 4.60 for the round-2 streaming decode (4 KiB ring, temporal);
+  // 16 KiB rings lose half the waves per CU (3.8-3.9 TB/s) (profiles/r03/ab/).
+  p->run_slots = p->nvar > 0 ? 8 : 0;
+  p->seg = 1;
+  p->run_nt = 1;
   // ... and shorter samples through the row-parallel decode (mdsx_rows.hip), its tiles and stage
   // sized per batch (rows_tile_rows).
   p->rows_kb = p->nvar > 0 ? -1 : 0;

@@ -366,21 +366,9 @@ __global__ __launch_bounds__(kRunBlock, 7) void run_decode_kernel(const DevArgs 
 // zero-length rule.
 
 // per-wave LDS of the lean path: the general path's, then the staged small fixed columns
-constexpr int kWinMax = kRunMaxRows;  // samples of a window: one per lane
-
-__host__ __device__ __forceinline__ uint32_t seg_small_off(int S, int TR, int nvar) {
-  return run_wave_lds(S, TR, nvar);
-}
-// window records after the small stage: [ncols][kWinMax] output position, stream position, length
-// (u32 each), then [ncols] UTF-8 failure bits
-__host__ __device__ __forceinline__ uint32_t seg_rec_off(int S, int TR, int nvar,
-                                                         uint32_t small) {
-  return seg_small_off(S, TR, nvar) + ((small * uint32_t(TR) + 15u) & ~15u);
-}
-__host__ __device__ __forceinline__ uint32_t seg_wave_lds(int S, int TR, int nvar, int ncols,
-                                                          uint32_t small, bool windows) {
-  return seg_rec_off(S, TR, nvar, small) +
-         (windows ? uint32_t(ncols) * (3u * kWinMax * 4u + 4u) : 0u);
+__host__ __device__ __forceinline__ uint32_t seg_wave_lds(int S, int TR, int nvar,
+                                                          uint32_t small) {
+  return run_wave_lds(S, TR, nvar) + ((small * uint32_t(TR) + 15u) & ~15u);
 }
 
 // One value of a wide column, all of its stream bytes landed: output bytes [d, d + len) (relative
@@ -430,159 +418,6 @@ __device__ __forceinline__ bool seg_copy(const lds_u8* ring, uint64_t base, uint
   return utf8 ? __any(bad) != 0 : false;
 }
 
-// One wide column of a window of m samples, all of their stream bytes landed: output bytes
-// [D, D + T) (relative to `base`), value i at window output bytes [wd[i], wd[i] + wl[i]) from
-// stream bytes [wp[i], ...) (wp[i] = ~0: zeros, a sample that failed its checks). Lane k of a
-// step assembles 16-byte output chunk k from the value(s) it covers (the first by binary search
-// over wd, one unaligned ring read per value piece), checks str pieces for strict UTF-8 (each
-// value in its own context, a failing value's bit set in *bad) and stores the chunk whole; the
-// window's first chunk takes the carried bytes, its partly filled last chunk is carried.
-template <int S, bool kNT>
-__device__ __forceinline__ void win_copy(const lds_u8* ring, const MDSX_L uint32_t* wd,
-                                         const MDSX_L uint32_t* wp, const MDSX_L uint32_t* wl,
-                                         int m, uint64_t base, uint32_t cst, uint32_t D,
-                                         uint32_t T, bool utf8, MDSX_L uint32_t* bad,
-                                         uint4& carry, uint32_t& ops, int lane) {
-  const uint32_t head = D & 15u, dbeg = D - head, dend = D + T;
-  const uint32_t nch = (dend - dbeg + 15u) >> 4;
-  const uint32_t nfull = (dend - dbeg) >> 4;
-  const uint32_t tail = dend & 15u;
-  const bool shared0 = dbeg < cst;
-  const uint64_t out = base + dbeg;
-  uint4 last = carry;
-  for (uint32_t g = 0; g < nch; g += 64) {  // wave-uniform
-    const uint32_t q = g + uint32_t(lane);
-    const int32_t x0 = int32_t(16u * q) - int32_t(head);  // window output byte of chunk byte 0
-    uint4 val = make_uint4(0, 0, 0, 0);
-    if (q < nch) {
-      int32_t x = max(x0, 0);
-      const int32_t hi = min(x0 + 16, int32_t(T));
-      // the value holding byte x: the last i with wd[i] <= x
-      int i = 0;
-      for (int w = 16; w > 0; w >>= 1)
-        if (i + w < m && int32_t(wd[i + w]) <= x) i += w;
-      while (x < hi) {  // the chunk's pieces, one value each
-        const int32_t ds = int32_t(wd[i]), de = ds + int32_t(wl[i]);
-        const int32_t pe = min(hi, de);
-        if (pe > x) {
-          const uint32_t sp = wp[i];
-          const uint4 v = sp == 0xffffffffu ? make_uint4(0, 0, 0, 0)
-                                            : ring16<S>(ring, sp - uint32_t(ds) + uint32_t(x0));
-          const uint4 piece = keep_bytes(v, uint32_t(x - x0), uint32_t(pe - x0));
-          val = make_uint4(val.x | piece.x, val.y | piece.y, val.z | piece.z, val.w | piece.w);
-          if (utf8) {
-            // the value's dword before the chunk, when the value started before it
-            uint32_t pw = 0;
-            if (x == x0 && x > ds) {
-              pw = ring_u32<S>(ring, sp - uint32_t(ds) + uint32_t(x0) - 4u);
-              const int32_t nv = x0 - ds;  // the value's bytes before the chunk
-              if (nv < 4) pw &= ~((1u << (8 * (4 - nv))) - 1u);
-            }
-            if (utf8_chunk_bad(piece, pw, pe == de)) atomicOr(bad, 1u << i);
-          }
-          x = pe;
-        }
-        ++i;
-      }
-    }
-    if (g == 0 && head && lane == 0) val = splice_lo(carry, val, head);
-    const bool skip0 = shared0 && g == 0;
-    if (q < nfull && !(skip0 && lane == 0)) st16<kNT>(out + 16ull * q, val);
-    if (min(nfull, g + 64u) > g + (skip0 ? 1u : 0u)) ++ops;  // that store was issued
-    if (skip0 && nfull > 0) wave_edge_store(val, 0, out, base + cst, out + 16, lane);
-    if (tail && nch - 1 - g < 64u) last = readlane4(val, int(nch - 1 - g));
-  }
-  carry = last;
-}
-
-// A window of m >= 2 consecutive samples (j .. j + m - 1; lane i: sample j + i), its bytes in
-// the ring together: each sample's size heads and column boundaries lane-parallel, every
-// column's window output by a wave prefix sum, the small fixed columns staged, each wide column
-// copied by win_copy over the window's whole output range.
-template <int S, bool kNT>
-__device__ __forceinline__ void seg_window(
-    const DevArgs& a, const MDSX_L DevCol* cols, Stream& st, const lds_u8* ring,
-    uint32_t ring_lds, uint32_t ob, uint64_t shard, uint64_t sbase, int j, int m, int TR,
-    const TileRun& r, int vi, uint32_t rb, uint32_t meta, bool small, uint64_t small_mask,
-    uint64_t wide_mask, uint32_t soff, uint32_t cst, uint64_t base, uint32_t& cur, uint4& carry,
-    MDSX_L uint32_t* obuf, MDSX_L uint8_t* fbuf, MDSX_L uint8_t* sbuf, MDSX_L uint32_t* wrec,
-    MDSX_L uint32_t* wbad, int lane) {
-  const int ncols = a.ncols;
-  const uint32_t hv = 4u * uint32_t(a.nvar);
-  const bool live = lane < m;
-  const int li = j + min(lane, m - 1);
-  const uint32_t wb = uint32_t(__shfl(int(ob), li)), we = uint32_t(__shfl(int(ob), li + 1));
-  const uint32_t w0 = uint32_t(__builtin_amdgcn_readlane(int(ob), j));
-  const uint32_t w1 = uint32_t(__builtin_amdgcn_readlane(int(ob), j + m));
-  const uint32_t sp0 = uint32_t(shard + w0 - sbase);
-  ensure<S, kNT>(st, ring, ring_lds, sp0, sp0 + (w1 - w0) + 15u, lane);  // the whole window
-  const uint32_t size = we - wb;
-  const uint32_t spi = uint32_t(shard + wb - sbase);  // stream position of this lane's sample
-  // the boundary check (mds/reader.py:111-125): heads and columns inside the sample
-  bool ok = live && hv <= size;
-  {
-    uint64_t need = hv;
-    for (int c = 0; c < ncols && ok; ++c) {
-      const int v = cols[c].var_index;
-      need += v >= 0 ? ring_u32<S>(ring, spi + 4u * uint32_t(v)) : cols[c].row_bytes;
-    }
-    ok = ok && need <= size;
-  }
-  if (live && !ok) report_decode(a, MDSX_E_BOUNDS, int(r.shard), int(r.r0) + j + lane, -1);
-  // every column: the window's output by a prefix sum over the samples
-  uint32_t rel = hv;
-  uint32_t Tw = 0;  // lane c: the window's output bytes of column c
-  for (int c = 0; c < ncols; ++c) {  // wave-uniform
-    const int v = cols[c].var_index;
-    const uint32_t w = cols[c].row_bytes;
-    uint32_t len = 0;
-    if (live) len = ok ? (v >= 0 ? ring_u32<S>(ring, spi + 4u * uint32_t(v)) : w) : (v >= 0 ? 0u : w);
-    const uint32_t incl = wave_incl_u32(len, lane, m);
-    const uint32_t T = uint32_t(__builtin_amdgcn_readlane(int(incl), m - 1));
-    if (lane == c) Tw = T;
-    const uint32_t d = incl - len;
-    const uint32_t pos = spi + rel;
-    if (live) {
-      wrec[(3 * c) * kWinMax + lane] = d;
-      wrec[(3 * c + 1) * kWinMax + lane] = ok ? pos : 0xffffffffu;
-      wrec[(3 * c + 2) * kWinMax + lane] = len;
-    }
-    if (v >= 0) {
-      const uint32_t cu = uint32_t(__builtin_amdgcn_readlane(int(cur), c));
-      if (live) {
-        obuf[v * TR + j + lane] = cu + d;
-        fbuf[v * TR + j + lane] = 0;
-      }
-    } else if (w <= uint32_t(kSmallMax)) {
-      const uint32_t so = uint32_t(__builtin_amdgcn_readlane(int(soff), c));
-      if (live)
-        lds_put(sbuf + so + uint32_t(j + lane) * w,
-                ok ? ring16<S>(ring, pos) : make_uint4(0, 0, 0, 0), w);
-    }
-    if (ok) rel += len;
-  }
-  // the wide columns, one window-wide copy each
-  for (uint64_t mk = wide_mask; mk; mk &= mk - 1) {
-    const int c = __builtin_ctzll(mk);
-    const uint32_t T = uint32_t(__builtin_amdgcn_readlane(int(Tw), c));
-    if (T == 0) continue;
-    const uint32_t D = uint32_t(__builtin_amdgcn_readlane(int(cur), c));
-    const uint32_t mc = uint32_t(__builtin_amdgcn_readlane(int(meta), c));
-    const bool utf8 = (mc >> 8) & 1u;
-    if (utf8 && lane == 0) wbad[c] = 0;
-    uint4 cy = (D & 15u) ? readlane4(carry, c) : make_uint4(0, 0, 0, 0);
-    win_copy<S, kNT>(ring, wrec + (3 * c) * kWinMax, wrec + (3 * c + 1) * kWinMax,
-                     wrec + (3 * c + 2) * kWinMax, m, readlane64(base, c),
-                     uint32_t(__builtin_amdgcn_readlane(int(cst), c)), D, T, utf8, wbad + c, cy,
-                     st.ops, lane);
-    if (lane == c) {
-      cur = D + T;
-      carry = cy;
-    }
-    if (utf8 && live && ((wbad[c] >> lane) & 1u)) fbuf[(int(mc & 255u) - 1) * TR + j + lane] = 1;
-  }
-}
-
 // The column table of a lean-path workgroup, ahead of the waves' LDS (dynamic, ncols entries).
 __host__ __device__ __forceinline__ uint32_t seg_cols_lds(int ncols) {
   return (uint32_t(ncols) * uint32_t(sizeof(DevCol)) + 15u) & ~15u;
@@ -602,8 +437,7 @@ __global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) 
   if (tile >= a.ntiles) return;  // wave-uniform; no barrier below
   const int TR = a.tile_rows;
   const int ncols = a.ncols, nvar = a.nvar;
-  uint8_t* wl = smem + seg_cols_lds(ncols) +
-                size_t(wave) * seg_wave_lds(S, TR, nvar, ncols, a.seg_small, a.seg_win > 1);
+  uint8_t* wl = smem + seg_cols_lds(ncols) + size_t(wave) * seg_wave_lds(S, TR, nvar, a.seg_small);
   const TileRun r = a.tile_run[tile];
   if (!(r.fast & 2)) {
     run_body<S, kNT>(a, cols, tile, r, wl, lane);
@@ -612,9 +446,7 @@ __global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) 
   const lds_u8* ring = (const lds_u8*)wl;
   MDSX_L uint32_t* obuf = (MDSX_L uint32_t*)(wl + S * 1024 + kMirror);  // [nvar][TR]
   MDSX_L uint8_t* fbuf = (MDSX_L uint8_t*)(wl + S * 1024 + kMirror + nvar * TR * 4);  // [nvar][TR]
-  MDSX_L uint8_t* sbuf = (MDSX_L uint8_t*)(wl + seg_small_off(S, TR, nvar));  // small columns
-  MDSX_L uint32_t* wrec = (MDSX_L uint32_t*)(wl + seg_rec_off(S, TR, nvar, a.seg_small));
-  MDSX_L uint32_t* wbad = wrec + 3 * kWinMax * ncols;
+  MDSX_L uint8_t* sbuf = (MDSX_L uint8_t*)(wl + run_wave_lds(S, TR, nvar));  // small columns
   const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(
       static_cast<uint32_t>(reinterpret_cast<uintptr_t>((const MDSX_L uint8_t*)wl)));
 
@@ -673,23 +505,8 @@ __global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) 
   const uint64_t small_mask = __ballot(small);
   const uint32_t hv = 4u * uint32_t(nvar);
 
-  // lane l: offsets[r0 + l + 1] (the end of sample l)
-  const uint32_t ob_next = uint32_t(__shfl_down(int(ob), 1));
   for (int j = 0; j < n;) {  // wave-uniform
     const uint32_t b = uint32_t(__builtin_amdgcn_readlane(int(ob), j));
-    // a window: the samples j .. j + m - 1 whose bytes fit the ring together (seg_win > 1)
-    int m = 1;
-    if (a.seg_win > 1) {
-      const bool fits = lane >= j && lane < min(n, j + int(a.seg_win)) && ob_next - b <= a.seg_lim;
-      m = __builtin_ctzll(~(__ballot(fits) >> j));
-    }
-    if (m > 1) {
-      seg_window<S, kNT>(a, cols, st, ring, ring_lds, ob, shard, sbase, j, m, TR, r, vi, rb, meta,
-                         small, small_mask, wide_mask, soff, cst, base, cur, carry, obuf, fbuf,
-                         sbuf, wrec, wbad, lane);
-      j += m;
-      continue;
-    }
     const uint32_t e = uint32_t(__builtin_amdgcn_readlane(int(ob), j + 1));
     const uint32_t size = e - b;
     const uint32_t sp = uint32_t(shard + b - sbase);  // stream position of the sample
@@ -779,10 +596,8 @@ int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
     return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode tiles hold at most 32 rows");
   if (a.seg_lim) {
     const int W = plan->seg_waves;
-    const size_t slds = seg_cols_lds(a.ncols) + size_t(W) * seg_wave_lds(a.run_slots, a.tile_rows,
-                                                                          a.nvar, a.ncols,
-                                                                          a.seg_small,
-                                                                          a.seg_win > 1);
+    const size_t slds = seg_cols_lds(a.ncols) +
+                        size_t(W) * seg_wave_lds(a.run_slots, a.tile_rows, a.nvar, a.seg_small);
     if (slds > 160 * 1024)
       return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode LDS exceeds 160 KiB");
     const unsigned sgrid = (a.ntiles + unsigned(W) - 1) / unsigned(W);

@@ -10,7 +10,10 @@
 // tile's ragged bytes (a sample failing a check counts zero, the decodes' rule) and writes each
 // tile's run record (stream range, offsets-table slice, whether every sample passes the file
 // checks and fits the lean path's ring); the tile bases then come from the scan kernels
-// (mdsx_kernels.hip) or, chained, from a look-back inside this pass.
+// (mdsx_kernels.hip). (A single-pass form -- the scan chained into this pass by a decoupled
+// look-back over workgroups in ticket order -- measured no faster on config C and 16 % slower on
+// short rows: with thousands of workgroups starting together the inclusive prefixes propagate
+// one block at a time.)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -22,94 +25,15 @@
 
 namespace mdsx_kernels {
 
-// Look-back status word of one (ragged column, block of tiles): flag in the top 2 bits (0 not yet
-// published, 1 the block's own aggregate, 2 its inclusive prefix), a byte count below.
-constexpr uint64_t kChainAgg = 1ull << 62, kChainIncl = 2ull << 62;
-constexpr uint64_t kChainValue = (1ull << 62) - 1;
-
-// One ragged column of a chained totals block: the block's tiles' exclusive prefixes (x: the
-// tile's total at its first thread, 0 elsewhere) from a block scan plus the block's base from the
-// look-back, written to tile_prefix; the last block also writes the column's total.
-__device__ __forceinline__ void chained_prefix(const DevArgs& a, int vi, uint32_t block,
-                                               uint32_t tile, int64_t x, bool head_thread,
-                                               int64_t* s_wsum, int64_t* s_base) {
-  typedef __attribute__((address_space(1))) uint64_t cu64;
-  int64_t agg;
-  const int64_t excl = block_exclusive_scan(x, s_wsum, &agg);
-  const int t = threadIdx.x, lane = t & 63;
-  const uint32_t nblocks = (a.ntiles + uint32_t(kBlock / a.tile_rows) - 1) /
-                           uint32_t(kBlock / a.tile_rows);
-  cu64* st = (cu64*)(a.chain + uint64_t(vi) * nblocks);
-  if (t < 64) {  // wave 0: publish, then look back over the earlier blocks
-    if (t == 0)
-      __hip_atomic_store(st + block, (block == 0 ? kChainIncl : kChainAgg) | uint64_t(agg),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint64_t base = 0;
-    int64_t j = int64_t(block) - 1;
-    bool done = block == 0;
-    uint32_t polls = 0;
-    while (!done) {  // wave-uniform
-      const int64_t k = j - lane;
-      const uint64_t w = k >= 0 ? __hip_atomic_load(st + k, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT)
-                                : kChainIncl;
-      const uint64_t incl = __ballot((w >> 62) == 2);
-      const uint64_t none = __ballot((w >> 62) == 0);
-      const uint64_t span = incl ? ((incl & (0 - incl)) << 1) - 1 : ~0ull;  // lanes <= first incl
-      // an earlier block is still scanning its rows (it holds an earlier ticket, so it runs);
-      // the bound only keeps a broken invariant from hanging the launch
-      if ((none & span) != 0 && ++polls < (1u << 22)) {
-        __builtin_amdgcn_s_sleep(1);
-        continue;
-      }
-      if ((none & span) != 0 && lane == 0) report_decode(a, MDSX_E_HIP, -1, -1, -1);
-      uint64_t v = ((span >> lane) & 1) ? (w & kChainValue) : 0;
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-      base += v;
-      if (incl) done = true;
-      else j -= 64;
-    }
-    if (t == 0) {
-      if (block != 0)
-        __hip_atomic_store(st + block, kChainIncl | (base + uint64_t(agg)), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      *s_base = int64_t(base);
-      if (block + 1 == nblocks) {  // the batch's last block: column totals
-        for (int c = 0; c < a.ncols; ++c)
-          if (a.cols[c].var_index == vi) a.cols[c].offsets[a.rows] = int64_t(base) + agg;
-        if (a.totals) a.totals[vi] = int64_t(base) + agg;
-      }
-    }
-  }
-  __syncthreads();
-  if (head_thread) a.tile_prefix[uint64_t(vi) * a.nscan + tile] = *s_base + excl;
-  __syncthreads();  // s_base is reused by the next column
-}
-
 // The totals pass: the ragged bytes of every tile (one thread per row; 256 / TR tiles
 // per workgroup), with the staged kernel's row rule: a row whose range, heads or columns do not
 // fit counts zero.
-//
-// kChained (tiles of <= 64 rows): the exclusive scan of the tile totals is done here too, in one
-// pass -- workgroups take their block of tiles in ticket order, block-scan their tiles' totals
-// and find the block's base by a decoupled look-back over the earlier blocks' status words (flag
-// and value in one 8-byte word, agent-scope atomics) -- so no scan kernels follow.
-template <bool kChained>
 __global__ __launch_bounds__(kBlock) void stage_totals_kernel(const DevArgs a) {
   __shared__ int64_t s_part[kBlock / 64][MDSX_MAX_COLUMNS];
   __shared__ uint32_t s_bad[kBlock / 64];
-  __shared__ int64_t s_wsum[kBlock / 64];
-  __shared__ int64_t s_base;
-  __shared__ uint32_t s_block;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int TR = a.tile_rows;
-  uint32_t block = blockIdx.x;
-  if constexpr (kChained) {
-    if (t == 0) s_block = atomicAdd(a.ticket, 1u);
-    __syncthreads();
-    block = s_block;
-  }
-  const uint32_t tile = block * uint32_t(kBlock / TR) + uint32_t(t / TR);
+  const uint32_t tile = blockIdx.x * uint32_t(kBlock / TR) + uint32_t(t / TR);
   const bool tile_ok = tile < a.ntiles;
   TileView v;
   if (tile_ok) v = tile_view(a, tile);
@@ -139,8 +63,6 @@ __global__ __launch_bounds__(kBlock) void stage_totals_kernel(const DevArgs a) {
     if (TR <= 64) {  // segments of TR lanes inside the wave
       for (int o = 1; o < TR; o <<= 1) x += __shfl_xor(x, o);
       if (tile_ok && t % TR == 0) a.tile_total[uint64_t(vi) * a.nscan + tile] = x;
-      if constexpr (kChained) chained_prefix(a, vi, block, tile, tile_ok && t % TR == 0 ? x : 0,
-                                             tile_ok && t % TR == 0, s_wsum, &s_base);
     } else {  // a tile spans TR / 64 waves
       for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
       if (lane == 0) s_part[wave][vi] = x;
@@ -255,12 +177,9 @@ __global__ __launch_bounds__(kBlock) void stage_huge_kernel(const DevArgs a) {
 
 }  // namespace
 
-int launch_stage_totals(const DevArgs& a, hipStream_t s, bool chained) {
+int launch_stage_totals(const DevArgs& a, hipStream_t s) {
   const unsigned grid = unsigned((uint64_t(a.ntiles) * a.tile_rows + kBlock - 1) / kBlock);
-  if (chained)
-    hipLaunchKernelGGL((stage_totals_kernel<true>), dim3(grid), dim3(kBlock), 0, s, a);
-  else
-    hipLaunchKernelGGL((stage_totals_kernel<false>), dim3(grid), dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL(stage_totals_kernel, dim3(grid), dim3(kBlock), 0, s, a);
   return hip_check(hipGetLastError(), "stage_totals_kernel launch");
 }
 

@@ -41,11 +41,8 @@ MODES = {
     'seg8': 'run=8,seg=1,rmin=0',
     'seg16': 'run=16,seg=1,rmin=0,rkb=1024',
     'seg8_nt': 'run=8,seg=1,rmin=0,rnt=1',
-    'seg8_1': 'run=8,seg=1,rmin=0,swin=1',  # one sample at a time (no windows of several)
-    'seg16_w4': 'run=16,seg=1,rmin=0,swin=4,rkb=64',
-    'seg8_chain': 'run=8,seg=1,rmin=0,chain=1',  # the totals scan chained into the totals pass
-    'seg8_wg1': 'run=8,seg=1,rmin=0,swg=1,chain=1',  # one wave (run) per workgroup
-    'run4_chain': 'run=4,rmin=0,rkb=4,chain=1',
+    'seg16_64k': 'run=16,seg=1,rmin=0,rkb=64',
+    'seg8_wg1': 'run=8,seg=1,rmin=0,swg=1',  # one wave (run) per workgroup
     'rows': 'rows=32,rmin=1000000000',  # the row-parallel decode (mdsx_rows.hip) for every size
     'rows_auto': 'rows=-1,rmin=1000000000',  # ... its tiles and stage sized per batch
     'rows_small': 'rows=2,rmin=1000000000',  # a 2 KiB stage: windows and HBM-direct samples

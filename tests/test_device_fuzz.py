@@ -26,8 +26,7 @@ MODES = {
     'run': 'run=4,rmin=0,rkb=8',  # the streaming decode whatever the sample size
     'seg': 'run=4,seg=1,rmin=0,rkb=8',  # ... its lean path where a sample fits the 4 KiB ring
     'seg16': 'run=16,seg=1,rmin=0,rkb=64',
-    'seg_1': 'run=8,seg=1,rmin=0,swin=1',
-    'seg_chain': 'run=8,seg=1,rmin=0,chain=1,swg=2',
+    'seg_wg2': 'run=8,seg=1,rmin=0,swg=2',
     'rows_small': 'rows=2,rmin=1000000000',  # row-parallel, 2 KiB stage (windows, huge rows)
     'register': 'run=0,rows=0',  # the register decode (+ gather / groups per column)
 }
