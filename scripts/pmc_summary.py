@@ -78,6 +78,29 @@ def main(out):
             'algorithmic_bytes_per_launch': cfg['roofline']['algorithmic_bytes_per_launch'],
             'kernel_stats': [r for r in stats if kernel in r['Name']],
         }
+        # the bench's timed launches: the kernel's last `steps` dispatches of this workload in
+        # the trace (warm-up and verification launches come before them), against the bench
+        # line's HIP-event timing of the same launches
+        durs = [int(r['End_Timestamp']) - int(r['Start_Timestamp'])
+                for r in sorted(rows(out, 'trace/**/*kernel_trace.csv'),
+                                key=lambda r: int(r['Start_Timestamp']))
+                if kernel in r['Kernel_Name'].replace('(anonymous namespace)::', '')]
+        steps = int(lines[0].get('steps', 20))
+        if len(durs) >= steps:
+            # the config's own launches: B's come first in the trace, C's after them
+            idx = configs(lines[0]).index(cfg)
+            same = [c for c in configs(lines[0]) if c['roofline']['kernel'] == kernel]
+            block = durs if len(same) == 1 else durs[idx * len(durs) // len(same):
+                                                      (idx + 1) * len(durs) // len(same)]
+            timed = block[-steps:]
+            avg = sum(timed) / len(timed)
+            algo = e['algorithmic_bytes_per_launch']
+            e['trace_timed'] = {
+                'launches': len(timed), 'avg_ns': avg,
+                'achieved_GBps': algo / avg, 'frac': algo / avg / 8000.0,
+                'bench_line_frac': cfg['roofline']['frac'],
+                'bench_line_kernel_ms': cfg['roofline']['kernel_ms'],
+            }
         # memory-side requests by size (TCC_EA0_*: the L2's requests to HBM / fabric), exact
         # bytes: a copy of N bytes counts N / 128 128-byte reads and N / 64 64-byte writes
         n32, n64, n128, nrd = (mean(out, 'read', f'TCC_EA0_RDREQ{s}_sum', kernel)

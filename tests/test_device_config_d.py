@@ -34,6 +34,9 @@ def test_config_d_rank0_share_bit_exact():
     assert sorted(g for r in range(WORLD_D) for g in owned_shards(SHARDS_D, r, WORLD_D)) == \
         list(range(SHARDS_D))
     dev = torch.device('cuda', 0)
+    torch.cuda.set_device(dev)
+    torch.zeros(1, device=dev)  # the context (the first GPU call of a fresh process)
+    torch.cuda.empty_cache()
     torch.cuda.reset_peak_memory_stats(dev)
     synth = fixed_b_batch_on_device(0, seed=SEED_B, shard_ids=mine, keep_sources=False)
     batch = synth.batch
