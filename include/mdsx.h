@@ -183,9 +183,11 @@ int mdsx_decode_shards(const mdsx_plan* plan, const mdsx_batch* batch,
                        void* stream);
 
 /* Single-pass decode: passes 1 and 2 in one launch sequence, with no host round trip for the
- * totals. Each tile of the decode kernel scans its own ragged lengths and finds its base by
- * decoupled look-back over the tiles before it (tiles are taken in dispatch order from a
- * ticket), so ragged outputs are sized BEFORE the totals are known: outs[c].capacity of a ragged
+ * totals. The register decode's tiles scan their own ragged lengths and find their bases by
+ * decoupled look-back over the tiles before them (tiles are taken in dispatch order from a
+ * ticket); streaming and row-parallel batches run their scan pass and decode back to back on the
+ * stream (a look-back across their ~1000 tiles in flight measured slower than the scan pass).
+ * Ragged outputs are sized BEFORE the totals are known: outs[c].capacity of a ragged
  * column is its allocation (an upper bound such as the batch's sample bytes); a column that
  * needs more reports MDSX_E_CAPACITY. offsets[rows] and d_totals (device int64[num_var], may be
  * NULL) receive the totals. Same outputs as mdsx_scan_shards + mdsx_decode_shards.

@@ -26,3 +26,9 @@ print('cpu', d['cpu_baseline'] and round(d['cpu_baseline']['value']))"
 TAG=$TAG/prof bash scripts/profile_bench.sh || exit 1
 TAG=$TAG/sq SET1=1 RUNS="${SQ_RUNS:-C:run=8,seg=1,rnt=1 C:run=4,seg=0,rnt=0}" bash scripts/gpu_sq.sh > "$OUT/sq.txt" 2>&1 || { tail -20 "$OUT/sq.txt"; exit 1; }
 cat "$OUT/sq.txt"
+# gpurun copies back at most 64 MiB: list the largest files, then drop the per-dispatch counter
+# dumps the summaries above were made from and compress the kernel traces
+du -ak "$OUT" | sort -n | tail -8
+find "$OUT" -name '*counter_collection.csv' -size +1M -delete
+find "$OUT" -name '*kernel_trace.csv' -size +1M -exec gzip -9 {} \;
+du -sk "$OUT"

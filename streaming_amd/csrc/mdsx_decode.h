@@ -163,6 +163,83 @@ __device__ __forceinline__ void report_decode(const DevArgs& a, int code, int sh
 
 constexpr uint64_t kStatusBlock = 256;
 
+// Single-pass decode (the register decode's kSingle form): tiles are
+// taken in dispatch order from a ticket counter, so every tile a workgroup waits on is held by a
+// workgroup that is already running. Each tile publishes its ragged bytes per ragged column and
+// finds its output base by a decoupled look-back over the earlier tiles' status words. Flag and
+// value share one 8-byte word written and read with agent-scope atomics, so no fence orders them.
+constexpr uint64_t kLbAggregate = 1ull << 62, kLbInclusive = 2ull << 62;
+constexpr uint64_t kLbValue = (1ull << 62) - 1;
+typedef __attribute__((address_space(1))) uint64_t gu64;
+
+// The look-back, run by one whole wave for every ragged column at once: agg[vi] is this tile's
+// ragged bytes of column vi, base[vi] receives the bytes of every earlier tile. The wave splits
+// into segments of W lanes, one per column (groups of 64 / W columns in turn); lane k of a
+// segment reads the status of tile j - k. A segment sums its window up to the nearest inclusive
+// prefix (tiles before 0 read as an inclusive zero), retrying while a tile inside that span has
+// not published yet, and steps back W tiles when the window holds no inclusive prefix. The
+// batch's last tile writes the column totals (offsets[rows], totals).
+__device__ __forceinline__ void lookback_bases(const DevArgs& a, uint32_t tile, const int64_t* agg,
+                                               int64_t* base_out, uint32_t shard, int lane) {
+  const int nv = a.nvar;
+  const int W = nv <= 1 ? 64 : nv <= 2 ? 32 : nv <= 4 ? 16 : 8;
+  const int kk = lane & (W - 1);
+  const int seg0 = lane & ~(W - 1);
+  const uint64_t wmask = W == 64 ? ~0ull : (1ull << W) - 1;
+  for (int g0 = 0; g0 < nv; g0 += 64 / W) {
+    const int vi = g0 + lane / W;
+    const bool mine = vi < nv;
+    gu64* st = (gu64*)(a.lookback + uint64_t(mine ? vi : 0) * a.ntiles);
+    const uint64_t ag = mine ? uint64_t(agg[vi]) : 0;
+    if (mine && kk == 0)
+      __hip_atomic_store(st + tile, (tile == 0 ? kLbInclusive : kLbAggregate) | ag,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t base = 0;
+    int64_t j = int64_t(tile) - 1;
+    bool done = !mine || tile == 0;
+    uint32_t polls = 0;
+    while (__ballot(!done) != 0) {
+      const int64_t k = j - kk;
+      const uint64_t w = (!done && k >= 0) ? __hip_atomic_load(st + k, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT)
+                                           : kLbInclusive;
+      const uint64_t incl = (__ballot((w >> 62) == 2) >> seg0) & wmask;
+      const uint64_t none = (__ballot((w >> 62) == 0) >> seg0) & wmask;
+      const uint64_t span = incl ? ((incl & (0 - incl)) << 1) - 1 : wmask;  // lanes <= first
+      // an earlier tile's workgroup is still scanning its rows (it is running: it holds a
+      // ticket); the bound only keeps a broken invariant from hanging the launch
+      const bool wait = !done && (none & span) != 0 && ++polls < (1u << 22);
+      uint64_t x = (!done && !wait && ((span >> kk) & 1)) ? (w & kLbValue) : 0;
+      for (int o = W >> 1; o > 0; o >>= 1) x += __shfl_xor(x, o);
+      if (!done && !wait) {
+        if ((none & span) != 0 && kk == 0) report_decode(a, MDSX_E_HIP, int(shard), -1, -1);
+        base += x;
+        if (incl) done = true;
+        else j -= W;
+      }
+      if (__ballot(wait) != 0) __builtin_amdgcn_s_sleep(1);
+    }
+    if (mine && kk == 0) {
+      if (tile != 0)
+        __hip_atomic_store(st + tile, kLbInclusive | (base + ag), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      base_out[vi] = int64_t(base);
+      if (tile + 1 == a.ntiles) {  // the batch's last tile: column totals
+        for (int c = 0; c < a.ncols; ++c)
+          if (a.cols[c].var_index == vi) a.cols[c].offsets[a.rows] = int64_t(base + ag);
+        if (a.totals) a.totals[vi] = int64_t(base + ag);
+      }
+    }
+  }
+}
+
+// The tile number of a single-pass workgroup (thread 0 draws the ticket; block-uniform).
+__device__ __forceinline__ uint32_t draw_ticket(const DevArgs& a, uint32_t* s_tile) {
+  if (threadIdx.x == 0) *s_tile = atomicAdd(a.ticket, 1u);
+  __syncthreads();
+  return __builtin_amdgcn_readfirstlane(*s_tile);
+}
+
 // The LDS-staged decode of ragged plans (mdsx_stage.hip). Pass 1: the ragged bytes of every tile
 // (then scan_totals_kernel, one entry per tile: a.scan_per == 1). Pass 2: every column of every
 // row from each tile's shard bytes staged once in LDS. Return MDSX_OK or a launch error.

@@ -291,20 +291,12 @@ __device__ __forceinline__ void ring_copy(const DevArgs& a, const DevCol* cols, 
 }
 
 
-// Look-back status word of one (ragged column, tile): flag in the top 2 bits (0 not yet
-// published, 1 the tile's own aggregate, 2 the inclusive prefix), a byte count below.
-constexpr uint64_t kLbAggregate = 1ull << 62, kLbInclusive = 2ull << 62;
-constexpr uint64_t kLbValue = (1ull << 62) - 1;
-typedef __attribute__((address_space(1))) uint64_t gu64;
-
 // Pass 2: per-row column boundaries; fixed columns decoded; ragged columns prepared for the
 // destination-major gather (final offsets, per-row source addresses, gather-tile row map).
-// kSingle: one pass, no scan kernels before it (mdsx_decode_shards_single). Tiles are taken in
-// dispatch order from a ticket counter, so every tile a workgroup waits on is held by a
-// workgroup that is already running; each tile block-scans its ragged lengths, publishes its
-// aggregate per ragged column and finds its base by decoupled look-back over the earlier tiles'
-// status words. Flag and value share one 8-byte word written and read with agent-scope atomics,
-// so no fence orders them.
+// kSingle: one pass, no scan kernels before it (mdsx_decode_shards_single): each tile
+// block-scans its ragged lengths and finds its base by the look-back (lookback_bases,
+// mdsx_decode.h; status word of one (ragged column, tile): flag in the top 2 bits -- 0 not yet
+// published, 1 the tile's own aggregate, 2 the inclusive prefix -- and a byte count below).
 // kSlots > 0: long ragged rows copied through the LDS-DMA ring (ring_copy) instead of wave_copy.
 template <int kUnroll, bool kNT, bool kRagged, bool kEdges, bool kSingle, int kSlots = 0>
 __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
@@ -398,63 +390,7 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
       if (t == 0) s_agg[vi] = tot;
     }
     __syncthreads();
-    if (wave == 0) {
-      // Wave-parallel look-back, every ragged column at once: the wave splits into segments of W
-      // lanes, one per column (groups of 64 / W columns in turn); lane k of a segment reads the
-      // status of tile j - k. A segment sums its window up to the nearest inclusive prefix (tiles
-      // before 0 read as an inclusive zero), retrying while a tile inside that span has not
-      // published yet, and steps back W tiles when the window holds no inclusive prefix.
-      const int nv = a.nvar;
-      const int W = nv <= 1 ? 64 : nv <= 2 ? 32 : nv <= 4 ? 16 : 8;
-      const int kk = lane & (W - 1);
-      const int seg0 = lane & ~(W - 1);
-      const uint64_t wmask = W == 64 ? ~0ull : (1ull << W) - 1;
-      for (int g0 = 0; g0 < nv; g0 += 64 / W) {
-        const int vi = g0 + lane / W;
-        const bool mine = vi < nv;
-        gu64* st = (gu64*)(a.lookback + uint64_t(mine ? vi : 0) * a.ntiles);
-        const uint64_t agg = mine ? uint64_t(s_agg[vi]) : 0;
-        if (mine && kk == 0)
-          __hip_atomic_store(st + tile, (tile == 0 ? kLbInclusive : kLbAggregate) | agg,
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        uint64_t base = 0;
-        int64_t j = int64_t(tile) - 1;
-        bool done = !mine || tile == 0;
-        uint32_t polls = 0;
-        while (__ballot(!done) != 0) {
-          const int64_t k = j - kk;
-          const uint64_t w = (!done && k >= 0) ? __hip_atomic_load(st + k, __ATOMIC_RELAXED,
-                                                                   __HIP_MEMORY_SCOPE_AGENT)
-                                               : kLbInclusive;
-          const uint64_t incl = (__ballot((w >> 62) == 2) >> seg0) & wmask;
-          const uint64_t none = (__ballot((w >> 62) == 0) >> seg0) & wmask;
-          const uint64_t span = incl ? ((incl & (0 - incl)) << 1) - 1 : wmask;  // lanes <= first
-          // an earlier tile's workgroup is still scanning its rows (it is running: it holds a
-          // ticket); the bound only keeps a broken invariant from hanging the launch
-          const bool wait = !done && (none & span) != 0 && ++polls < (1u << 22);
-          uint64_t x = (!done && !wait && ((span >> kk) & 1)) ? (w & kLbValue) : 0;
-          for (int o = W >> 1; o > 0; o >>= 1) x += __shfl_xor(x, o);
-          if (!done && !wait) {
-            if ((none & span) != 0 && kk == 0) report_decode(a, MDSX_E_HIP, v.shard_idx, -1, -1);
-            base += x;
-            if (incl) done = true;
-            else j -= W;
-          }
-          if (__ballot(wait) != 0) __builtin_amdgcn_s_sleep(1);
-        }
-        if (mine && kk == 0) {
-          if (tile != 0)
-            __hip_atomic_store(st + tile, kLbInclusive | (base + agg), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-          s_base[vi] = int64_t(base);
-          if (tile + 1 == a.ntiles) {  // the batch's last tile: column totals
-            for (int c = 0; c < a.ncols; ++c)
-              if (cols[c].var_index == vi) cols[c].offsets[a.rows] = int64_t(base + agg);
-            if (a.totals) a.totals[vi] = int64_t(base + agg);
-          }
-        }
-      }
-    }
+    if (wave == 0) lookback_bases(a, tile, s_agg, s_base, v.shard_idx, lane);
     __syncthreads();
     if (!v.table_ok) return;  // block-uniform; published its zero aggregates above
   }
@@ -1268,15 +1204,11 @@ uint64_t mdsx_workspace_bytes(const mdsx_plan* plan, const mdsx_batch* batch) {
   return workspace_layout(plan, batch).total;
 }
 
-int mdsx_scan_shards(const mdsx_plan* plan, const mdsx_batch* batch, const mdsx_column_out* outs,
-                     void* d_workspace, uint64_t workspace_bytes, int64_t* d_totals,
-                     void* stream) {
-  DevArgs a;
-  int rc = build_args(plan, batch, outs, d_workspace, workspace_bytes, d_totals, &a);
-  if (rc != MDSX_OK) return rc;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  rc = hip_check(hipMemsetAsync(d_workspace, 0, kStatusBlock, s), "hipMemsetAsync");
-  if (rc != MDSX_OK || plan->nvar == 0) return rc;
+}  // extern "C"
+
+// Pass 1 of a ragged plan: tile totals, their scan, offsets and column totals.
+static int scan_pass(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
+  int rc = MDSX_OK;
   if (a.ntiles > 0 && (a.run_slots || a.rows_bytes)) {
     rc = launch_stage_totals(a, s);
     if (rc != MDSX_OK) return rc;
@@ -1297,6 +1229,20 @@ int mdsx_scan_shards(const mdsx_plan* plan, const mdsx_batch* batch, const mdsx_
   return hip_check(hipGetLastError(), "scan_apply_kernel launch");
 }
 
+extern "C" {
+
+int mdsx_scan_shards(const mdsx_plan* plan, const mdsx_batch* batch, const mdsx_column_out* outs,
+                     void* d_workspace, uint64_t workspace_bytes, int64_t* d_totals,
+                     void* stream) {
+  DevArgs a;
+  int rc = build_args(plan, batch, outs, d_workspace, workspace_bytes, d_totals, &a);
+  if (rc != MDSX_OK) return rc;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  rc = hip_check(hipMemsetAsync(d_workspace, 0, kStatusBlock, s), "hipMemsetAsync");
+  if (rc != MDSX_OK || plan->nvar == 0) return rc;
+  return scan_pass(plan, a, s);
+}
+
 }  // extern "C"
 
 // The decode kernel (single: with its own look-back scan) and, for gather columns, the
@@ -1304,8 +1250,13 @@ int mdsx_scan_shards(const mdsx_plan* plan, const mdsx_batch* batch, const mdsx_
 static int launch_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s, bool single,
                          const uint64_t* mode_bytes) {
   int rc = MDSX_OK;
-  if (plan->nvar > 0 && !single && a.run_slots > 0) return launch_run_decode(plan, a, s);
-  if (plan->nvar > 0 && !single && a.rows_bytes > 0) return launch_rows_decode(plan, a, s);
+  if (plan->nvar > 0 && (a.run_slots > 0 || a.rows_bytes > 0)) {
+    // the streaming and row-parallel decodes have no single-pass form: their scan pass, then
+    // the decode (a look-back across the ~1000 tiles in flight measured slower than the pass:
+    // profiles/r03/negative/rows_single_pass)
+    if (single && (rc = scan_pass(plan, a, s)) != MDSX_OK) return rc;
+    return a.run_slots > 0 ? launch_run_decode(plan, a, s) : launch_rows_decode(plan, a, s);
+  }
   const size_t lds =
       size_t(a.tile_rows) * (12 * size_t(plan->nvar) + 4 * size_t(plan->ncols) + 1) + 16;
   const bool nt = plan->nontemporal != 0, ragged = plan->nvar > 0;

@@ -14,7 +14,8 @@ import pytest
 import torch
 
 from oracle import mds_oracle
-from streaming_amd.decoder import Plan, RaggedColumn, decode_batch, gather_sources, stage_shards
+from streaming_amd.decoder import (BatchDecoder, Plan, RaggedColumn, decode_batch, gather_sources,
+                                   stage_shards)
 from tests.test_device_decode import _random_dataset
 
 pytestmark = pytest.mark.gpu
@@ -29,6 +30,12 @@ MODES = {
     'seg_wg2': 'run=8,seg=1,rmin=0,swg=2',
     'rows_small': 'rows=2,rmin=1000000000',  # row-parallel, 2 KiB stage (windows, huge rows)
     'register': 'run=0,rows=0',  # the register decode (+ gather / groups per column)
+}
+# the single pass (mdsx_decode_shards_single), fresh and re-run with known totals
+SINGLE_MODES = {
+    'single': '',  # streaming / row-parallel batches: scan pass + decode, no host round trip
+    'single_rows_small': 'rows=2,rmin=1000000000',  # ... row-parallel in windows, huge rows
+    'single_register': 'run=0,rows=0',  # the register decode's single-pass form (look-back)
 }
 
 
@@ -70,6 +77,21 @@ def test_fuzz_decode_and_gather(tmp_path, monkeypatch, seed):
         assert dec.rows == sum(counts)
         for c, parts in want.items():
             _check(dec[c], parts, (seed, mode, c))
+    for mode, tune in SINGLE_MODES.items():
+        monkeypatch.setenv('MDSX_TUNE', tune)
+        plan = Plan(info['column_names'], info['column_encodings'], info['column_sizes'])
+        batch = stage_shards(data, counts, plan)
+        dec = decode_batch(plan, batch, single=True)
+        for c, parts in want.items():
+            _check(dec[c], parts, (seed, mode, c))
+        # a two-pass decoder re-running with its totals known
+        bd = BatchDecoder(plan, batch)
+        bd.run()
+        bd.check()
+        again = bd.run()
+        bd.check()
+        for c, parts in want.items():
+            _check(again[c], parts, (seed, mode, 'rerun', c))
     # multi-source gather: one source per shard, random ids (repeats, every shard)
     monkeypatch.setenv('MDSX_TUNE', '')
     plan = Plan(info['column_names'], info['column_encodings'], info['column_sizes'])

@@ -1,5 +1,7 @@
-"""GPU parity of the single-pass decode (``mdsx_decode_shards_single``: the decode kernel scans
-its own ragged lengths by decoupled look-back, outputs sized at the payload bound).
+"""GPU parity of the single-pass decode (``mdsx_decode_shards_single``: one launch sequence with
+no host round trip, outputs sized at the payload bound; the register decode scans its own ragged
+lengths by decoupled look-back, streaming and row-parallel batches run their scan pass and decode
+back to back).
 
 The decode tests of ``test_device_decode`` / ``test_device_copy_modes`` are collected here a
 second time with ``decode_batch`` switched to the single pass (every module that calls it), so
@@ -67,8 +69,11 @@ def _columns_equal(a, b):
 C_PLAN = (['b', 'n', 's'], ['bytes', 'int', 'str'], [None, 8, None])
 
 
-def test_single_equals_two_pass_on_many_tiles():
-    """160k rows of config C: 5000 tiles of look-back per column, both passes bit-identical."""
+@pytest.mark.parametrize('tune', ['', 'run=0,rows=0'])
+def test_single_equals_two_pass_on_many_tiles(monkeypatch, tune):
+    """160k rows of config C, both passes bit-identical: the default decodes, and the register
+    decode's look-back over 5000 tiles per column."""
+    monkeypatch.setenv('MDSX_TUNE', tune)
     shards, counts, src = var_c_shards(160_000, seed=41, blob_bytes=(0, 600))
     plan = Plan(*C_PLAN)
     batch = stage_shards(shards, counts, plan)
