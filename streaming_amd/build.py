@@ -15,11 +15,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SOURCES = [
     os.path.join(HERE, 'csrc', name)
-    for name in ('mdsx_kernels.hip', 'mdsx_stage.hip', 'mdsx_run.hip', 'mdsx_rows.hip', 'mdsx_encode.hip', 'mdsx_hash.hip',
-                 'mdsx_plan.cpp')
+    for name in ('mdsx_kernels.hip', 'mdsx_stage.hip', 'mdsx_run.hip', 'mdsx_rows.hip',
+                 'mdsx_encode.hip', 'mdsx_hash.hip', 'mdsx_plan.cpp')
 ]
 HEADERS = [os.path.join(HERE, 'csrc', name)
-           for name in ('mdsx_internal.h', 'mdsx_device.h', 'mdsx_decode.h', 'mdsx_ring.h')]
+           for name in ('mdsx_internal.h', 'mdsx_device.h', 'mdsx_decode.h', 'mdsx_ring.h',
+                        'mdsx_run_body.h')]
 OUTPUT = os.path.join(HERE, 'lib', 'libmdsx.so')
 ARCH = os.environ.get('MDSX_OFFLOAD_ARCH', 'gfx950')
 
