@@ -206,10 +206,23 @@ __device__ __forceinline__ uint32_t byte_of(const uint4& v, int j) {
   return (w >> (8 * (j & 3))) & 0xffu;
 }
 
-__device__ __forceinline__ uint4 shfl_down1(const uint4 v) {
-  return make_uint4(__shfl_down(v.x, 1), __shfl_down(v.y, 1), __shfl_down(v.z, 1),
-                    __shfl_down(v.w, 1));
+// Cross-lane moves by DPP (a VALU modifier: no LDS round trip, unlike ds_bpermute). Lanes with
+// no source read 0.
+template <int kCtrl>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
+  return uint32_t(__builtin_amdgcn_update_dpp(0, int(v), kCtrl, 0xF, 0xF, true));
 }
+template <int kCtrl>
+__device__ __forceinline__ uint4 dpp_mov4(const uint4 v) {
+  return make_uint4(dpp_mov<kCtrl>(v.x), dpp_mov<kCtrl>(v.y), dpp_mov<kCtrl>(v.z),
+                    dpp_mov<kCtrl>(v.w));
+}
+constexpr int kDppWaveShl1 = 0x130;  // lane i <- lane i + 1 across the wave (lane 63: 0)
+constexpr int kDppRowShl1 = 0x101;   // lane i <- lane i + 1 inside its row of 16 (lane 15: 0)
+constexpr int kDppRowRor15 = 0x12F;  // lane i <- lane (i + 1) mod 16 of its row
+
+// Lane i gets lane i + 1's chunk (lane 63: zeros; every caller replaces it).
+__device__ __forceinline__ uint4 shfl_down1(const uint4 v) { return dpp_mov4<kDppWaveShl1>(v); }
 
 __device__ __forceinline__ uint4 readlane0(const uint4 v) {
   return make_uint4(__builtin_amdgcn_readlane(v.x, 0), __builtin_amdgcn_readlane(v.y, 0),
@@ -500,13 +513,10 @@ __device__ __forceinline__ void group_copy(const uint8_t* src, uint8_t* dst, uin
       const uint64_t k0 = base + uint64_t(u) * 16;
       if (k0 >= maxc) break;  // wave-uniform
       const uint64_t k = k0 + gl;
-      uint4 hi = make_uint4(__shfl_down(lo[u].x, 1, 16), __shfl_down(lo[u].y, 1, 16),
-                            __shfl_down(lo[u].z, 1, 16), __shfl_down(lo[u].w, 1, 16));
-      const uint4 nx = u + 1 < kUnroll ? lo[u + 1 < kUnroll ? u + 1 : u] : tail;
-      const uint4 nxt = u + 1 < kUnroll
-                            ? make_uint4(__shfl(nx.x, 0, 16), __shfl(nx.y, 0, 16),
-                                         __shfl(nx.z, 0, 16), __shfl(nx.w, 0, 16))
-                            : tail;
+      // the group neighbour's chunk (gl 15: the group's next step's gl 0, or the extra load)
+      uint4 hi = dpp_mov4<kDppRowShl1>(lo[u]);
+      const uint4 nxt = u + 1 < kUnroll ? dpp_mov4<kDppRowRor15>(lo[u + 1 < kUnroll ? u + 1 : u])
+                                        : tail;
       if (gl == 15) hi = nxt;
       const uint4 out = sh ? funnel16_lane(lo[u], hi, sh) : lo[u];
       const uint64_t D = dbeg + 16 * k;
