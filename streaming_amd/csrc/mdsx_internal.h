@@ -46,7 +46,8 @@ struct mdsx_plan {
   int ring_slots = 0;   // long ragged rows through a per-wave LDS-DMA ring of this many KiB (0: off)
   int stage_debug = 0;  // measurement only: parts of the row-parallel decode skipped (bits)
   int run_slots = 0;    // ragged plans: KiB of the streaming decode's per-wave LDS ring (0: off)
-  int run_kb = 32;      // streaming decode: about this many KiB of samples per tile (tile sizing)
+  int run_kb = 16;      // streaming decode: about this many KiB of samples per tile (tile sizing:
+                        // runs of at most ~8 KiB; measured DESIGN.md §5, profiles/r03/run_size/)
   int64_t run_min = 3072;  // streaming decode for batches whose samples average >= this many bytes
   int run_nt = 0;          // streaming decode: non-temporal ring loads and stores (the lean path
                            // is faster with them; the general one alone was slower)

@@ -134,7 +134,7 @@ def test_tile_rows_for_sizes_ragged_tiles_to_the_decode(monkeypatch):
     assert c.tile_rows_for(1 << 26, (1 << 26) // 250) == 64
     assert c.tile_rows_for(1 << 26, (1 << 26) // 1000) == 32
     assert c.tile_rows_for(1 << 26, (1 << 26) // 2000) == 16
-    assert c.tile_rows_for(1 << 26, 15_700) == 4  # ~4.3 KB samples: streaming, 4-row tiles
+    assert c.tile_rows_for(1 << 26, 15_700) == 2  # ~4.3 KB samples: streaming, 2-row runs
     assert c.tile_rows_for(1 << 26, (1 << 26) // 2048) == 16
     assert c.tile_rows_for(1 << 26, 10) == 1  # 6.7 MB samples: one per tile
     wide = Plan([f'c{i:02d}' for i in range(64)], ['str'] * 64, [None] * 64)
