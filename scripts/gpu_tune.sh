@@ -11,7 +11,7 @@ if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 600 python3 -u -m pytest ${TESTS:-tests/test_device_copy_modes.py} -m gpu -x -q --timeout 120 --timeout-method thread -k "${KSEL:-default}" > "$OUT/pytest.log" 2>&1 || { tail -40 "$OUT/pytest.log"; exit 1; }
   tail -2 "$OUT/pytest.log"
 fi
-for i in 1 2; do
+for i in $(seq 1 ${REPS:-2}); do
   timeout -k 10 300 python3 -u scripts/tune_decode.py ${CARGS:---config C --shards 64} --rounds ${ROUNDS:-4} --variants $VARIANTS > "$OUT/r$i.json" 2> "$OUT/r$i.err" || { tail -20 "$OUT/r$i.err"; exit 1; }
   python3 -c "
 import json; d = json.load(open('$OUT/r$i.json'))
