@@ -12,7 +12,7 @@ if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 600 python3 -u -m pytest ${TESTS:-tests/test_device_copy_modes.py tests/test_device_fuzz.py tests/test_device_decode.py} -m gpu -x -q --timeout 120 --timeout-method thread -k "${KSEL:-rows or default or fuzz or decode}" > "$OUT/pytest.log" 2>&1 || { tail -40 "$OUT/pytest.log"; exit 1; }
   tail -2 "$OUT/pytest.log"
 fi
-V=${VARIANTS:-"rows=-1 rows=-1,sdbg=32 rows=-1,sdbg=1"}
+V=${VARIANTS:-"rows=-1 rows=-1#b rows=-1,sdbg=1,nocheck"}
 for shape in "short 32,256 8,64" "medium 256,1024 64,256"; do
   set -- $shape
   timeout -k 10 300 python3 -u scripts/tune_decode.py --config C --shards 16 --blob $2 --chars $3 --rounds ${ROUNDS:-4} --variants $V > "$OUT/$1.json" 2> "$OUT/$1.err" || { tail -20 "$OUT/$1.err"; exit 1; }
