@@ -42,6 +42,8 @@ def main():
     ap.add_argument('--variants', nargs='+', default=['tile=256'])
     ap.add_argument('--blob', default='3072,5120', help="config C 'b' byte-length range")
     ap.add_argument('--chars', default='16,256', help="config C 's' code-point range")
+    ap.add_argument('--str-widths', type=int, default=4,
+                    help="config C 's': code points of 1..N UTF-8 bytes (1: ASCII text)")
     ap.add_argument('--own-outputs', action='store_true',
                     help='each variant allocates its own outputs (the round-2 harness)')
     args = ap.parse_args()
@@ -55,7 +57,7 @@ def main():
         blob = tuple(int(x) for x in args.blob.split(','))
         chars = tuple(int(x) for x in args.chars.split(','))
         synth = var_c_batch_on_device(list(range(args.shards)), seed=4, str_chars=chars,
-                                      blob_bytes=blob)
+                                      blob_bytes=blob, str_widths=args.str_widths)
         names = (['b', 'n', 's'], ['bytes', 'int', 'str'], [None, 8, None])
         base_batch, src = synth.batch, synth.sources
     decs = {}

@@ -353,14 +353,20 @@ __global__ __launch_bounds__(kRowsBlock, 4) void rows_decode_kernel(const DevArg
                 const int32_t nv = pos - dsA;  // A's bytes before the chunk
                 if (nv < 4) pw &= ~((1u << (8 * (4 - nv))) - 1u);
               }
-              uint32_t e = utf8_chunk_err2(X, pw, sB);
-              if (sB < 16 && utf8_open_at(X, pw, sB)) e |= 1u;
-              if (end == P0 + 16 && end == deL) {
-                if (sB < 16) e |= utf8_open_at(keep_bytes(X, sB, 16), 0, 16) ? 2u : 0u;
-                else e |= utf8_open_at(X, pw, 16) ? 1u : 0u;
+              // a chunk of ASCII with no lead byte before it cannot err, and no sequence is open
+              // at its values' ends: the check is skipped when that holds for the whole wave
+              // (measurement knob sdbg 32: always check)
+              const bool plain = (((X.x | X.y | X.z | X.w) & 0x80808080u) | hi_c0(pw)) == 0;
+              if (!__all(plain) || (a.stage_debug & 32)) {
+                uint32_t e = utf8_chunk_err2(X, pw, sB);
+                if (sB < 16 && utf8_open_at(X, pw, sB)) e |= 1u;
+                if (end == P0 + 16 && end == deL) {
+                  if (sB < 16) e |= utf8_open_at(keep_bytes(X, sB, 16), 0, 16) ? 2u : 0u;
+                  else e |= utf8_open_at(X, pw, 16) ? 1u : 0u;
+                }
+                if (e & 1u) atomicOr(&bad[r >> 5], 1u << (r & 31));
+                if (e & 2u) atomicOr(&bad[(r + 1) >> 5], 1u << ((r + 1) & 31));
               }
-              if (e & 1u) atomicOr(&bad[r >> 5], 1u << (r & 31));
-              if (e & 2u) atomicOr(&bad[(r + 1) >> 5], 1u << ((r + 1) & 31));
             }
           } else {
             // three or more values, an empty value, or a gap (a fixed column's failed sample

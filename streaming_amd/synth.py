@@ -163,7 +163,8 @@ def var_c_columns_on_device(shard_ids: list[int],
                             size_limit: int = 1 << 26,
                             device: Union[str, torch.device, None] = None,
                             str_chars: tuple[int, int] = (16, 256),
-                            blob_bytes: tuple[int, int] = (3072, 5120)):
+                            blob_bytes: tuple[int, int] = (3072, 5120),
+                            str_widths: int = 4):
     """Config C columns (``n: int``, ``b: bytes U[3072,5120]``, ``s: str`` of U[16,256] code
     points, 25 % each of 1/2/3/4-byte UTF-8) for full 64 MiB shards of a larger dataset, built
     on the device: global shard ``g`` draws from a generator seeded ``seed + g`` and holds
@@ -171,7 +172,8 @@ def var_c_columns_on_device(shard_ids: list[int],
     (per-shard columns in decoder layout, rows per shard).
 
     Shards are separate writer runs (each starts a fresh shard), so the rows of shard ``g + 1``
-    never move into shard ``g`` as one writer's greedy split of the concatenation could."""
+    never move into shard ``g`` as one writer's greedy split of the concatenation could.
+    ``str_widths`` < 4 draws code points of 1..str_widths UTF-8 bytes only (1: ASCII text)."""
     dev = torch.device(device or 'cuda')
     if dev.index is None:
         dev = torch.device('cuda', torch.cuda.current_device())
@@ -186,7 +188,7 @@ def var_c_columns_on_device(shard_ids: list[int],
         kw = dict(device=dev, generator=gen)
         b_len = torch.randint(blob_bytes[0], blob_bytes[1] + 1, (rows_try, ), **kw)
         chars = torch.randint(str_chars[0], str_chars[1] + 1, (rows_try, ), **kw)
-        width = torch.randint(0, 4, (int(chars.sum()), ), **kw)
+        width = torch.randint(0, str_widths, (int(chars.sum()), ), **kw)
         lo = torch.tensor([0x20, 0x80, 0x800, 0x10000], device=dev)[width]
         hi = torch.tensor([0x7F, 0x800, 0x10000 - 0x800, 0x110000], device=dev)[width]
         cp = lo + (torch.rand(width.shape, dtype=torch.float64, **kw) * (hi - lo)).long()
@@ -213,7 +215,8 @@ def var_c_batch_on_device(shard_ids: list[int],
                           size_limit: int = 1 << 26,
                           device: Union[str, torch.device, None] = None,
                           str_chars: tuple[int, int] = (16, 256),
-                          blob_bytes: tuple[int, int] = (3072, 5120)) -> SynthShards:
+                          blob_bytes: tuple[int, int] = (3072, 5120),
+                          str_widths: int = 4) -> SynthShards:
     """Config C shards (``shard_ids`` of a dataset of full shards, see
     :func:`var_c_columns_on_device`) written by the device MDS encoder into one decode batch."""
     from streaming_amd.decoder import stage_shards
@@ -222,7 +225,7 @@ def var_c_batch_on_device(shard_ids: list[int],
     plan = Plan(names, encs, sizes)
     config = shard_config_bytes(names, encs, sizes, None, [], size_limit)
     parts, counts = var_c_columns_on_device(shard_ids, seed, size_limit, device, str_chars,
-                                            blob_bytes)
+                                            blob_bytes, str_widths)
     files = []
     for cols, n in zip(parts, counts):
         enc, consumed = encode_batch(plan, cols, config, size_limit)
