@@ -43,6 +43,7 @@ MODES = {
     'seg8_nt': 'run=8,seg=1,rmin=0,rnt=1',
     'seg16_64k': 'run=16,seg=1,rmin=0,rkb=64',
     'seg8_wg1': 'run=8,seg=1,rmin=0,swg=1',  # one wave (run) per workgroup
+    'seg8_wg4': 'run=8,seg=1,rmin=0,swg=4',  # four (the default is two)
     'rows': 'rows=32,rmin=1000000000',  # the row-parallel decode (mdsx_rows.hip) for every size
     'rows_auto': 'rows=-1,rmin=1000000000',  # ... its tiles and stage sized per batch
     'rows_small': 'rows=2,rmin=1000000000',  # a 2 KiB stage: windows and HBM-direct samples
