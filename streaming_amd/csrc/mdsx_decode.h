@@ -79,6 +79,7 @@ struct DevArgs {
   uint32_t rows_bytes;   // LDS stage of the row-parallel decode (0: not the row-parallel decode)
   uint32_t seg_lim;      // streaming decode, lean path: largest sample it takes (0: lean path off)
   uint32_t seg_small;    // lean path: bytes per row of the fixed columns of <= 16 bytes
+  uint32_t xcd_order;    // lean path: workgroups remapped to XCD-contiguous ranges of runs
   uint32_t gather_block0[MDSX_MAX_COLUMNS + 1];  // first gather workgroup of each ragged column
   DevCol cols[MDSX_MAX_COLUMNS];
 };

@@ -809,6 +809,7 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   if (a->run_slots && plan->seg) {
     // lean path: a sample must fit the ring with a slot to spare (seg_decode_kernel)
     a->seg_lim = a->run_slots * 1024u - 1024u - 32u;
+    a->xcd_order = uint32_t(plan->xcd_order);
     for (int c = 0; c < plan->ncols; ++c)
       if (plan->cols[c].kind == MDSX_KIND_FIXED && plan->cols[c].row_bytes <= kSmallMax)
         a->seg_small += uint32_t(plan->cols[c].row_bytes);

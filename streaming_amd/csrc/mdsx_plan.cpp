@@ -217,6 +217,8 @@ void apply_tuning(mdsx_plan* p) {
       p->seg_waves = int(v);
     } else if (key == "seg") {
       p->seg = v ? 1 : 0;
+    } else if (key == "xcd") {
+      p->xcd_order = v ? 1 : 0;
     } else if (key == "rkb" && v >= 1 && v <= 4096) {
       p->run_kb = int(v);
     }

@@ -44,6 +44,7 @@ MODES = {
     'seg16_64k': 'run=16,seg=1,rmin=0,rkb=64',
     'seg8_wg1': 'run=8,seg=1,rmin=0,swg=1',  # one wave (run) per workgroup
     'seg8_wg4': 'run=8,seg=1,rmin=0,swg=4',  # four (the default is two)
+    'seg8_xcd0': 'run=8,seg=1,rmin=0,xcd=0',  # runs in launch order (default: XCD-contiguous ranges)
     'rows': 'rows=32,rmin=1000000000',  # the row-parallel decode (mdsx_rows.hip) for every size
     'rows_auto': 'rows=-1,rmin=1000000000',  # ... its tiles and stage sized per batch
     'rows_small': 'rows=2,rmin=1000000000',  # a 2 KiB stage: windows and HBM-direct samples
