@@ -46,6 +46,8 @@ struct TileRun {
 };
 static_assert(sizeof(TileRun) == 48, "TileRun layout");
 
+constexpr uint32_t kXcdSeg = 1, kXcdRegister = 2, kXcdRows = 4;  // DevArgs::xcd_order bits
+
 struct DevArgs {
   const uint8_t* batch;
   const mdsx_shard_desc* shards;
@@ -79,7 +81,7 @@ struct DevArgs {
   uint32_t rows_bytes;   // LDS stage of the row-parallel decode (0: not the row-parallel decode)
   uint32_t seg_lim;      // streaming decode, lean path: largest sample it takes (0: lean path off)
   uint32_t seg_small;    // lean path: bytes per row of the fixed columns of <= 16 bytes
-  uint32_t xcd_order;    // lean path: workgroups remapped to XCD-contiguous ranges of runs
+  uint32_t xcd_order;    // kXcd* bits: decodes whose workgroups take XCD-contiguous tile ranges
   uint32_t gather_block0[MDSX_MAX_COLUMNS + 1];  // first gather workgroup of each ragged column
   DevCol cols[MDSX_MAX_COLUMNS];
 };
@@ -96,6 +98,14 @@ struct TileView {
   uint64_t hdr_end;
   bool table_ok;   // the offsets table of `samples` rows fits in the file
 };
+
+// Workgroups are dealt round robin over the 8 XCDs (MI355X_MICROARCH.md, dispatch). Remapped, XCD
+// k takes the k-th contiguous eighth of the blocks (the last n % 8 keep their place), so the line
+// two neighbouring tiles share meets in one L2 instead of two. A bijection on [0, n).
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n) {
+  const uint32_t per = n >> 3;
+  return b < per * 8u ? (b & 7u) * per + (b >> 3) : b;
+}
 
 __device__ __forceinline__ TileView tile_view(const DevArgs& a, uint32_t tile) {
   TileView v;

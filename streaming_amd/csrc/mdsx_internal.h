@@ -53,8 +53,9 @@ struct mdsx_plan {
                            // is faster with them; the general one alone was slower)
   int seg = 0;             // streaming decode: the lean path for clean runs of samples that fit
                            // the ring (seg_decode_kernel; others take the general path)
-  int xcd_order = 1;       // lean path: each XCD takes a contiguous range of runs (+3 % on config
-                           // C, neutral on 3.5 and 12 KB samples: profiles/r03/xcd_order/)
+  int xcd_order = 3;       // bits: decodes whose XCDs each take a contiguous range of tiles
+                           // (profiles/r03/xcd_order/): 1 the lean path (+3 % on config C), 2 the
+                           // register decode (+1.1 % on config B); not 4, the row-parallel (-1 %)
   int seg_waves = 2;       // lean path: waves (runs) per workgroup (1, 2 or 4; 2: 18 waves per CU,
                            // +4 % on 3-5 KB samples, profiles/r03/seg_waves/)
   int rows_kb = 0;         // row-parallel decode of shorter samples: LDS stage in KiB (0: off,

@@ -320,7 +320,8 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
   const DevCol* const cols = kSlots > 0 ? s_cols : a.cols;
   if constexpr (kSlots > 0)
     for (int i = t; i < a.ncols; i += kBlock) s_cols[i] = a.cols[i];
-  uint32_t tile = blockIdx.x;
+  uint32_t tile = (!kSingle && (a.xcd_order & kXcdRegister)) ? xcd_block(blockIdx.x, gridDim.x)
+                                                              : blockIdx.x;
   if constexpr (kSingle) {
     if (t == 0) s_tile = atomicAdd(a.ticket, 1u);
   }
@@ -805,11 +806,11 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   if (tr < 1 || tr > kBlock || (tr & (tr - 1)))
     return mdsx::fail(MDSX_E_ARG, "mdsx: batch tile_rows must be a power of two in [1, 256]");
   a->stage_debug = uint32_t(plan->stage_debug);
+  a->xcd_order = uint32_t(plan->xcd_order);
   a->run_slots = use_run_decode(plan, b->bytes, b->rows) ? uint32_t(plan->run_slots) : 0u;
   if (a->run_slots && plan->seg) {
     // lean path: a sample must fit the ring with a slot to spare (seg_decode_kernel)
     a->seg_lim = a->run_slots * 1024u - 1024u - 32u;
-    a->xcd_order = uint32_t(plan->xcd_order);
     for (int c = 0; c < plan->ncols; ++c)
       if (plan->cols[c].kind == MDSX_KIND_FIXED && plan->cols[c].row_bytes <= kSmallMax)
         a->seg_small += uint32_t(plan->cols[c].row_bytes);

@@ -217,8 +217,9 @@ void apply_tuning(mdsx_plan* p) {
       p->seg_waves = int(v);
     } else if (key == "seg") {
       p->seg = v ? 1 : 0;
-    } else if (key == "xcd") {
-      p->xcd_order = v ? 1 : 0;
+    } else if (key == "xcd" || key == "xcdb" || key == "xcdr") {
+      const int bit = key == "xcd" ? 1 : key == "xcdb" ? 2 : 4;  // kXcdSeg / Register / Rows
+      p->xcd_order = v ? (p->xcd_order | bit) : (p->xcd_order & ~bit);
     } else if (key == "rkb" && v >= 1 && v <= 4096) {
       p->run_kb = int(v);
     }

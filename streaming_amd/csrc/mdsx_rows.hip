@@ -99,7 +99,7 @@ __global__ __launch_bounds__(kRowsBlock, 4) void rows_decode_kernel(const DevArg
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   for (int c = t; c < a.ncols; c += kRowsBlock) s_cols[c] = a.cols[c];
   const MDSX_L DevCol* cols = (const MDSX_L DevCol*)s_cols;
-  const uint32_t tile = blockIdx.x;
+  const uint32_t tile = (a.xcd_order & kXcdRows) ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
   const int TR = a.tile_rows;
   const int ncols = a.ncols, nvar = a.nvar;
   const uint32_t cap = a.rows_bytes;

@@ -150,11 +150,9 @@ __global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) 
   for (int c = t; c < a.ncols; c += 64 * W) s_cols[c] = a.cols[c];
   __syncthreads();
   const MDSX_L DevCol* cols = (const MDSX_L DevCol*)s_cols;
-  // workgroups are dealt round robin over the 8 XCDs (MI355X_MICROARCH.md, dispatch); remapped,
-  // XCD k takes the k-th contiguous eighth of the runs, so the line two neighbouring runs share
-  // (read: the run starts on a 128-byte line; written: partial output chunks) meets in one L2
-  const uint32_t nb = gridDim.x, per = nb >> 3, bx = blockIdx.x;
-  const uint32_t blk = (a.xcd_order && bx < per * 8u) ? (bx & 7u) * per + (bx >> 3) : bx;
+  // XCD-contiguous runs: the line two neighbouring runs share (read: a run starts on a 128-byte
+  // line; written: partial output chunks) meets in one L2
+  const uint32_t blk = (a.xcd_order & kXcdSeg) ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
   const uint32_t tile = blk * W + uint32_t(wave);
   if (tile >= a.ntiles) return;  // wave-uniform; no barrier below
   const int TR = a.tile_rows;

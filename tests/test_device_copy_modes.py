@@ -48,11 +48,13 @@ MODES = {
     'rows': 'rows=32,rmin=1000000000',  # the row-parallel decode (mdsx_rows.hip) for every size
     'rows_auto': 'rows=-1,rmin=1000000000',  # ... its tiles and stage sized per batch
     'rows_small': 'rows=2,rmin=1000000000',  # a 2 KiB stage: windows and HBM-direct samples
+    'rows_xcd': 'rows=-1,rmin=1000000000,xcdr=1',  # row-parallel tiles in XCD-contiguous ranges
     'rows_temporal': 'rows=-1,rownt=0,rmin=1000000000',  # temporal loads / stores (default: nt)
     'gather': 'run=0,rows=0,gmin=1000000000',
     'group': 'run=0,rows=0,gmin=0,gmax=1000000000',
     'group_nt': 'run=0,rows=0,gmin=0,gmax=1000000000,strc=0',  # str rows streamed (non-temporal) too
     'wave': 'run=0,rows=0,gmin=0,gmax=0,ring=0',
+    'wave_xcd0': 'run=0,rows=0,gmin=0,gmax=0,ring=0,xcdb=0',  # register tiles in launch order
     'ring': 'run=0,rows=0,gmin=0,gmax=0,ring=8',   # one row per wave through the LDS-DMA ring
     'ring4': 'run=0,rows=0,gmin=0,gmax=0,ring=4',
 }
