@@ -7,16 +7,23 @@ cache that ``StreamingDataset`` manages (``cache_limit``, ``evict_shard`` /
 ``format/base/reader.py:128-134``). The device reader decodes a whole shard at a time; this cache
 bounds what those decodes keep resident, with two separate bounds:
 
-* ``limit_bytes`` -- decoded outputs in device memory, **per device**. The decodes of a
-  ``DataLoader`` run in its worker processes, each with its own copy of the cache; inside a worker
-  the bound is split evenly over the loader's ``num_workers`` (``torch.utils.data.
-  get_worker_info``), so the workers of one loader together stay within it on their GPU;
-* ``host_limit_bytes`` -- the host copies ``get_item`` slices samples from, per process.
+* ``limit_bytes`` -- decoded outputs in device memory, **per device**: entries are counted
+  against the device they were decoded on, so readers on two GPUs sharing one cache object (the
+  process-wide default) each get the full bound on their own GPU. The decodes of a ``DataLoader``
+  run in its worker processes, each with its own copy of the cache; inside a worker the bound is
+  split evenly over the loader's ``num_workers`` (``torch.utils.data.get_worker_info``), so the
+  workers of one loader together stay within it on their GPU;
+* ``host_limit_bytes`` -- the host copies ``get_item`` slices samples from, per cache object.
 
-When either bound is exceeded the least recently used shards are dropped (their tensors return to
-the PyTorch caching allocator) and are decoded again from their files on next use. The most
-recently used shard is always kept, even when it alone exceeds a bound (a warning says so once):
-repeated reads of one shard never decode it twice.
+When a device's bound is exceeded, that device's least recently used shards are dropped (their
+tensors return to the PyTorch caching allocator) and are decoded again from their files on next
+use; the host bound drops the least recently used host-holding entries. The most recently used
+shard of each device is always kept, even when it alone exceeds a bound (a warning says so once):
+repeated reads of one shard never decode it twice. So ``limit_bytes=0`` keeps exactly one decoded
+shard per device (the one last used), not none.
+
+``clear()`` and ``discard()`` also cancel decodes in flight: their owner hands the result to the
+callers waiting on it but does not insert it.
 
 A miss decodes OUTSIDE the cache lock: readers of other shards keep hitting (and decoding) while
 one shard decodes; concurrent first touches of the same shard wait for the one decode in flight.
@@ -58,6 +65,7 @@ class _InFlight:
         self.done = threading.Event()
         self.value: Any = None
         self.error: Optional[BaseException] = None
+        self.cancelled = False  # clear() / discard() ran meanwhile: do not insert the result
 
 
 class DecodedShardCache:
@@ -76,10 +84,10 @@ class DecodedShardCache:
         self.limit_bytes = int(limit_bytes)
         self.host_limit_bytes = int(host_limit_bytes)
         self._lock = threading.RLock()
-        # key -> [value, device bytes, host bytes]
+        # key -> [value, device bytes, host bytes, device]
         self._entries: 'OrderedDict[int, list]' = OrderedDict()
         self._inflight: dict[int, _InFlight] = {}
-        self._bytes = 0
+        self._device_bytes: dict[Any, int] = {}
         self._host_bytes = 0
         self._warned = False
         self.hits = 0
@@ -93,8 +101,12 @@ class DecodedShardCache:
 
     @property
     def resident_bytes(self) -> int:
-        """Device bytes of the decoded shards held."""
-        return self._bytes
+        """Device bytes of the decoded shards held (all devices)."""
+        return sum(self._device_bytes.values())
+
+    def device_bytes(self, device: Any = None) -> int:
+        """Device bytes of the decoded shards held on ``device``."""
+        return self._device_bytes.get(device, 0)
 
     @property
     def resident_host_bytes(self) -> int:
@@ -116,11 +128,13 @@ class DecodedShardCache:
             self._entries.move_to_end(key)
             return hit[0]
 
-    def get_or_create(self, key: int, create: Callable[[], tuple[Any, int]]) -> Any:
-        """The value for ``key``, made by ``create() -> (value, device bytes)`` on a miss.
+    def get_or_create(self, key: int, create: Callable[[], tuple]) -> Any:
+        """The value for ``key``, made by ``create() -> (value, device bytes[, device])`` on a
+        miss.
 
         ``create`` runs without the cache lock held; a second caller of the same key waits for
-        it (and gets its error, if it raised)."""
+        it (and gets its error, if it raised). A ``clear()`` / ``discard(key)`` meanwhile cancels
+        the insertion (the callers still get the value)."""
         with self._lock:
             hit = self._entries.get(key)
             if hit is not None:
@@ -140,7 +154,9 @@ class DecodedShardCache:
                 raise flight.error
             return flight.value
         try:
-            value, nbytes = create()
+            made = create()
+            value, nbytes = made[0], made[1]
+            device = made[2] if len(made) > 2 else None
         except BaseException as e:
             with self._lock:
                 self._inflight.pop(key, None)
@@ -149,7 +165,8 @@ class DecodedShardCache:
             raise
         with self._lock:
             self._inflight.pop(key, None)
-            self.put(key, value, nbytes)
+            if not flight.cancelled:
+                self.put(key, value, nbytes, device=device)
         flight.value = value
         flight.done.set()
         return value
@@ -161,15 +178,16 @@ class DecodedShardCache:
     def __setstate__(self, state: dict) -> None:
         self.__init__(state['limit_bytes'], state.get('host_limit_bytes'))
 
-    def put(self, key: int, value: Any, nbytes: int, host_bytes: int = 0) -> None:
-        """Insert (or replace) ``key`` as the most recently used entry and evict down to the
-        bounds; the entry itself is kept even when it alone exceeds one."""
+    def put(self, key: int, value: Any, nbytes: int, host_bytes: int = 0,
+            device: Any = None) -> None:
+        """Insert (or replace) ``key`` as the most recently used entry of ``device`` and evict
+        down to the bounds; the entry itself is kept even when it alone exceeds one."""
         with self._lock:
-            self.discard(key)
-            self._entries[key] = [value, int(nbytes), int(host_bytes)]
-            self._bytes += int(nbytes)
+            self._drop(key)
+            self._entries[key] = [value, int(nbytes), int(host_bytes), device]
+            self._device_bytes[device] = self._device_bytes.get(device, 0) + int(nbytes)
             self._host_bytes += int(host_bytes)
-            self._shrink()
+            self._shrink(key)
 
     def set_host_bytes(self, key: int, host_bytes: int) -> None:
         """Count a resident entry's host copy (added after its decode) and evict to the bounds."""
@@ -180,36 +198,54 @@ class DecodedShardCache:
             self._host_bytes += int(host_bytes) - hit[2]
             hit[2] = int(host_bytes)
             self._entries.move_to_end(key)
-            self._shrink()
+            self._shrink(key)
 
-    def _shrink(self) -> None:
+    def _shrink(self, newest: int) -> None:
+        """Evict to the bounds after ``newest`` was inserted or grew: the device bound over the
+        entries of its device, the host bound over every entry; ``newest`` itself stays."""
         dev_limit = self.device_limit()
-        while len(self._entries) > 1 and (self._bytes > dev_limit or
-                                          self._host_bytes > self.host_limit_bytes):
-            _, (_, old, old_host) = self._entries.popitem(last=False)
-            self._bytes -= old
-            self._host_bytes -= old_host
+        device = self._entries[newest][3]
+        for key in [k for k, e in self._entries.items() if e[3] == device and k != newest]:
+            if self._device_bytes.get(device, 0) <= dev_limit:
+                break
+            self._drop(key)
             self.evictions += 1
-        if (self._bytes > dev_limit or self._host_bytes > self.host_limit_bytes) and \
-                not self._warned:
+        for key in [k for k, e in self._entries.items() if e[2] and k != newest]:
+            if self._host_bytes <= self.host_limit_bytes:
+                break
+            self._drop(key)
+            self.evictions += 1
+        over_dev = self._device_bytes.get(device, 0) > dev_limit
+        if (over_dev or self._host_bytes > self.host_limit_bytes) and not self._warned:
             self._warned = True
-            warnings.warn(f'streaming_amd: one decoded shard ({self._bytes} device bytes, '
-                          f'{self._host_bytes} host bytes) exceeds the decoded-shard cache bound '
-                          f'({dev_limit} device bytes for this process, {self.host_limit_bytes} '
-                          f'host bytes); it is kept while it is the most recently used')
+            warnings.warn(f'streaming_amd: one decoded shard ({self._device_bytes.get(device, 0)} '
+                          f'device bytes, {self._host_bytes} host bytes) exceeds the decoded-shard '
+                          f'cache bound ({dev_limit} device bytes for this process, '
+                          f'{self.host_limit_bytes} host bytes); it is kept while it is the most '
+                          f'recently used')
+
+    def _drop(self, key: int) -> None:
+        hit = self._entries.pop(key, None)
+        if hit is not None:
+            self._device_bytes[hit[3]] -= hit[1]
+            self._host_bytes -= hit[2]
 
     def discard(self, key: int) -> None:
+        """Drop ``key`` (and cancel the insertion of a decode of it in flight)."""
         with self._lock:
-            hit = self._entries.pop(key, None)
-            if hit is not None:
-                self._bytes -= hit[1]
-                self._host_bytes -= hit[2]
+            self._drop(key)
+            flight = self._inflight.get(key)
+            if flight is not None:
+                flight.cancelled = True
 
     def clear(self) -> None:
+        """Drop every entry (and cancel the insertion of every decode in flight)."""
         with self._lock:
             self._entries.clear()
-            self._bytes = 0
+            self._device_bytes.clear()
             self._host_bytes = 0
+            for flight in self._inflight.values():
+                flight.cancelled = True
 
 
 _default: Optional[DecodedShardCache] = None

@@ -10,9 +10,14 @@
 //
 // Pass 1 (stage_totals_kernel + the reduce-then-scan kernels, mdsx_stage.hip / mdsx_kernels.hip):
 // each tile's ragged bytes from the offsets table and the heads, scanned into each tile's output
-// base per ragged column.
+// base per ragged column; each run's record says whether the lean path can take it.
 //
-// Pass 2 (run_decode_kernel): a wave keeps up to S KiB of its run in flight into its LDS ring
+// Pass 2, by default seg_decode_kernel (the lean path, below): one wait per sample, lane-parallel
+// column geometry, for every run whose samples pass the file checks and fit the ring; the runs it
+// does not take go to the general path, run_body (mdsx_run_body.h), which is also a kernel of its
+// own (run_decode_kernel, MDSX_TUNE=seg=0) and is described here.
+//
+// The general path: a wave keeps up to S KiB of its run in flight into its LDS ring
 // (global_load_lds_dwordx4: 1 KiB per wave-instruction, no VGPR destination) and walks the run's
 // samples in order, all control wave-uniform:
 //   * the sample's size heads are read from the ring (decode_sample's head loop) and its column

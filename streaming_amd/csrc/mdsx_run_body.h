@@ -1,7 +1,8 @@
-// The streaming decode's general path (run_body), shared by the streaming decode (mdsx_run.hip)
-// and the wave-parallel row decode (mdsx_wrows.hip, which hands it the runs its fast path does not
-// take): a wave streams its run -- consecutive samples of one shard -- through its LDS ring once,
-// sample by sample, any sample size, samples failing the file checks reported one by one.
+// The streaming decode's general path (run_body), used by both kernels of mdsx_run.hip: the
+// general-path kernel (run_decode_kernel) and the lean path (seg_decode_kernel), which hands it
+// the runs its fast form does not take. A wave streams its run -- consecutive samples of one
+// shard -- through its LDS ring once, sample by sample, any sample size, samples failing the file
+// checks reported one by one.
 // (The reference: MDSReader.get_sample_data / decode_sample, streaming/base/format/mds/
 // reader.py:103-149; column decoders, encodings.py:62-397, 760-773.)
 #pragma once

@@ -361,7 +361,8 @@ def ndarray_meta(col: 'RaggedColumn', dtype_id: int = 0) -> NdarrayMeta:
 @dataclass
 class DecodedBatch:
     """Decoded columns of a :class:`DeviceBatch` (device tensors). ``stream``: the stream the
-    decode ran on (None: the gathers' own stream, e.g. a gather's output)."""
+    columns were written on (the decode's, or the gather's that made them; None: unknown,
+    taken as the reader's current stream)."""
     columns: dict[str, Union[torch.Tensor, RaggedColumn]]
     rows: int
     row0: list[int] = field(default_factory=list)
@@ -436,7 +437,7 @@ class DecodedBatch:
             st = _native.Status.from_buffer_copy(ws[:16].cpu().numpy().tobytes())
             if st.code != 0:
                 raise IndexError(f'sample id out of range at position {st.row} of the gather')
-        return DecodedBatch(out, m)
+        return DecodedBatch(out, m, stream=torch.cuda.current_stream(dev))
 
 
 def _require_device_columns(batches: Sequence['DecodedBatch']) -> None:
@@ -557,7 +558,8 @@ def gather_sources(sources: Sequence[DecodedBatch], src: np.ndarray, rows: np.nd
         out[name] = RaggedColumn(vals[:cap], offs[name], flags)
     # (a source freed after this returns is reused in stream order: these kernels come first;
     # sources of another stream were marked in use by this one, _on_current_stream)
-    return DecodedBatch({name: out[name] for name in names}, m)
+    return DecodedBatch({name: out[name] for name in names}, m,
+                        stream=torch.cuda.current_stream(dev))
 
 
 def _status_error(status: _native.Status, plan: Plan) -> Exception:

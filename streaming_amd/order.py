@@ -36,7 +36,7 @@ import torch
 from streaming_amd.decoder import DecodedBatch, RaggedColumn, gather_sources
 from streaming_amd.reader import MDSReader
 
-__all__ = ['worker_sample_ids', 'concat_batches', 'DeviceSampleGather']
+__all__ = ['worker_sample_ids', 'loader_batches', 'concat_batches', 'DeviceSampleGather']
 
 
 def worker_sample_ids(epoch_sample_ids: np.ndarray, node: int, rank_of_node: int,
@@ -44,6 +44,32 @@ def worker_sample_ids(epoch_sample_ids: np.ndarray, node: int, rank_of_node: int
     """One worker's portion of ``generate_work``'s array, flattened (``dataset.py:1054-1056``);
     the ``-1`` padding is kept (the iteration skips it)."""
     return np.asarray(epoch_sample_ids, np.int64)[node, rank_of_node, worker_of_rank].reshape(-1)
+
+
+def loader_batches(epoch_sample_ids: np.ndarray, node: int, rank_of_node: int, workers: int,
+                   batch_size: int) -> list[np.ndarray]:
+    """The sample ids of each batch a ``DataLoader(dataset, batch_size, num_workers=workers)``
+    over a ``StreamingDataset`` yields on one rank, in the loader's order.
+
+    Each worker iterates its own slice of ``generate_work``'s array (``world.py:150-163``,
+    ``dataset.py:1054-1056``), ``-1`` skipped (``_each_sample_id``), and the loader's fetcher
+    cuts that stream into batches of ``batch_size`` consecutive samples (the last one may be
+    short). Torch hands out batch index i to the workers round robin and returns them in index
+    order, skipping a worker once it is exhausted (its remaining indices are dropped,
+    ``torch/utils/data/dataloader.py`` ``_MultiProcessingDataLoaderIter``): batch k of every
+    worker still running, worker by worker, for k = 0, 1, ... ``workers`` 0 (no worker
+    processes) iterates as one worker."""
+    workers = max(1, int(workers))
+    arr = np.asarray(epoch_sample_ids, np.int64)
+    per_worker = []
+    for w in range(workers):
+        ids = worker_sample_ids(arr, node, rank_of_node, w)
+        ids = ids[ids != -1]
+        per_worker.append([ids[lo:lo + batch_size] for lo in range(0, ids.size, batch_size)])
+    out = []
+    for k in range(max((len(b) for b in per_worker), default=0)):
+        out.extend(b[k] for b in per_worker if k < len(b))
+    return out
 
 
 def concat_batches(parts: Sequence[DecodedBatch]) -> DecodedBatch:
@@ -65,7 +91,10 @@ def concat_batches(parts: Sequence[DecodedBatch]) -> DecodedBatch:
             cols[name] = RaggedColumn(vals, torch.cat(offs), flags)
         else:
             cols[name] = torch.cat(xs)
-    return DecodedBatch(cols, sum(p.rows for p in parts))
+    first = next(iter(cols.values()))
+    dev = (first.offsets if isinstance(first, RaggedColumn) else first).device
+    return DecodedBatch(cols, sum(p.rows for p in parts),
+                        stream=torch.cuda.current_stream(dev) if dev.type == 'cuda' else None)
 
 
 class DeviceSampleGather:

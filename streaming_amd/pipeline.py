@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import os
 import threading
+import time
 from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass
 from typing import Iterator, Optional, Sequence, Union
@@ -164,6 +165,18 @@ class ShardPipeline:
         self.pool = ThreadPoolExecutor(max_workers=max(1, workers))
         self.copy_stream = torch.cuda.Stream(dev)
         self._lock = threading.Lock()
+        # measurement only (scripts/e2e_bench.py --trace): a list collects (what, batch, host
+        # seconds, timing event on the stream the step was queued on or None)
+        self.trace: Optional[list] = None
+
+    def _mark(self, what: str, gi: int, stream: Optional[torch.cuda.Stream] = None) -> None:
+        if self.trace is None:
+            return
+        ev = None
+        if stream is not None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(stream)
+        self.trace.append((what, gi, time.perf_counter(), ev))
 
     def _stage(self, slot: _Slot, group: Sequence[ShardFile], after: bool = False):
         """Read / decompress ``group`` into the slot's pinned buffer on the pool threads; with
@@ -204,10 +217,13 @@ class ShardPipeline:
             slot, futs, sizes, offsets, total, group = pending.pop(0)
             for f in futs:
                 f.result()
+            self._mark('staged', gi)
             with torch.cuda.stream(self.copy_stream):
                 self.copy_stream.wait_event(slot.decoded)  # device slot free again
+                self._mark('h2d_start', gi, self.copy_stream)
                 slot.dev[:total].copy_(slot.host[:total], non_blocking=True)
                 slot.copied.record(self.copy_stream)
+                self._mark('h2d_end', gi, self.copy_stream)
             compute.wait_event(slot.copied)
             # Restage this slot for batch gi + depth right away: the pool threads wait for this
             # copy to land, then refill the pinned buffer, while this loop moves on (copies are
@@ -230,8 +246,10 @@ class ShardPipeline:
                 slot.decoder._abi = batch.abi()
                 if self.plan.num_var:
                     slot.decoder._sized = False  # ragged totals differ per batch: re-size
+            self._mark('decode_start', gi, compute)
             out = slot.decoder.run()
             slot.decoded.record(compute)
+            self._mark('decode_end', gi, compute)
             if digests is not None:
                 _status_check(hstatus)
                 for got, shard in zip(hex_digests(self.validate_hash, digests), group):
@@ -241,6 +259,7 @@ class ShardPipeline:
             # reference raises when that sample is read); waits for this batch's decode, while
             # the next batches' reads and copies stay queued
             slot.decoder.check()
+            self._mark('yield', gi)
             yield out
 
     def iter_host(self) -> Iterator[dict[str, Union[np.ndarray, tuple]]]:
@@ -254,15 +273,18 @@ class ShardPipeline:
         compute = torch.cuda.current_stream(self.device)
         d2h = torch.cuda.Stream(self.device)
         prev = None
-        for out in self:
-            host, done = _to_host_async(out, d2h, compute)
+        for gi, out in enumerate(self):
+            host, done = _to_host_async(out, d2h, compute, self._mark if self.trace is not None
+                                        else None, gi)
             compute.wait_event(done)  # the slot's outputs are reused by later decodes
             if prev is not None:
                 prev[1].synchronize()
+                self._mark('host_yield', gi - 1)
                 yield _host_arrays(prev[0])
             prev = (host, done)
         if prev is not None:
             prev[1].synchronize()
+            self._mark('host_yield', len(self.groups) - 1)
             yield _host_arrays(prev[0])
 
     def close(self) -> None:
@@ -270,12 +292,14 @@ class ShardPipeline:
 
 
 def _to_host_async(decoded: DecodedBatch, stream: torch.cuda.Stream,
-                   after: torch.cuda.Stream) -> tuple[dict, torch.cuda.Event]:
+                   after: torch.cuda.Stream, mark=None, gi: int = 0) -> tuple[dict, torch.cuda.Event]:
     """Queue the D2H copies of every column of ``decoded`` (pinned host tensors) on ``stream``,
     behind the work queued so far on ``after``; returns the host tensors and the copies' event."""
     ready = torch.cuda.Event()
     ready.record(after)
     stream.wait_event(ready)
+    if mark is not None:
+        mark('d2h_start', gi, stream)
     lib = _native.lib()
     out = {}
     with torch.cuda.stream(stream):
@@ -300,6 +324,8 @@ def _to_host_async(decoded: DecodedBatch, stream: torch.cuda.Stream,
                     h.copy_(t, non_blocking=True)
                 host.append(h)
             out[name] = host if isinstance(col, RaggedColumn) else host[0]
+    if mark is not None:
+        mark('d2h_end', gi, stream)
     done = torch.cuda.Event()
     done.record(stream)
     return out, done

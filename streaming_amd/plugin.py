@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import os
 import sys
+from bisect import bisect_right
 from concurrent.futures import ThreadPoolExecutor, wait
 from threading import Event
 from time import time_ns
@@ -86,15 +87,41 @@ def register_device_stream(name: str = 'mdsx',
     return cls
 
 
-def _iterator_class(dataset: Any) -> type:
-    """The reference's ``_Iterator`` (``dataset.py:64-166``), from the module that defines the
-    dataset's iteration methods (any ``StreamingDataset`` subclass, or a stand-in)."""
+# What device_iter drives of StreamingDataset.__iter__ (dataset.py:1475-1513), by name. They are
+# private to the reference; device_iter checks them up front against the installed version.
+_ITER_METHODS = ('_resume_incr_epoch', '_prepare_thread', '_ready_thread', '_each_sample_id',
+                 'on_exception', 'prepare_shard')
+_ITER_STATE = ('_shard_access_times', '_unique_rank_world', '_parallel_rank_world')
+_TESTED_REFERENCE = '0.14.0.dev0'  # mosaicml/streaming, streaming/_version.py:6
+
+
+def _iteration_module(dataset: Any) -> Any:
+    """The module that defines the dataset's iteration methods (any ``StreamingDataset``
+    subclass, or a stand-in): it holds ``_Iterator``, ``generate_work`` and ``World``."""
     for klass in type(dataset).__mro__:
         if '_each_sample_id' in klass.__dict__:
-            mod = sys.modules[klass.__module__]
-            if hasattr(mod, '_Iterator'):
-                return mod._Iterator
-    raise TypeError(f'{type(dataset).__name__} has no StreamingDataset iteration to follow')
+            return sys.modules.get(klass.__module__)
+    return None
+
+
+def _require_iteration_surface(dataset: Any, num_workers: int) -> Any:
+    """Check, before anything runs, that every private piece of ``StreamingDataset.__iter__``
+    that :func:`device_iter` drives exists; one ``TypeError`` names all that are missing."""
+    missing = [a for a in _ITER_METHODS if not callable(getattr(dataset, a, None))]
+    missing += [a for a in _ITER_STATE if not hasattr(dataset, a)]
+    if num_workers <= 1 and not callable(getattr(dataset, '_get_work', None)):
+        missing.append('_get_work')
+    mod = _iteration_module(dataset)
+    needed = ['_Iterator'] + (['generate_work', 'World'] if num_workers > 1 else [])
+    missing += [f'{getattr(mod, "__name__", "<module>")}.{n}' for n in needed
+                if mod is None or not hasattr(mod, n)]
+    if missing:
+        top = sys.modules.get((getattr(mod, '__name__', '') or '').split('.')[0])
+        version = getattr(top, '__version__', 'unknown')
+        raise TypeError(f'device_iter: {type(dataset).__name__} lacks the StreamingDataset '
+                        f'iteration internals it drives: {", ".join(missing)} (installed streaming '
+                        f'{version}; device_iter follows mosaicml/streaming {_TESTED_REFERENCE})')
+    return mod
 
 
 def _gather_batch(dataset: Any, gather: Any, ids: list, retry: int) -> DecodedBatch:
@@ -134,36 +161,43 @@ def _gather_batch(dataset: Any, gather: Any, ids: list, retry: int) -> DecodedBa
     return out
 
 
-def device_iter(dataset: Any, batch_size: int, *, retry: int = 7,
+def device_iter(dataset: Any, batch_size: int, *, num_workers: int = 0, retry: int = 7,
                 gather: Optional[Any] = None) -> Iterator[DecodedBatch]:
-    """``StreamingDataset.__iter__`` (``dataset.py:1475-1513``) yielding DEVICE batches.
+    """``StreamingDataset.__iter__`` (``dataset.py:1475-1513``) yielding DEVICE batches, in the
+    order ``DataLoader(dataset, batch_size, num_workers=num_workers)`` yields them on this rank.
 
     The reference's own control flow, step for step: the previous epoch's iterator is exited,
     the worker world detected, the epoch incremented or resumed (``_resume_incr_epoch``: a
-    ``load_state_dict`` checkpoint resumes mid-epoch, ``dataset.py:691-776``), this worker's ids
-    laid out by ``_get_work`` (``generate_work``, ``dataset.py:1012-1066``), and the
-    ``_prepare_thread`` / ``_ready_thread`` started on the dataset's executor to download and
-    ready shards ahead of the loop (``dataset.py:1313-1428``). The ids then come from
-    ``_each_sample_id`` -- in order, ``-1`` skipped, each once its shard is ready -- and every
-    ``batch_size`` of them (the last batch may be short) are gathered on the GPU from the
-    shards' decoded columns (:class:`streaming_amd.order.DeviceSampleGather`: shards decoded
-    on demand through the bounded decoded-shard cache, one launch sequence per column) instead
-    of ``map(self.__getitem__, ...)`` and ``default_collate``. Each batch carries its
+    ``load_state_dict`` checkpoint resumes mid-epoch, ``dataset.py:691-776``), the ids laid out
+    (``_get_work`` / ``generate_work``, ``dataset.py:1012-1066``), and the ``_prepare_thread`` /
+    ``_ready_thread`` started on the dataset's executor to download and ready shards ahead of the
+    loop (``dataset.py:1313-1428``). The ids then come from ``_each_sample_id`` -- in order,
+    ``-1`` skipped, each once its shard is ready -- and each batch's ids are gathered on the GPU
+    from the shards' decoded columns (:class:`streaming_amd.order.DeviceSampleGather`: shards
+    decoded on demand through the bounded decoded-shard cache, one launch sequence per column)
+    instead of ``map(self.__getitem__, ...)`` and ``default_collate``. Each batch carries its
     ``sample_ids``.
 
-    The dataset's shards must be device readers (``stream_name='mdsx'``,
-    :func:`register_device_stream`). Run it in the process that owns the GPU (a ``DataLoader``
-    with ``num_workers=0``, or no loader): the decode runs on the device, so there is nothing
-    for host workers to parallelise. Checkpoints are the reference's: ``dataset.state_dict(
-    num_samples, from_beginning)`` with the samples consumed so far, then ``load_state_dict`` and
-    a new ``device_iter`` resume there.
+    ``num_workers``: the loader being replaced. 0 or 1: this rank's one partition in batches of
+    ``batch_size`` (the last may be short). W > 1: the W worker partitions of ``generate_work``
+    for a World of W workers per rank (``world.py:150-163``), each cut into batches of its own,
+    interleaved as torch's DataLoader returns them (:func:`streaming_amd.order.loader_batches`)
+    -- all in this one process, which owns the GPU (the decode runs on the device; there is
+    nothing for host workers to parallelise). Run it in every rank: under ``RANK`` /
+    ``WORLD_SIZE`` each rank gets its own partition as with the reference.
 
-    ``gather``: what turns ids into a batch (default: a ``DeviceSampleGather`` over
-    ``dataset.shards``); an object with ``gather(ids)``, ``locate(ids)`` and ``shards``.
+    Checkpoints are ``StreamingDataLoader``'s (:class:`DeviceBatches`).
+
+    The dataset's shards must be device readers (``stream_name='mdsx'``,
+    :func:`register_device_stream`). ``gather``: what turns ids into a batch (default: a
+    ``DeviceSampleGather`` over ``dataset.shards``); an object with ``gather(ids)``,
+    ``locate(ids)`` and ``shards``.
     """
     if batch_size <= 0:
         raise ValueError('batch_size must be positive')
     ds = dataset
+    workers = max(1, int(num_workers))
+    mod = _require_iteration_surface(ds, workers)
     if gather is None:
         from streaming_amd.order import DeviceSampleGather
         bad = [i for i, s in enumerate(ds.shards) if not isinstance(s, MDSReader)]
@@ -172,7 +206,6 @@ def device_iter(dataset: Any, batch_size: int, *, retry: int = 7,
                             f'not a device reader (build the dataset with stream_name=\'mdsx\', '
                             f'streaming_amd.plugin.register_device_stream)')
         gather = DeviceSampleGather(ds.shards)
-    Iterator_ = _iterator_class(ds)
     # -- StreamingDataset.__iter__, dataset.py:1481-1510
     if hasattr(ds, '_iterator'):
         ds._iterator.exit()
@@ -182,34 +215,86 @@ def device_iter(dataset: Any, batch_size: int, *, retry: int = 7,
         ds._event = Event()
     elif ds._event.is_set():
         raise RuntimeError('Background thread failed. Check other traceback.')
+    # this process is the rank's only iterating process: a one-worker world for the epoch
+    # barrier of _resume_incr_epoch / _get_work
     ds._unique_worker_world = ds._unique_rank_world.detect_workers()
     ds._parallel_worker_world = ds._parallel_rank_world.detect_workers()
     epoch, sample_in_epoch = ds._resume_incr_epoch()
-    sample_ids = ds._get_work(epoch, sample_in_epoch)
+    if workers == 1:
+        sample_ids = ds._get_work(epoch, sample_in_epoch)
+        sizes = None
+    else:
+        sample_ids, sizes = _loader_work(ds, mod, workers, batch_size, epoch, sample_in_epoch)
     if not len(sample_ids):  # resumed at the end of the epoch: out of samples
         return
-    ds._iterator = it = Iterator_(sample_ids)
+    ds._iterator = it = mod._Iterator(sample_ids)
     prepare_future = ds._executor.submit(ds._prepare_thread, it)
     prepare_future.add_done_callback(ds.on_exception)
     ready_future = ds._executor.submit(ds._ready_thread, it)
     ready_future.add_done_callback(ds.on_exception)
     # -- in place of `yield from map(self.__getitem__, self._each_sample_id(it))`
-    pending = []
+    stamp = _access_stamper(ds, gather)
+    pending: list[int] = []
+    k = 0
+    want = sizes[0] if sizes else batch_size
     for sample_id in ds._each_sample_id(it):
+        stamp(sample_id)  # get_item's access-time touch, as each sample is read (dataset.py:1270)
         pending.append(sample_id)
-        if len(pending) == batch_size:
+        if len(pending) == want:
             yield _gather_batch(ds, gather, pending, retry)
             pending = []
+            k += 1
+            want = sizes[k] if sizes and k < len(sizes) else batch_size
     if pending:
         yield _gather_batch(ds, gather, pending, retry)
     wait([prepare_future, ready_future], return_when='FIRST_EXCEPTION')
     it.exit()
 
 
+def _loader_work(ds: Any, mod: Any, workers: int, batch_size: int, epoch: int,
+                 sample_in_epoch: int) -> tuple[np.ndarray, list[int]]:
+    """This rank's ids in a W-worker loader's order, and its batch sizes: ``generate_work``
+    (what ``_get_work``'s local leader runs, ``dataset.py:1041-1052``) for a World of W workers
+    per rank, then each worker's slice interleaved as the DataLoader returns them."""
+    from streaming_amd.order import loader_batches
+    if not isinstance(getattr(ds, 'batch_size', None), int):
+        raise ValueError(f'Please pass `batch_size` to StreamingDataset. It should be ' +
+                         f'set the same as the DataLoader, and is the number of samples ' +
+                         f'per batch, for each device. It is necessary for ' +
+                         f'deterministic resumption and optimal performance.')
+    pw = ds._parallel_rank_world
+    world = mod.World(num_nodes=pw.num_nodes, ranks_per_node=pw.ranks_per_node,
+                      workers_per_rank=workers, worker=pw.rank * workers)
+    epoch_ids = mod.generate_work(ds.batching_method, ds, world, epoch, sample_in_epoch)
+    batches = loader_batches(epoch_ids, world.node, world.rank_of_node, workers, batch_size)
+    ids = np.concatenate(batches) if batches else np.empty(0, np.int64)
+    return ids, [len(b) for b in batches]
+
+
+def _access_stamper(ds: Any, gather: Any) -> Callable[[int], None]:
+    """Per sample id: stamp its shard's access time (``dataset.py:1270``) so the prepare
+    thread's ``cache_limit`` eviction sees the shards of a pending batch as recently used."""
+    times = ds._shard_access_times
+    starts = getattr(gather, 'starts', None)
+    if starts is not None:
+        bounds = [int(x) for x in starts]
+
+        def stamp(sid: int) -> None:
+            times[bisect_right(bounds, sid) - 1] = time_ns()
+    else:
+
+        def stamp(sid: int) -> None:
+            times[int(gather.locate(np.asarray([sid], np.int64))[0][0])] = time_ns()
+
+    return stamp
+
+
 class DeviceBatches:
     """An iterable of device batches over a ``StreamingDataset`` (one :func:`device_iter` per
-    epoch), counting the samples it hands out so that :meth:`state_dict` checkpoints mid-epoch as
-    ``StreamingDataLoader`` does (``dataloader.py:50-96``, single process)."""
+    epoch) that checkpoints like ``StreamingDataLoader`` (``dataloader.py:50-96``): it counts
+    the samples it hands out on this rank, and :meth:`state_dict` passes the global count --
+    this rank's times the number of ranks, divided by ``replication`` when set -- to
+    ``dataset.state_dict(num_samples, False)``."""
 
     def __init__(self, dataset: Any, batch_size: int, **kwargs: Any) -> None:
         self.dataset = dataset
@@ -225,7 +310,12 @@ class DeviceBatches:
 
     def state_dict(self) -> dict[str, Any]:
         """The dataset's checkpoint after the samples handed out so far this epoch."""
-        return self.dataset.state_dict(self.num_samples_yielded, False)
+        num_ranks = int(getattr(self.dataset._unique_rank_world, 'num_ranks', 1))
+        num_samples = self.num_samples_yielded * num_ranks
+        replication = getattr(self.dataset, 'replication', None)
+        if replication is not None:
+            num_samples = num_samples // replication
+        return self.dataset.state_dict(num_samples, False)
 
     def load_state_dict(self, obj: dict[str, Any]) -> None:
         self.dataset.load_state_dict(obj)

@@ -340,7 +340,7 @@ class MDSReader(JointReader):
             out = dec.run()
             status = dec.status()  # waits for the decode
             nbytes = output_bytes(plan, out)
-            return _Decoded(out, status, nbytes), nbytes
+            return _Decoded(out, status, nbytes), nbytes, str(batch.device)  # bound per device
 
         with self._lock:
             return self.cache.get_or_create(self._key, create)

@@ -95,6 +95,44 @@ def main(ref: str, scratch: str) -> None:
         res['resume_count'] = len(numbers) == st['iter_resume_count']
         del ds3
         out[name] = res
+    # multi-worker loaders (tests/golden/order/loader.json, one rank): device_iter(num_workers=W)
+    # against the reference's StreamingDataLoader(num_workers=W), start, checkpoint and resume
+    with open(os.path.join(REPO, 'tests', 'golden', 'order', 'loader.json')) as f:
+        loaders = {s['name']: s for s in json.load(f)['settings']}
+    for name in ('py1e_r1w2', 'noshuffle_r1w3'):
+        st = loaders[name]
+        pr = st['per_rank'][0]
+        bs, W = st['kwargs']['batch_size'], st['workers']
+        clean_stale_shared_memory()
+        local = os.path.join(scratch, name)
+        shutil.copytree(os.path.join(REPO, 'tests', 'golden', 'config_a'), local)
+        with open(os.path.join(local, 'index.json')) as f:
+            infos = json.load(f)['shards']
+        OracleGather.readers = [OracleMDSReader(local, None, info) for info in infos]
+        res = {}
+        ds = StreamingDataset(local=local, stream_name='mdsx', **st['kwargs'])
+        numbers, words, sizes = run(device_iter(ds, bs, num_workers=W,
+                                                gather=OracleGather(ds.shards)))
+        res['start'] = digest(numbers, words) == pr['iter_start_sha256']
+        res['start_sizes'] = sizes == pr['start_batch_sizes']
+        ds2 = StreamingDataset(local=local, stream_name='mdsx', **st['kwargs'])
+        batches = DeviceBatches(ds2, bs, num_workers=W, gather=OracleGather(ds2.shards))
+        it = iter(batches)
+        for _ in range(st['resume_batches']):
+            next(it)
+        state = batches.state_dict()
+        res['state_dict'] = state == st['state_dict']
+        ds2._iterator.exit()
+        del it, batches, ds2, ds
+        clean_stale_shared_memory()
+        ds3 = StreamingDataset(local=local, stream_name='mdsx', **st['kwargs'])
+        ds3.load_state_dict(state)
+        numbers, words, sizes = run(device_iter(ds3, bs, num_workers=W,
+                                                gather=OracleGather(ds3.shards)))
+        res['resume'] = digest(numbers, words) == pr['iter_resume_sha256']
+        res['resume_sizes'] = sizes == pr['resume_batch_sizes']
+        del ds3
+        out[name] = res
     clean_stale_shared_memory()
     print(json.dumps(out))
 

@@ -36,23 +36,53 @@ class _Iterator:
         pass
 
 
-class _World:
+class World:
+    """world.py:39-163 restated: node / rank / worker coordinates of one process."""
 
-    def detect_workers(self) -> '_World':
-        return self
+    def __init__(self, num_nodes, ranks_per_node, workers_per_rank, worker) -> None:
+        self.node = worker // (ranks_per_node * workers_per_rank)
+        self.num_nodes = num_nodes
+        self.rank = worker // workers_per_rank
+        self.num_ranks = num_nodes * ranks_per_node
+        self.rank_of_node = self.rank % ranks_per_node
+        self.ranks_per_node = ranks_per_node
+        self.worker = worker
+        self.workers_per_rank = workers_per_rank
+        self.worker_of_rank = worker % workers_per_rank
+        self.workers_per_node = ranks_per_node * workers_per_rank
+        self.is_local_leader = not (worker % self.workers_per_node)
+
+    def detect_workers(self) -> 'World':  # no DataLoader worker processes here
+        return World(self.num_nodes, self.ranks_per_node, 1, self.rank)
+
+
+def generate_work(batching_method, dataset, world, epoch, sample_in_epoch):
+    """batching/__init__.py:28-45: the stand-in returns the epoch's recorded 5-D id array."""
+    return dataset._epoch_work(world, epoch, sample_in_epoch)
 
 
 class StandInDataset:
 
-    def __init__(self, shards, work) -> None:
-        """``work(epoch, sample_in_epoch)``: this worker's flattened ids (``-1`` padding kept)."""
+    def __init__(self, shards, work, epoch_work=None, world=(1, 1, 0), batch_size=None) -> None:
+        """``work(epoch, sample_in_epoch)``: this worker's flattened ids (``-1`` padding kept);
+        ``epoch_work(world, epoch, sample_in_epoch)``: ``generate_work``'s 5-D array for a World
+        (multi-worker iteration); ``world``: (nodes, ranks per node, rank)."""
         self.shards = shards
         self._work = work
+        self._epoch_work = epoch_work
+        self.batch_size = batch_size
+        self.batching_method = 'random'
+        self.replication = None
         self._shard_access_times = np.zeros(len(shards), np.uint64)
-        self._unique_rank_world = self._parallel_rank_world = _World()
+        nodes, rpn, rank = world
+        self._unique_rank_world = self._parallel_rank_world = World(nodes, rpn, 1, rank)
         self.next_epoch = 0
         self._resume = None
         self.prepared = []
+
+    def state_dict(self, num_samples, from_beginning):
+        """dataset.py:778-814, the fields the stand-in keeps."""
+        return {'epoch': self.next_epoch - 1, 'sample_in_epoch': num_samples}
 
     def load_state_dict(self, obj) -> None:
         self._resume = (obj['epoch'], obj['sample_in_epoch'])

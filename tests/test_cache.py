@@ -124,3 +124,55 @@ def test_failed_decode_reaches_every_waiter_and_is_not_cached():
     for t in threads:
         t.join()
     assert len(errors) == 3 and 9 not in c
+
+
+def test_bound_is_per_device():
+    """Readers on two GPUs sharing one cache object (the process-wide default) each get the
+    whole bound on their own device: an entry of one device never evicts the other's."""
+    c = DecodedShardCache(100)
+    c.put(1, 'a', 60, device='cuda:0')
+    c.put(2, 'b', 60, device='cuda:1')
+    assert 1 in c and 2 in c
+    assert c.device_bytes('cuda:0') == 60 and c.device_bytes('cuda:1') == 60
+    c.put(3, 'c', 60, device='cuda:0')  # cuda:0 over its bound: only cuda:0's LRU goes
+    assert 1 not in c and 2 in c and 3 in c
+    assert c.resident_bytes == 120
+    made = c.get_or_create(4, lambda: ('d', 30, 'cuda:1'))  # create() may name its device
+    assert made == 'd' and c.device_bytes('cuda:1') == 90 and 2 in c
+
+
+def test_limit_zero_keeps_the_last_shard_per_device():
+    c = DecodedShardCache(0)
+    with pytest.warns(UserWarning):
+        c.put(1, 'a', 10, device='cuda:0')
+    c.put(2, 'b', 10, device='cuda:0')
+    c.put(3, 'c', 10, device='cuda:1')
+    assert list(c._entries) == [2, 3]
+
+
+@pytest.mark.parametrize('how', ['clear', 'discard'])
+def test_clear_or_discard_cancels_a_decode_in_flight(how):
+    """A decode running while clear() / discard(key) runs is handed to its waiters but not
+    inserted: clear() leaves the cache empty."""
+    c = DecodedShardCache(1 << 20)
+    started, release = threading.Event(), threading.Event()
+
+    def create():
+        started.set()
+        release.wait(5)
+        return 'v', 10
+
+    got = []
+    t = threading.Thread(target=lambda: got.append(c.get_or_create(1, create)))
+    t.start()
+    started.wait(5)
+    waiter = threading.Thread(target=lambda: got.append(c.get_or_create(1, lambda: ('x', 1))))
+    waiter.start()
+    time.sleep(0.05)
+    c.clear() if how == 'clear' else c.discard(1)
+    release.set()
+    t.join(5)
+    waiter.join(5)
+    assert got == ['v', 'v']
+    assert len(c) == 0 and c.resident_bytes == 0
+    assert c.get_or_create(1, lambda: ('w', 5)) == 'w' and 1 in c  # a later touch decodes again

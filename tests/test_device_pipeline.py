@@ -165,3 +165,107 @@ def test_pipeline_validate_hash(name, algo):
         for _ in pipe:
             pass
     pipe.close()
+
+
+def _config_e_files(tmp, cfg):
+    """Full-size config E: 64 MiB shards written with compression='zstd'
+    (level 3, stream.py:319-351 / compression.py:243-258 decompress them); B-compressible
+    (small integers as float32) or config C. Two full shards and a partial one."""
+    from streaming_amd.compression import compress
+    from streaming_amd.pipeline import ShardFile
+    from streaming_amd.synth import config_b_samples_per_shard, var_c_shards
+    from streaming_amd.writer import encode_fixed_shard, shard_config_bytes
+    rng = np.random.default_rng(11)
+    if cfg == 'B':
+        names, encs, sizes = ['id', 'x'], ['int32', 'ndarray:float32:1024'], [4, 4096]
+        config = shard_config_bytes(names, encs, sizes, 'zstd', [], 1 << 26)
+        per = config_b_samples_per_shard()
+        counts = [per, per, 1234]
+        total = sum(counts)
+        x = rng.integers(0, 256, (total, 1024)).astype(np.float32)
+        first = np.concatenate([[0], np.cumsum(counts)])
+        raws = [encode_fixed_shard(config, [np.arange(a, b, dtype=np.int32), x[a:b]])
+                for a, b in zip(first[:-1], first[1:])]
+        src = {'x': x}
+    else:
+        names, encs, sizes = ['b', 'n', 's'], ['bytes', 'int', 'str'], [None, 8, None]
+        raws, counts, src = var_c_shards(34000, seed=12)
+        assert len(counts) == 3 and max(len(r) for r in raws[:2]) > 60 << 20
+    files = []
+    for i, (raw, n) in enumerate(zip(raws, counts)):
+        path = os.path.join(tmp, f'shard.{i:05}.mds.zstd')
+        with open(path, 'wb') as f:
+            f.write(compress('zstd', raw))
+        files.append(ShardFile(path, len(raw), n, 'zstd', {}))
+    return Plan(names, encs, sizes), files, counts, src
+
+
+def _check_e_host(cfg, host, src, r0, r1):
+    if cfg == 'B':
+        assert np.array_equal(host['id'], np.arange(r0, r1, dtype=np.int32))
+        assert np.array_equal(host['x'].view(np.uint32), src['x'][r0:r1].view(np.uint32))
+        return
+    assert np.array_equal(host['n'], src['n'][r0:r1])
+    for name in ('b', 's'):
+        lens = src[name + '_len']
+        off = np.concatenate([[0], np.cumsum(lens)])
+        vals, offs = host[name][0], host[name][1]
+        assert np.array_equal(offs, off[r0:r1 + 1] - off[r0])
+        assert np.array_equal(vals, src[name + '_pool'][off[r0]:off[r1]])
+    assert not host['s'][2].any()
+
+
+def _check_e_device(cfg, out, src, r0, r1):
+    """The device hand-off compared on the device, against the sources uploaded."""
+    dev = out.columns[next(iter(out.columns))]
+    dev = (dev.offsets if isinstance(dev, RaggedColumn) else dev).device
+
+    def same(got, exp):
+        exp = torch.from_numpy(np.ascontiguousarray(exp)).to(dev)
+        assert got.shape == exp.shape and torch.equal(got, exp)
+
+    if cfg == 'B':
+        same(out['id'], np.arange(r0, r1, dtype=np.int32))
+        same(out['x'].view(torch.int32), src['x'][r0:r1].view(np.int32))
+        return
+    same(out['n'], src['n'][r0:r1])
+    for name in ('b', 's'):
+        off = np.concatenate([[0], np.cumsum(src[name + '_len'])])
+        same(out[name].offsets, off[r0:r1 + 1] - off[r0])
+        same(out[name].values, src[name + '_pool'][off[r0]:off[r1]])
+    assert not bool(out['s'].flags.any())
+
+
+@pytest.fixture(scope='module', params=['B', 'C'])
+def config_e(request, tmp_path_factory):
+    tmp = tmp_path_factory.mktemp(f'config_e_{request.param}')
+    return (request.param, ) + _config_e_files(str(tmp), request.param)
+
+
+@pytest.mark.parametrize('handoff,per,depth', [('device', 1, 2), ('device', 2, 2),
+                                               ('iter_host', 1, 2), ('iter_host', 1, 3),
+                                               ('to_host', 2, 1)])
+def test_pipeline_full_size_config_e(config_e, handoff, per, depth):
+    """Full 64 MiB zstd shards (config E) through host decompress -> pinned -> H2D -> device
+    decode, bit-exact against the columns the shards were written from, with the device
+    hand-off, the overlapped host hand-off (iter_host) and a blocking to_host."""
+    cfg, plan, files, counts, src = config_e
+    pipe = ShardPipeline(plan, files, shards_per_batch=per, depth=depth, workers=4)
+    first = np.concatenate([[0], np.cumsum(counts)])
+    if handoff == 'iter_host':
+        outs = pipe.iter_host()
+    elif handoff == 'to_host':
+        outs = (to_host(b) for b in pipe)
+    else:
+        outs = iter(pipe)
+    n = 0
+    for gi, out in enumerate(outs):
+        s0 = gi * per
+        s1 = min(s0 + per, len(files))
+        if handoff == 'device':
+            _check_e_device(cfg, out, src, int(first[s0]), int(first[s1]))
+        else:
+            _check_e_host(cfg, out, src, int(first[s0]), int(first[s1]))
+        n += 1
+    pipe.close()
+    assert n == len(pipe.groups)

@@ -80,3 +80,35 @@ def test_device_iter_reprepares_an_evicted_shard(tmp_path):
     ds.shards[0].evict()  # gone before the first batch needs it
     numbers, _, _ = _rows(device_iter(standin, 16))
     assert len(numbers) == 10_000 and 0 in standin.prepared
+
+
+@pytest.mark.parametrize('name,rank', [('py1e_r1w2', 0), ('noshuffle_r1w3', 0), ('py1s_r2w2', 0),
+                                       ('py1s_r2w2', 1)])
+def test_device_iter_multi_worker_loader(name, rank):
+    """device_iter(num_workers=W): the W worker partitions gathered on the GPU and interleaved as
+    torch's DataLoader returns them give, on each rank, the samples and batch sizes the REAL
+    reference's StreamingDataLoader(num_workers=W) yielded (tests/golden/order/loader.json), and
+    DeviceBatches checkpoints (this rank's count times the ranks) and resumes as it does."""
+    from tests.test_plugin_iter import _standin, loader_settings
+    st = loader_settings()[name]
+    pr = st['per_rank'][rank]
+    bs, W = st['kwargs']['batch_size'], st['workers']
+    ds = LocalDataset(gu.GOLDEN + '/config_a', decoded_cache_bytes=1 << 20)
+    standin = _standin(name, rank, ds.shards)
+    numbers, words, sizes = _rows(device_iter(standin, bs, num_workers=W))
+    assert sizes == pr['start_batch_sizes']
+    assert digest(numbers, words) == pr['iter_start_sha256']
+    standin = _standin(name, rank, ds.shards)
+    loader = DeviceBatches(standin, bs, num_workers=W)
+    it = iter(loader)
+    for _ in range(st['resume_batches']):
+        next(it)
+    state = loader.state_dict()
+    assert state['sample_in_epoch'] == st['state_dict']['sample_in_epoch']
+    standin._iterator.exit()
+    standin = _standin(name, rank, ds.shards)
+    standin.load_state_dict(state)
+    numbers, words, sizes = _rows(device_iter(standin, bs, num_workers=W))
+    assert sizes == pr['resume_batch_sizes']
+    assert digest(numbers, words) == pr['iter_resume_sha256']
+    torch.cuda.synchronize()

@@ -44,3 +44,44 @@ def test_device_iter_follows_the_reference_iteration(tmp_path):
     out = json.loads(res.stdout.strip().splitlines()[-1])
     for name, r in out.items():
         assert all(r.values()), (name, r)
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _ranks(script, args):
+    port = _free_port()
+    procs = []
+    for rank in range(2):
+        env = dict(os.environ, PYTHONDONTWRITEBYTECODE='1', HIP_VISIBLE_DEVICES='',
+                   RANK=str(rank), WORLD_SIZE='2', LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE='2',
+                   MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script] + args, env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        out, err = p.communicate(timeout=600)
+        assert p.returncode == 0, err[-3000:]
+        outs.append(json.loads(out.strip().splitlines()[-1]))
+    return outs
+
+
+def test_device_iter_two_ranks_two_workers(tmp_path):
+    """Two ranks (RANK / WORLD_SIZE, gloo on 127.0.0.1), each device_iter(num_workers=2) over the
+    real StreamingDataset: each rank's samples equal what the reference's
+    StreamingDataLoader(num_workers=2) yielded on that rank, and DeviceBatches.state_dict (this
+    rank's count times the ranks, dataloader.py:74-84) checkpoints and resumes as the reference."""
+    import shutil
+    local = tmp_path / 'a'
+    shutil.copytree(os.path.join(HERE, 'golden', 'config_a'), local)
+    script = os.path.join(HERE, 'integration', 'device_iter_ranks_check.py')
+    start = _ranks(script, [REF, str(local), 'start'])
+    for r in start:
+        assert r['start'] and r['start_sizes'] and r['state_dict'], r
+    resumed = _ranks(script, [REF, str(local), 'resume', json.dumps(start[0]['state'])])
+    for r in resumed:
+        assert r['resume'] and r['resume_sizes'], r
