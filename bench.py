@@ -312,27 +312,36 @@ def committed_traffic(key, kernel):
     return None, None
 
 
+COPY_VARIANTS = (1, 3, 4, 5, 6)  # include/mdsx.h mdsx_copy_probe_variant shapes
+
+
 def copy_ceiling(batch, iters=10):
-    """Median rate of a read+write streaming copy of the batch's shard bytes (GB/s)."""
+    """The same-run copy ceiling: a read+write streaming copy of the batch's shard bytes in each
+    probe shape (include/mdsx.h), interleaved launch by launch; the fastest shape's median (GB/s)."""
     from streaming_amd import _native
     lib = _native.lib()
     src = batch.buffer
     dst = torch.empty_like(src)
     stream = torch.cuda.current_stream(src.device)
-    start = [torch.cuda.Event(enable_timing=True) for _ in range(iters + 1)]
-    end = [torch.cuda.Event(enable_timing=True) for _ in range(iters + 1)]
+    ev = {v: [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(iters + 1)] for v in COPY_VARIANTS}
     for i in range(iters + 1):
-        start[i].record(stream)
-        rc = lib.mdsx_copy_probe(src.data_ptr(), dst.data_ptr(), src.numel(), stream.cuda_stream)
-        end[i].record(stream)
-        if rc != 0:
-            raise RuntimeError(f'mdsx_copy_probe failed: {lib.mdsx_last_error().decode()}')
+        for v in COPY_VARIANTS:
+            ev[v][i][0].record(stream)
+            rc = lib.mdsx_copy_probe_variant(src.data_ptr(), dst.data_ptr(), src.numel(), v,
+                                             stream.cuda_stream)
+            ev[v][i][1].record(stream)
+            if rc != 0:
+                raise RuntimeError(f'mdsx_copy_probe failed: {lib.mdsx_last_error().decode()}')
     torch.cuda.synchronize(src.device)
     if not torch.equal(src[-4096:], dst[-4096:]):
         raise RuntimeError('mdsx_copy_probe: copy mismatch')
-    ms = float(np.median([start[i].elapsed_time(end[i]) for i in range(1, iters + 1)]))
+    ms = {v: float(np.median([a.elapsed_time(b) for a, b in ev[v][1:]])) for v in COPY_VARIANTS}
+    best = min(ms, key=ms.get)
     del dst
-    return {'GBps': 2 * src.numel() / ms / 1e6, 'ms': ms, 'bytes_per_launch': 2 * src.numel()}
+    return {'GBps': 2 * src.numel() / ms[best] / 1e6, 'ms': ms[best], 'variant': best,
+            'GBps_by_variant': {str(v): 2 * src.numel() / t / 1e6 for v, t in ms.items()},
+            'bytes_per_launch': 2 * src.numel()}
 
 
 def measure(args, config, world, rank, dev, tmpdir):
@@ -417,6 +426,7 @@ def measure(args, config, world, rank, dev, tmpdir):
             'scan_ms': float(np.mean(scan_ms)),
             'step_frac': (R + W) / step_s / 1e9 / HBM_PEAK_GBS,
             'frac_of_measured_copy': achieved / COPY_MEASURED_GBS,
+            'frac_of_same_run_copy': achieved / copy['GBps'] if copy else None,
             'copy_ceiling_same_run': copy,
         },
         'cpu_baseline': None,

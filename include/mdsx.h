@@ -330,14 +330,17 @@ int mdsx_copy_probe(const void* d_src, void* d_dst, uint64_t bytes, void* stream
 /* The probe's shapes, for measurement: 0 a 256 KiB loop per workgroup (8 loads per lane in
  * flight, non-temporal); 1 one 4 KiB piece per wave, non-temporal loads and stores (the shape of
  * the config-B row copy; what mdsx_copy_probe runs); 2 as 1 with plain loads; 3 as 1 with 8 KiB
- * per wave; 4 as 1 with plain loads and stores. */
+ * per wave; 4 as 1 with plain loads and stores; 5 as 1 and 6 as 3 with the workgroups dealt
+ * to the 8 XCDs in contiguous ranges (the register decode's tile order). The bench reports the
+ * fastest variant of its run as the same-run copy ceiling. */
 int mdsx_copy_probe_variant(const void* d_src, void* d_dst, uint64_t bytes, int variant,
                             void* stream);
-/* Host hand-off copy: the same 16-byte streaming kernel storing into PINNED host memory (a
+/* Host hand-off copy: a 16-byte streaming kernel storing into PINNED host memory (a
  * device-accessible host pointer) over PCIe, `bytes` a multiple of 16, both pointers 16-byte
- * aligned. A DMA-engine D2H and H2D do not overlap on this platform (they serialise, measured);
- * this copy runs beside a DMA-engine H2D at ~43 GB/s each way (scripts/pcie_duplex.py), so a
- * decoded batch goes to the host while the next batch's shards come in. */
+ * aligned; at most 64 workgroups striding over the bytes, so the CUs stay free for the next
+ * batch's decode and H2D copy. A DMA-engine D2H and H2D do not overlap on this platform (they
+ * serialise, measured); this copy runs beside the H2D (scripts/pcie_duplex.py), so a decoded
+ * batch goes to the host while the next batch's shards come in. */
 int mdsx_copy_to_host(const void* d_src, void* h_dst, uint64_t bytes, void* stream);
 
 #ifdef __cplusplus

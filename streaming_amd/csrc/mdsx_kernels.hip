@@ -913,10 +913,13 @@ __global__ __launch_bounds__(kBlock) void copy_probe_kernel(const uint4* __restr
 // The same stream cut per wave: each wave copies its own contiguous kU x 1 KiB (64 lanes x 16 B,
 // kU loads per lane in flight, then kU stores) -- the access shape of the config-B decode's row
 // copy (one 4 KiB row per wave), which outruns the 256 KiB-per-workgroup loop above on MI355X.
-template <int kU, bool kNTLoad, bool kNTStore>
+// kXcd: workgroups dealt to the 8 XCDs in contiguous ranges (xcd_block), the tile order of the
+// register decode (config B) -- the line two neighbouring workgroups share meets in one L2.
+template <int kU, bool kNTLoad, bool kNTStore, bool kXcd = false>
 __global__ __launch_bounds__(kBlock) void copy_wave_kernel(const uint4* __restrict__ src,
                                                            uint4* __restrict__ dst, uint64_t n) {
-  const uint64_t w = uint64_t(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+  const uint32_t blk = kXcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint64_t w = uint64_t(blk) * (kBlock / 64) + (threadIdx.x >> 6);
   const uint64_t b0 = w * (64 * kU) + (threadIdx.x & 63);
   uint4 v[kU];
 #pragma unroll
@@ -1607,14 +1610,46 @@ int mdsx_copy_probe_variant(const void* d_src, void* d_dst, uint64_t bytes, int 
       hipLaunchKernelGGL((copy_wave_kernel<4, false, false>),
                          dim3(unsigned((n + per4 - 1) / per4)), dim3(kBlock), 0, s, src, dst, n);
       break;
+    case 5:
+      hipLaunchKernelGGL((copy_wave_kernel<4, true, true, true>),
+                         dim3(unsigned((n + per4 - 1) / per4)), dim3(kBlock), 0, s, src, dst, n);
+      break;
+    case 6:
+      hipLaunchKernelGGL((copy_wave_kernel<8, true, true, true>),
+                         dim3(unsigned((n + per8 - 1) / per8)), dim3(kBlock), 0, s, src, dst, n);
+      break;
     default:
-      return mdsx::fail(MDSX_E_ARG, "mdsx_copy_probe_variant: variant 0..4");
+      return mdsx::fail(MDSX_E_ARG, "mdsx_copy_probe_variant: variant 0..6");
   }
   return hip_check(hipGetLastError(), "copy probe launch");
 }
 
 int mdsx_copy_probe(const void* d_src, void* d_dst, uint64_t bytes, void* stream) {
   return mdsx_copy_probe_variant(d_src, d_dst, bytes, 1, stream);
+}
+
+// The host hand-off copy: a FEW workgroups striding over the bytes (8 x 16 B per lane in flight,
+// non-temporal), enough for PCIe (~57 GB/s x a few us of latency = well under 1 MiB in flight)
+// while leaving the CUs to the next batch's decode and to a blit-kernel H2D copy on another
+// stream. (A grid covering the whole buffer -- 2048 workgroups for a 512 MiB batch, all resident
+// for the ~10 ms of the transfer -- kept a concurrent H2D copy from starting until it ended.)
+constexpr unsigned kToHostGrid = 64;
+__global__ __launch_bounds__(kBlock) void copy_to_host_kernel(const uint4* __restrict__ src,
+                                                              uint4* __restrict__ dst, uint64_t n) {
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock * 8;
+  for (uint64_t base = uint64_t(blockIdx.x) * kBlock * 8; base < n; base += stride) {
+    uint4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint64_t i = base + u * kBlock + threadIdx.x;
+      if (i < n) v[u] = ld16<true>(src + i);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint64_t i = base + u * kBlock + threadIdx.x;
+      if (i < n) st16<true>(reinterpret_cast<uint64_t>(dst + i), v[u]);
+    }
+  }
 }
 
 int mdsx_copy_to_host(const void* d_src, void* h_dst, uint64_t bytes, void* stream) {
@@ -1624,11 +1659,12 @@ int mdsx_copy_to_host(const void* d_src, void* h_dst, uint64_t bytes, void* stre
                       "mdsx_copy_to_host: 16-byte aligned pointers and size required");
   const uint64_t n = bytes / 16;
   if (n == 0) return MDSX_OK;
-  const unsigned grid = unsigned((n + kProbeBlock - 1) / kProbeBlock);
-  hipLaunchKernelGGL(copy_probe_kernel, dim3(grid), dim3(kBlock), 0,
+  const uint64_t need = (n + uint64_t(kBlock) * 8 - 1) / (uint64_t(kBlock) * 8);
+  const unsigned grid = unsigned(std::min<uint64_t>(need, kToHostGrid));
+  hipLaunchKernelGGL(copy_to_host_kernel, dim3(grid), dim3(kBlock), 0,
                      static_cast<hipStream_t>(stream), static_cast<const uint4*>(d_src),
                      static_cast<uint4*>(h_dst), n);
-  return hip_check(hipGetLastError(), "copy_probe_kernel launch (to host)");
+  return hip_check(hipGetLastError(), "copy_to_host_kernel launch");
 }
 
 }  // extern "C"

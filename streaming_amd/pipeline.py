@@ -108,6 +108,7 @@ class _Slot:
         self.dev = torch.empty(total, dtype=torch.uint8, device=device)
         self.copied = torch.cuda.Event()
         self.decoded = torch.cuda.Event()
+        self.handed: Optional[torch.cuda.Event] = None  # iter_host: D2H of its outputs queued
         self.hasher = DeviceHasher(device)
         self.decoder: Optional[BatchDecoder] = None
         self.key: Optional[tuple] = None
@@ -120,7 +121,11 @@ class ShardPipeline:
         plan: the shards' schema (all shards of a pipeline share it).
         shards: shard files in order.
         shards_per_batch: shards decoded per device batch.
-        depth: staging/device slots in flight (2 = double buffering).
+        depth: staging/device slots in flight (2 = double buffering). Default: enough slots
+            for every worker thread to have a shard to read or decompress, ``ceil(workers /
+            shards_per_batch) + 1`` and at least 2 (a slot is refilled only after its H2D copy,
+            so with 16 threads and 8-shard batches two slots leave half the threads idle:
+            config E 18 GiB/s at depth 2, 23 at depth 3).
         workers: host threads reading / decompressing shards.
         device: CUDA device.
         validate_hash: check every shard against its index.json ``raw_data.hashes[algo]``
@@ -136,7 +141,7 @@ class ShardPipeline:
                  plan: Plan,
                  shards: Sequence[ShardFile],
                  shards_per_batch: int = 8,
-                 depth: int = 2,
+                 depth: Optional[int] = None,
                  workers: int = 8,
                  device: Union[str, torch.device, None] = None,
                  validate_hash: Optional[str] = None) -> None:
@@ -154,6 +159,8 @@ class ShardPipeline:
                         f'creation `{sorted((s.hashes or {}).keys())}`. Provide one of those.')
         self._device_hash = bool(validate_hash) and validate_hash in PIPELINE_DEVICE_HASHES
         self.per = max(1, shards_per_batch)
+        if depth is None:
+            depth = max(2, -(-max(1, workers) // self.per) + 1)
         self.depth = max(1, depth)
         dev = torch.device(device or 'cuda')
         if dev.index is None:
@@ -246,6 +253,9 @@ class ShardPipeline:
                 slot.decoder._abi = batch.abi()
                 if self.plan.num_var:
                     slot.decoder._sized = False  # ragged totals differ per batch: re-size
+            if slot.handed is not None:  # iter_host: this slot's last outputs are off the device
+                compute.wait_event(slot.handed)
+                slot.handed = None
             self._mark('decode_start', gi, compute)
             out = slot.decoder.run()
             slot.decoded.record(compute)
@@ -260,6 +270,7 @@ class ShardPipeline:
             # the next batches' reads and copies stay queued
             slot.decoder.check()
             self._mark('yield', gi)
+            self._current = slot
             yield out
 
     def iter_host(self) -> Iterator[dict[str, Union[np.ndarray, tuple]]]:
@@ -268,7 +279,8 @@ class ShardPipeline:
         in flight, and the next decode waits for it (the outputs it reads belong to the slot); a
         batch is handed out once its copy has landed. The D2H is a kernel storing into pinned
         memory (``mdsx_copy_to_host``): two DMA-engine copies in opposite directions serialise
-        on this platform, a kernel beside a DMA copy does not. ``depth=3`` measured best
+        on this platform, a kernel beside a DMA copy does not. Only the slot's next decode
+        (``depth`` batches later), which rewrites the outputs being copied, waits for the copy
         (DESIGN.md §7)."""
         compute = torch.cuda.current_stream(self.device)
         d2h = torch.cuda.Stream(self.device)
@@ -276,7 +288,7 @@ class ShardPipeline:
         for gi, out in enumerate(self):
             host, done = _to_host_async(out, d2h, compute, self._mark if self.trace is not None
                                         else None, gi)
-            compute.wait_event(done)  # the slot's outputs are reused by later decodes
+            self._current.handed = done  # the slot's outputs are reused by its next decode
             if prev is not None:
                 prev[1].synchronize()
                 self._mark('host_yield', gi - 1)
@@ -309,6 +321,7 @@ def _to_host_async(decoded: DecodedBatch, stream: torch.cuda.Stream,
             host = []
             for t in parts:
                 t = t.contiguous()
+                t.record_stream(stream)  # read on this stream (a kernel torch does not see)
                 h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
                 nbytes = t.numel() * t.element_size()
                 body = nbytes & ~15

@@ -8,6 +8,7 @@ import json
 import os
 import subprocess
 import sys
+import tempfile
 
 import pytest
 
@@ -16,6 +17,16 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 pytestmark = pytest.mark.skipif(not os.path.isdir(os.path.join(REF, 'streaming')),
                                 reason='the reference source tree is not present')
+
+
+@pytest.fixture(autouse=True)
+def _one_reference_run_at_a_time():
+    """The reference keeps its state in /dev/shm under global names, and its
+    clean_stale_shared_memory() removes every such segment: two of these tests running at once
+    (pytest-xdist workers) would pull each other's state away. One at a time, across processes."""
+    from filelock import FileLock
+    with FileLock(os.path.join(tempfile.gettempdir(), 'mdsx_reference_tests.lock')):
+        yield
 
 
 def test_streaming_dataset_with_device_stream(tmp_path):
@@ -63,10 +74,16 @@ def _ranks(script, args):
         procs.append(subprocess.Popen([sys.executable, script] + args, env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
     outs = []
-    for p in procs:
-        out, err = p.communicate(timeout=600)
-        assert p.returncode == 0, err[-3000:]
-        outs.append(json.loads(out.strip().splitlines()[-1]))
+    try:
+        for p in procs:
+            out, err = p.communicate(timeout=300)
+            assert p.returncode == 0, err[-3000:]
+            outs.append(json.loads(out.strip().splitlines()[-1]))
+    finally:
+        for p in procs:  # a rank left waiting for the other at a barrier
+            if p.poll() is None:
+                p.kill()
+                p.wait()
     return outs
 
 
