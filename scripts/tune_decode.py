@@ -32,6 +32,15 @@ def retile(batch: DeviceBatch, plan: Plan) -> DeviceBatch:
                        batch.samples, row0, tiles, rows, tr)
 
 
+def src_abs_offset(nvar: int, ntiles: int, nbytes: int) -> int:
+    """Workspace byte offset of the src_abs region (mdsx_kernels.hip workspace_layout)."""
+    r256 = lambda x: (x + 255) // 256 * 256  # noqa: E731
+    tile_prefix = 256 + r256(nvar * ntiles * 8)
+    chunk_sum = tile_prefix + r256(nvar * ntiles * 8)
+    tile_run = chunk_sum + r256(nvar * (ntiles // (256 * 16) + 1) * 8)
+    return tile_run + r256(ntiles * 48 if nvar else 0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--config', default='B')
@@ -148,7 +157,19 @@ def main():
     phases = {}
     for v, dec in decs.items():  # sdbg bit 16: the staged decode's cycles per phase, per tile
         dbg = [int(kv[5:], 0) for kv in v.split('#')[0].split(',') if kv.startswith('sdbg=')]
-        if dbg and dbg[0] & 16:
+        if dbg and dbg[0] & 64:  # the row-parallel decode's phase stamps (mdsx_rows.hip)
+            dec.run()
+            torch.cuda.synchronize()
+            ntile = int(dec.batch.tile_shard.numel())
+            off = src_abs_offset(dec.plan.num_var, ntile, int(dec.batch.buffer.numel()))
+            raw = dec.workspace[off:off + 32 * ntile].cpu().view(torch.int64).view(ntile, 4)
+            med = raw.double().median(dim=0).values.tolist()
+            phases[v] = dict(zip(['dma_wait', 'geometry_scan_map', 'write', 'flags'],
+                                 [round(x) for x in raw.double().mean(dim=0).tolist()]))
+            phases[v]['median'] = [round(x) for x in med]
+            phases[v]['tiles'] = ntile
+            phases[v]['rows_per_tile'] = dec.batch.tile_rows
+        elif dbg and dbg[0] & 16:
             dec.run()
             torch.cuda.synchronize()
             raw = dec.workspace[200:256].cpu().view(torch.int64).tolist()

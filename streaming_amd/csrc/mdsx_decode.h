@@ -82,6 +82,7 @@ struct DevArgs {
   uint32_t seg_lim;      // streaming decode, lean path: largest sample it takes (0: lean path off)
   uint32_t seg_small;    // lean path: bytes per row of the fixed columns of <= 16 bytes
   uint32_t xcd_order;    // kXcd* bits: decodes whose workgroups take XCD-contiguous tile ranges
+  uint32_t rows_pipe;    // row-parallel decode: tiles per workgroup through two stages (0: one)
   uint32_t gather_block0[MDSX_MAX_COLUMNS + 1];  // first gather workgroup of each ragged column
   DevCol cols[MDSX_MAX_COLUMNS];
 };
@@ -131,7 +132,18 @@ __device__ __forceinline__ int sample_range(const TileView& v, uint32_t i, uint3
   return MDSX_OK;
 }
 
-// Exclusive scan over the 256 threads of the block; *total gets the block sum.
+// A workgroup barrier for kernels whose waves exchange data through LDS only: the wave's LDS
+// operations done, then s_barrier. __syncthreads()'s release fence also waits for every
+// vector-memory operation of the wave (vmcnt(0)): its global stores acknowledged and any LDS-DMA
+// load landed -- store latency on every barrier (measured in the row-parallel decode's phases)
+// and no DMA left in flight across it.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Exclusive scan over the 256 threads of the block; *total gets the block sum. kRaw: LDS-only
+// barriers (lds_barrier).
+template <bool kRaw = false>
 __device__ __forceinline__ int64_t block_exclusive_scan(int64_t x, int64_t* s_wsum,
                                                         int64_t* total) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -142,7 +154,8 @@ __device__ __forceinline__ int64_t block_exclusive_scan(int64_t x, int64_t* s_ws
     if (lane >= o) incl += y;
   }
   if (lane == 63) s_wsum[w] = incl;
-  __syncthreads();
+  if constexpr (kRaw) lds_barrier();
+  else __syncthreads();
   int64_t base = 0, tot = 0;
 #pragma unroll
   for (int k = 0; k < kBlock / 64; ++k) {
@@ -150,7 +163,8 @@ __device__ __forceinline__ int64_t block_exclusive_scan(int64_t x, int64_t* s_ws
     base += (k < w) ? s : 0;
     tot += s;
   }
-  __syncthreads();
+  if constexpr (kRaw) lds_barrier();
+  else __syncthreads();
   *total = tot;
   return base + incl - x;
 }

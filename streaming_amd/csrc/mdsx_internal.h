@@ -61,6 +61,13 @@ struct mdsx_plan {
   int rows_kb = 0;         // row-parallel decode of shorter samples: LDS stage in KiB (0: off,
                            // -1: sized per batch, rows_tile_rows / rows_stage_bytes)
   int rows_nt = 1;         // row-parallel decode: non-temporal loads and stores (measured faster)
+  int rows_slack = 8;      // row-parallel decode: the stage holds (1 + 1/rows_slack) x a tile's
+                           // average bytes (+ 1 KiB)
+  int rows_occ = 0;        // row-parallel decode: waves per SIMD its registers are bounded for
+                           // (4, 6 or 8; 0: 6 for stages up to 24 KiB -- short samples, +7 % --
+                           // else 4)
+  int rows_pipe = 0;       // row-parallel decode: tiles per workgroup, the next tile's DMA in
+                           // flight while one is written (two stages; 0: one tile, one stage)
   int gather_chunks = 2;  // 16-byte chunks per lane in the ragged gather (tile = 4 KiB x this)
   int gather_min = 256;   // ragged columns averaging fewer bytes per row use the gather kernel
   int group_max = 1024;   // ... fewer than this (and >= gather_min): four rows per wave
@@ -86,14 +93,15 @@ inline bool use_rows_decode(const mdsx_plan* p, uint64_t bytes, uint64_t rows) {
 // Row-parallel decode sizing. A workgroup's LDS: the stage, [ncols][tile rows] 16-byte value
 // records, UTF-8 marks, one chunk map per ragged column, and the kernel's static arrays.
 inline uint64_t rows_lds_bytes_est(const mdsx_plan* p, uint64_t stage, uint64_t tr) {
-  return 192 + stage + tr * uint64_t(p->ncols) * 16 + uint64_t(p->ncols) * 32 +
-         uint64_t(p->nvar) * (stage / 16 + 4) + 4352;
+  const uint64_t nstage = p->rows_pipe > 0 ? 2 : 1;
+  return 192 * nstage + stage * nstage + tr * uint64_t(p->ncols) * 16 + uint64_t(p->ncols) * 32 +
+         uint64_t(p->nvar) * (stage / 16 + 4) + uint64_t(p->ncols) * 64 + 64;
 }
 
-// The stage a tile of tr samples of per_row bytes needs: 9/8 of its average bytes plus 1 KiB
-// (4..96 KiB; a tile that does not fit is decoded in windows).
-inline uint64_t rows_auto_stage(uint64_t per_row, uint64_t tr) {
-  const uint64_t kb = (tr * per_row * 9 / 8 + 1023) / 1024 + 1;
+// The stage a tile of tr samples of per_row bytes needs: (1 + 1/slack) of its average bytes plus
+// 1 KiB (4..96 KiB; a tile that does not fit is decoded in windows). slack 8 by default.
+inline uint64_t rows_auto_stage(uint64_t per_row, uint64_t tr, uint64_t slack = 8) {
+  const uint64_t kb = (tr * per_row * (slack + 1) / slack + 1023) / 1024 + 1;
   return (kb < 4 ? 4 : kb > 96 ? 96 : kb) * 1024;
 }
 
@@ -108,7 +116,7 @@ inline int rows_tile_rows(const mdsx_plan* p, uint64_t per_row) {
   int tr = 1;
   while (tr < 256) {
     const uint64_t t2 = uint64_t(tr) * 2;
-    const uint64_t stage = p->rows_kb > 0 ? target : rows_auto_stage(per_row, t2);
+    const uint64_t stage = p->rows_kb > 0 ? target : rows_auto_stage(per_row, t2, p->rows_slack);
     if (t2 * per_row * 9 > target * 8 || rows_lds_bytes_est(p, stage, t2) > 160 * 1024) break;
     tr = int(t2);
   }
@@ -118,5 +126,6 @@ inline int rows_tile_rows(const mdsx_plan* p, uint64_t per_row) {
 // The stage of a batch decoded in tiles of tr rows.
 inline uint32_t rows_stage_bytes(const mdsx_plan* p, uint64_t per_row, int tr) {
   return p->rows_kb > 0 ? uint32_t(p->rows_kb) * 1024u
-                        : uint32_t(rows_auto_stage(per_row ? per_row : 1, uint64_t(tr)));
+                        : uint32_t(rows_auto_stage(per_row ? per_row : 1, uint64_t(tr),
+                                                   uint64_t(p->rows_slack)));
 }

@@ -822,6 +822,7 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   // decode)
   if (a->rows_bytes && rows_lds_bytes_est(plan, a->rows_bytes, uint64_t(tr)) > 160 * 1024)
     a->rows_bytes = 0;
+  a->rows_pipe = a->rows_bytes ? uint32_t(plan->rows_pipe) : 0u;
   if (a->run_slots && tr > 32)
     return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode tiles hold at most 32 rows");
   // the staged and streaming decodes scan one total per tile; the register-copy decode one per

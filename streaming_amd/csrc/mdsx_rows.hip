@@ -37,6 +37,7 @@
 #include "mdsx_decode.h"
 #include "mdsx_device.h"
 #include "mdsx_internal.h"
+#include "mdsx_ring.h"
 
 namespace mdsx_kernels {
 namespace {
@@ -66,10 +67,55 @@ __host__ __device__ __forceinline__ uint32_t rows_map_len(uint32_t cap) { return
 // byte of the value inside the window's output, stage byte, length), the UTF-8 marks ([ncols]
 // [8] bits, one per sample) and the chunk maps ([nvar][map_len]: the sample holding the first
 // window byte of each output chunk).
+// (then, 16-byte aligned, the per-column workgroup state: column table, next output byte,
+// window base and length, skip flag -- sized by ncols, so a narrow schema leaves room for more
+// workgroups per CU)
+__host__ __device__ __forceinline__ size_t rows_lds_tables(uint32_t cap, int TR, int ncols,
+                                                           int nvar, int nstage) {
+  return size_t(nstage) * (kStageFront + size_t(cap) + kStageSlack) +
+         size_t(TR) * size_t(ncols) * 16 + size_t(ncols) * 32 + size_t(nvar) * rows_map_len(cap);
+}
+__host__ __device__ __forceinline__ size_t rows_lds_colstate(int ncols) {
+  return size_t(ncols) * (sizeof(DevCol) + 8 + 8 + 4 + 4);
+}
 __host__ __device__ __forceinline__ size_t rows_lds_bytes(uint32_t cap, int TR, int ncols,
-                                                          int nvar) {
-  return kStageFront + size_t(cap) + kStageSlack + size_t(TR) * size_t(ncols) * 16 +
-         size_t(ncols) * 32 + size_t(nvar) * rows_map_len(cap);
+                                                          int nvar, int nstage = 1) {
+  return ((rows_lds_tables(cap, TR, ncols, nvar, nstage) + 15) & ~size_t(15)) +
+         rows_lds_colstate(ncols);
+}
+
+template <bool kFence>
+__device__ __forceinline__ void rows_barrier() {
+  if constexpr (kFence) __syncthreads();
+  else lds_barrier();
+}
+
+// Measurement only (MDSX_TUNE sdbg bit 64): shader-clock time of each phase of a tile (DMA wait,
+// column geometry + scan + chunk maps, column writes, flags), written by thread 0 of each tile's
+// workgroup to src_abs[4 tile + k] (the huge-row list's space; plain stores, no shared counter).
+__device__ __forceinline__ uint64_t shader_clock() {
+  uint64_t c;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(c)::"memory");
+  return c;
+}
+__device__ __forceinline__ void prof_mark(const DevArgs& a, uint32_t tile, int k, uint64_t& ts) {
+  const uint64_t now = shader_clock();
+  if (threadIdx.x == 0) a.src_abs[4ull * tile + k] = now - ts;
+  ts = now;
+}
+
+// The DMA of a clean run's bytes (its TileRun, stage_totals_kernel) into a stage: the range
+// started on a 128-byte line, 1 KiB per wave-instruction, the waves taking turns.
+template <bool kNT>
+__device__ __forceinline__ void rows_dma(const DevArgs& a, const TileRun& run, uint32_t stage_lds,
+                                         int wave, int lane) {
+  const uint64_t lo_al = run.stream & ~uint64_t(127);
+  const uint32_t nq = uint32_t((run.stream + run.bytes - lo_al + 15) >> 4);
+  const uint4* src = reinterpret_cast<const uint4*>(a.batch + lo_al);
+  for (uint32_t kb = uint32_t(wave); kb * 64 < nq; kb += kRowsBlock / 64) {
+    const uint32_t k = kb * 64 + uint32_t(lane);
+    if (k < nq) glds16<kNT>(src + k, stage_lds + kb * 1024u);  // lanes past nq write nothing
+  }
 }
 
 // One value of the window: output byte inside the window's output of its column, bytes (0: a
@@ -86,36 +132,85 @@ struct RowsTab {
 
 // Launch bound 4 waves per SIMD: the same 96 VGPRs as at 5 (occupancy is set by the LDS stage),
 // scheduled 1.5 % faster on 32-256 and 256-1024-byte rows (two A/B runs); 6 spills (9 % slower).
-template <bool kNT>
-__global__ __launch_bounds__(kRowsBlock, 4) void rows_decode_kernel(const DevArgs a) {
+//
+// kPipe: the workgroup decodes a.rows_pipe consecutive tiles through two stages, the next clean
+// tile's DMA (and its offsets) issued once this tile's column geometry is done, so it lands while
+// this tile's columns are written; the barriers it crosses leave it in flight (lds_barrier).
+// kFence (measurement only, MDSX_TUNE sdbg bit 128): __syncthreads() barriers, as before
+// lds_barrier replaced them.
+// kOcc: waves per SIMD the registers are bounded for (6: at most 80 VGPRs, so that six
+// workgroups fit a CU where their LDS does).
+// kFlat: the write loop over all columns' chunks at once (else one loop per column; measurement
+// control, MDSX_TUNE sdbg bit 256).
+template <bool kNT, bool kPipe, bool kProf = false, bool kFence = false, int kOcc = 4,
+          bool kFlat = true>
+__global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const DevArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  __shared__ DevCol s_cols[MDSX_MAX_COLUMNS];
   __shared__ int64_t s_wsum[kRowsBlock / 64];
-  __shared__ uint64_t s_base[MDSX_MAX_COLUMNS];   // next output byte of each column (rel. data)
-  __shared__ uint64_t s_wbase[MDSX_MAX_COLUMNS];  // the window's first output byte (rel. data)
-  __shared__ uint32_t s_wlen[MDSX_MAX_COLUMNS];   // the window's output bytes
-  __shared__ uint32_t s_skip[MDSX_MAX_COLUMNS];   // the tile's bytes exceed the column capacity
   __shared__ uint32_t s_gb, s_lo, s_hi;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  for (int c = t; c < a.ncols; c += kRowsBlock) s_cols[c] = a.cols[c];
-  const MDSX_L DevCol* cols = (const MDSX_L DevCol*)s_cols;
-  const uint32_t tile = (a.xcd_order & kXcdRows) ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint32_t blk = (a.xcd_order & kXcdRows) ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
   const int TR = a.tile_rows;
   const int ncols = a.ncols, nvar = a.nvar;
   const uint32_t cap = a.rows_bytes;
   const uint32_t map_len = rows_map_len(cap);
-  const lds_u8* stage = (const lds_u8*)(smem + kStageFront);
+  const uint32_t stage_stride = kStageFront + cap + kStageSlack;  // (16-byte multiple)
+  constexpr int kStages = kPipe ? 2 : 1;
   RowsTab T;
-  T.rec = (MDSX_L RowsRec*)(smem + kStageFront + cap + kStageSlack);
+  T.rec = (MDSX_L RowsRec*)(smem + kStages * stage_stride);
   T.bad = (MDSX_L uint32_t*)(T.rec + size_t(ncols) * TR);
   T.map = (MDSX_L uint8_t*)(T.bad + size_t(ncols) * 8);
-  const uint32_t stage_lds = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(
+  // the per-column workgroup state (rows_lds_colstate)
+  MDSX_L uint8_t* cs = (MDSX_L uint8_t*)(
+      smem + ((rows_lds_tables(cap, TR, ncols, nvar, kStages) + 15) & ~size_t(15)));
+  MDSX_L DevCol* s_cols = (MDSX_L DevCol*)cs;
+  MDSX_L uint64_t* s_base = (MDSX_L uint64_t*)(s_cols + ncols);  // next output byte (rel. data)
+  MDSX_L uint64_t* s_wbase = s_base + ncols;  // the window's first output byte (rel. data)
+  MDSX_L uint32_t* s_wlen = (MDSX_L uint32_t*)(s_wbase + ncols);  // the window's output bytes
+  MDSX_L uint32_t* s_skip = s_wlen + ncols;  // the tile's bytes exceed the column capacity
+  for (int c = t; c < ncols; c += kRowsBlock) s_cols[c] = a.cols[c];
+  const MDSX_L DevCol* cols = s_cols;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(
       reinterpret_cast<uintptr_t>((const MDSX_L uint8_t*)(smem + kStageFront))));
+  const uint32_t per = kPipe ? a.rows_pipe : 1u;
+  const uint32_t first = blk * per;
+  const uint32_t last = kPipe ? min(first + per, a.ntiles) : first + 1u;
+  auto fits = [&](const TileRun& r) { return r.fast && (r.stream & 127) + r.bytes <= cap; };
+  // kPipe: whether the current tile's bytes and offsets are already on their way (prefetched)
+  bool pre = false;
+  uint32_t pb = 0, pe = 0;  // its offsets pair (this thread's sample)
+  if constexpr (kPipe) {
+    const TileRun r0_ = a.tile_run[first];
+    if (fits(r0_)) {
+      rows_dma<kNT>(a, r0_, lds0, wave, lane);
+      if (t < int(r0_.nrows)) {
+        const uint32_t* o = reinterpret_cast<const uint32_t*>(a.batch + r0_.offs);
+        pb = o[t];
+        pe = o[t + 1];
+      }
+      pre = true;
+    }
+  }
+
+  const uint32_t count = kPipe ? last - first : 1u;  // (1: the loop folds away)
+  for (uint32_t it = 0; it < count; ++it) {  // block-uniform
+  const uint32_t tile = first + it;
+  const uint32_t sbuf = kPipe ? it & 1u : 0u;
+  const lds_u8* stage = (const lds_u8*)(smem + kStageFront + sbuf * stage_stride);
+  const uint32_t stage_lds = lds0 + sbuf * stage_stride;
+  if (kPipe && it != 0) {
+    // the previous tile's readers of the tables are done (its end barrier); its stores, this
+    // tile's DMA and offsets retire here
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    rows_barrier<kFence>();
+  }
   for (int i = t; i < ncols * 8; i += kRowsBlock) T.bad[i] = 0;
+  constexpr bool prof = kProf;
+  uint64_t ts = prof ? shader_clock() : 0;
 
   // ---- the tile: its run record (scan pass) or its shard's view
   const TileRun run = a.tile_run[tile];
-  const bool fast = run.fast && (run.stream & 127) + run.bytes <= cap;  // block-uniform
+  const bool fast = fits(run);  // block-uniform
   const uint8_t* frame;  // b / e below are byte positions relative to frame
   int n;
   uint64_t row0;
@@ -129,22 +224,25 @@ __global__ __launch_bounds__(kRowsBlock, 4) void rows_decode_kernel(const DevArg
     shard_idx = run.shard;
     r0 = run.r0;
     frame = a.batch + run.shard_off;
-    const uint64_t lo_al = run.stream & ~uint64_t(127);
-    const uint32_t nq = uint32_t((run.stream + run.bytes - lo_al + 15) >> 4);
-    const uint4* src = reinterpret_cast<const uint4*>(a.batch + lo_al);
-    for (uint32_t kb = uint32_t(wave); kb * 64 < nq; kb += kRowsBlock / 64) {
-      const uint32_t k = kb * 64 + uint32_t(lane);
-      if (k < nq) glds16<kNT>(src + k, stage_lds + kb * 1024u);  // lanes past nq write nothing
+    if (kPipe && pre) {
+      b = pb;
+      e = pe;
+    } else {
+      rows_dma<kNT>(a, run, stage_lds, wave, lane);
+      if (t < n) {
+        const uint32_t* o = reinterpret_cast<const uint32_t*>(a.batch + run.offs);
+        b = o[t];
+        e = o[t + 1];
+      }
     }
-    if (t < n) {
-      const uint32_t* o = reinterpret_cast<const uint32_t*>(a.batch + run.offs);
-      b = o[t];
-      e = o[t + 1];
-      in_range = true;  // run.fast: every sample of the run passed the file checks
-    }
+    in_range = t < n;  // run.fast: every sample of the run passed the file checks
   } else {
     const TileView v = tile_view(a, tile);
-    if (!v.table_ok) return;  // block-uniform; reported by the scan pass
+    if (!v.table_ok) {  // block-uniform; reported by the scan pass
+      if constexpr (!kPipe) return;
+      pre = false;  // (nothing was prefetched for the next tile either)
+      continue;
+    }
     n = int(v.nrows);
     row0 = v.d.row0 + v.r0;
     shard_idx = v.shard_idx;
@@ -180,21 +278,21 @@ __global__ __launch_bounds__(kRowsBlock, 4) void rows_decode_kernel(const DevArg
       lo_al = uint32_t((run.stream & ~uint64_t(127)) - run.shard_off);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
-      __syncthreads();  // the previous window's readers of the stage and the tables are done
+      rows_barrier<kFence>();  // the previous window's readers of the stage and the tables are done
       if (t == 0) s_gb = uint32_t(n), s_lo = 0xffffffffu, s_hi = 0;
-      __syncthreads();
+      rows_barrier<kFence>();
       if (t >= ga && in_range) atomicMin(&s_lo, b);  // the window's first in-range byte
-      __syncthreads();
+      rows_barrier<kFence>();
       const uint32_t lo = s_lo;
       if (t >= ga && in_range && !(b >= lo && e - lo <= cap)) atomicMin(&s_gb, uint32_t(t));
-      __syncthreads();
+      rows_barrier<kFence>();
       gb = int(s_gb);
       direct = gb == ga;  // sample ga alone is larger than the stage: the huge-row kernel's
       if (direct) gb = ga + 1;
       lo_al = lo & ~127u;
       // ---- 1. the window's bytes [lo_al, hi) into LDS, hi the largest end of its samples
       if (t >= ga && t < gb && in_range) atomicMax(&s_hi, e);
-      __syncthreads();
+      rows_barrier<kFence>();
       const uint32_t hi = s_hi;
       if (!direct && lo != 0xffffffffu && hi > lo_al) {
         const uint32_t nq = (hi - lo_al + 15) >> 4;
@@ -206,7 +304,8 @@ __global__ __launch_bounds__(kRowsBlock, 4) void rows_decode_kernel(const DevArg
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     }
-    __syncthreads();
+    rows_barrier<kFence>();
+    if constexpr (prof) prof_mark(a, tile, 0, ts);
 
     // ---- 2. column boundaries of this thread's sample (mds/reader.py:111-125)
     const bool mine = t >= ga && t < gb;
@@ -257,9 +356,23 @@ __global__ __launch_bounds__(kRowsBlock, 4) void rows_decode_kernel(const DevArg
       const uint64_t len1 = mine ? T.rec[c1 * TR + t].len : 0u;
       const uint64_t len2 = (mine && pair) ? T.rec[c2 * TR + t].len : 0u;
       const uint64_t base1 = s_base[c1], base2 = pair ? s_base[c2] : 0;
-      int64_t total;
+      int64_t total, excl;
       // each half sums at most the window's bytes (< 2^32): no carry between the halves
-      const int64_t excl = block_exclusive_scan(int64_t(len1 | (len2 << 32)), s_wsum, &total);
+      const int64_t x = int64_t(len1 | (len2 << 32));
+      if (TR <= 64) {  // block-uniform: every sample of the tile is in wave 0 -- no barriers
+        int64_t incl = x;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int64_t y = __shfl_up(incl, o);
+          if (lane >= o) incl += y;
+        }
+        excl = incl - x;
+        total = int64_t((uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint64_t(incl) >> 32), 63)))
+                         << 32) |
+                        uint32_t(__builtin_amdgcn_readlane(int(incl), 63)));
+      } else {
+        excl = block_exclusive_scan<!kFence>(x, s_wsum, &total);
+      }
       for (int h = 0; h < (pair ? 2 : 1); ++h) {
         const int c = h ? c2 : c1;
         const MDSX_L DevCol& col = cols[c];
@@ -294,13 +407,64 @@ __global__ __launch_bounds__(kRowsBlock, 4) void rows_decode_kernel(const DevArg
       const uint32_t slot = atomicAdd(count, 1u);
       a.src_abs[slot] = (uint64_t(tile) << 32) | uint32_t(t);
     }
-    __syncthreads();
+    rows_barrier<kFence>();
+    if constexpr (prof) prof_mark(a, tile, 1, ts);
+    if constexpr (kPipe) {
+      // the next clean tile's bytes and offsets, into the other stage (last read by the tile
+      // before this one, whose readers passed this tile's first barrier), while this one's
+      // columns are written
+      if (gb == n) {
+        pre = false;
+        if (tile + 1 < last) {
+          const TileRun nx = a.tile_run[tile + 1];
+          if (fits(nx)) {
+            rows_dma<kNT>(a, nx, lds0 + (sbuf ^ 1u) * stage_stride, wave, lane);
+            if (t < int(nx.nrows)) {
+              const uint32_t* o = reinterpret_cast<const uint32_t*>(a.batch + nx.offs);
+              pb = o[t];
+              pe = o[t + 1];
+            }
+            pre = true;
+          }
+        }
+      }
+    }
 
     // ---- 4. every column, output-chunk-parallel, str pieces checked on the way
     if (!direct) {
-      for (int c = 0; c < ncols; ++c) {
+      // kFlat: the columns' output chunks as one index space -- consecutive threads take
+      // consecutive chunks across the column ends, so a tile's writes take the fewest rounds of
+      // the (latency-bound) chunk loop; lane c counts column c's chunks. Else a loop per column.
+      uint32_t cincl = 0, total = 0;
+      if constexpr (kFlat) {
+        uint32_t cn = 0;
+        if (lane < ncols && !s_skip[lane]) {
+          const uint64_t w = reinterpret_cast<uint64_t>(cols[lane].data) + s_wbase[lane];
+          cn = uint32_t(((w & 15) + s_wlen[lane] + 15) >> 4);
+        }
+        cincl = wave_incl_u32(cn, lane, ncols);
+        total = (a.stage_debug & 2) ? 0u : uint32_t(__builtin_amdgcn_readlane(int(cincl), ncols - 1));
+      }
+      for (int cl = 0; cl < (kFlat ? 1 : ncols); ++cl) {
+        if (!kFlat && s_skip[cl]) continue;  // block-uniform
+        const uint32_t kend = kFlat ? total
+                                    : (a.stage_debug & 2) ? 0u
+                                    : uint32_t(((((reinterpret_cast<uint64_t>(cols[cl].data) +
+                                                   s_wbase[cl]) & 15) + s_wlen[cl] + 15) >> 4));
+        for (uint32_t kg = uint32_t(t); kg < kend; kg += kRowsBlock) {
+        // the chunk's column c and its index k inside the column
+        int c = cl;
+        uint32_t c0 = 0;
+        if constexpr (kFlat) {
+          // uniform loop of scalar reads of the column ends (v_readlane ignores the exec mask;
+          // a lane shuffle would read the ends of lanes that left the loop as zeros)
+          for (int j = 0; j + 1 < ncols; ++j) {
+            const uint32_t e = uint32_t(__builtin_amdgcn_readlane(int(cincl), j));
+            if (kg >= e) c = j + 1, c0 = e;
+          }
+        }
+        const uint32_t k = kg - c0;
         const MDSX_L DevCol& col = cols[c];
-        if (s_skip[c]) continue;  // block-uniform
         const int base = c * TR;
         // (measurement only, MDSX_TUNE sdbg: 1 no UTF-8 check, 2 no copy, 16 no stores)
         const bool utf8 = col.kind == MDSX_KIND_STR && col.flags != nullptr && !(a.stage_debug & 1);
@@ -308,11 +472,10 @@ __global__ __launch_bounds__(kRowsBlock, 4) void rows_decode_kernel(const DevArg
         const uint32_t wlen = s_wlen[c];
         const uint64_t D0 = wout & ~uint64_t(15);
         const int32_t hd = int32_t(wout - D0);
-        const uint32_t nch = uint32_t((uint64_t(hd) + wlen + 15) >> 4);
         const uint32_t rb = col.var_index >= 0 ? 0u : col.row_bytes;
         const MDSX_L uint8_t* mp = T.map + size_t(col.var_index >= 0 ? col.var_index : 0) * map_len;
         MDSX_L uint32_t* bad = T.bad + c * 8;
-        for (uint32_t k = uint32_t(t); k < (a.stage_debug & 2 ? 0u : nch); k += kRowsBlock) {
+        {
           const int32_t P0 = int32_t(k * 16) - hd;  // window output byte of the chunk's byte 0
           int32_t pos = max(P0, 0);
           const int32_t end = min(P0 + 16, int32_t(wlen));
@@ -402,9 +565,11 @@ __global__ __launch_bounds__(kRowsBlock, 4) void rows_decode_kernel(const DevArg
           if (P0 >= 0 && P0 + 16 <= int32_t(wlen)) st16<kNT>(D, val);
           else store_bytes(D, val, uint32_t(max(P0, 0) - P0), uint32_t(end - P0));
         }
+        }
       }
-      __syncthreads();  // every piece's UTF-8 mark is in
+      rows_barrier<kFence>();  // every piece's UTF-8 mark is in (a next tile's DMA may be in flight)
     }
+    if constexpr (prof) prof_mark(a, tile, 2, ts);
     // ---- 5. flags (a sample listed for the huge-row kernel: set there when its value fails)
     if (mine) {
       for (int c = 0; c < ncols; ++c) {
@@ -413,8 +578,11 @@ __global__ __launch_bounds__(kRowsBlock, 4) void rows_decode_kernel(const DevArg
           *gp(col.flags + row0 + t) = uint8_t((T.bad[c * 8 + (t >> 5)] >> (t & 31)) & 1u);
       }
     }
+    if constexpr (prof) prof_mark(a, tile, 3, ts);
     ga = gb;
   }
+  if constexpr (kPipe) rows_barrier<kFence>();  // this tile's readers of the tables and its stage are done
+  }  // tile
 }
 
 }  // namespace
@@ -429,24 +597,85 @@ int launch_rows_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
                                     4, s),
                      "hipMemsetAsync");
   if (rc != MDSX_OK) return rc;
-  const size_t lds = rows_lds_bytes(a.rows_bytes, a.tile_rows, a.ncols, a.nvar);
+  const bool pipe = a.rows_pipe > 0;
+  const size_t lds = rows_lds_bytes(a.rows_bytes, a.tile_rows, a.ncols, a.nvar, pipe ? 2 : 1);
   if (lds > 160 * 1024)
     return mdsx::fail(MDSX_E_ARG, "mdsx: row-parallel decode stage and tables exceed 160 KiB of LDS");
   const bool nt = plan->rows_nt != 0;
-  const void* fn = nt ? reinterpret_cast<const void*>(rows_decode_kernel<true>)
-                      : reinterpret_cast<const void*>(rows_decode_kernel<false>);
-  if (lds > 64 * 1024) {
-    rc = hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)),
-                   "hipFuncSetAttribute");
-    if (rc != MDSX_OK) return rc;
+  const unsigned grid = pipe ? (a.ntiles + a.rows_pipe - 1) / a.rows_pipe : a.ntiles;
+  // registers bounded for six waves per SIMD where six workgroups' stages fit a CU (measured:
+  // +7 % on 32-256-byte samples, -1 % on 256-1024-byte ones)
+  const int occ = plan->rows_occ ? plan->rows_occ : (a.rows_bytes <= 24 * 1024 ? 6 : 4);
+#define MDSX_ROWS_CASE(NT, PIPE)                                                                \
+  if (nt == NT && pipe == PIPE) {                                                               \
+    if (lds > 64 * 1024) {                                                                      \
+      rc = hip_check(hipFuncSetAttribute(reinterpret_cast<const void*>(                         \
+                                             rows_decode_kernel<NT, PIPE>),                     \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)), \
+                     "hipFuncSetAttribute");                                                    \
+      if (rc != MDSX_OK) return rc;                                                             \
+    }                                                                                           \
+    mdsx::set_last_kernel("rows_decode_kernel<" #NT ", " #PIPE ">");                            \
+    hipLaunchKernelGGL((rows_decode_kernel<NT, PIPE>), dim3(grid), dim3(kRowsBlock), lds, s, a); \
   }
-  if (nt) {
-    mdsx::set_last_kernel("rows_decode_kernel<true>");
-    hipLaunchKernelGGL((rows_decode_kernel<true>), dim3(a.ntiles), dim3(kRowsBlock), lds, s, a);
+  if (a.stage_debug & 256) {  // measurement only: one write loop per column
+    if (lds > 64 * 1024) {
+      rc = hip_check(hipFuncSetAttribute(reinterpret_cast<const void*>(
+                                             rows_decode_kernel<true, false, false, false, 4, false>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)),
+                     "hipFuncSetAttribute");
+      if (rc != MDSX_OK) return rc;
+    }
+    mdsx::set_last_kernel("rows_decode_kernel<true, false, false, false, 4, false>");
+    hipLaunchKernelGGL((rows_decode_kernel<true, false, false, false, 4, false>), dim3(a.ntiles),
+                       dim3(kRowsBlock), lds, s, a);
+  } else if (a.stage_debug & 128) {  // measurement only: __syncthreads() barriers
+    if (lds > 64 * 1024) {
+      rc = hip_check(hipFuncSetAttribute(
+                         reinterpret_cast<const void*>(rows_decode_kernel<true, false, false, true>),
+                         hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)),
+                     "hipFuncSetAttribute");
+      if (rc != MDSX_OK) return rc;
+    }
+    mdsx::set_last_kernel("rows_decode_kernel<true, false, false, true>");
+    hipLaunchKernelGGL((rows_decode_kernel<true, false, false, true>), dim3(a.ntiles),
+                       dim3(kRowsBlock), lds, s, a);
+  } else if (a.stage_debug & 64) {  // measurement only: the phase stamps (src_abs)
+    if (lds > 64 * 1024) {
+      rc = hip_check(hipFuncSetAttribute(
+                         reinterpret_cast<const void*>(rows_decode_kernel<true, false, true>),
+                         hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)),
+                     "hipFuncSetAttribute");
+      if (rc != MDSX_OK) return rc;
+    }
+    mdsx::set_last_kernel("rows_decode_kernel<true, false, true>");
+    hipLaunchKernelGGL((rows_decode_kernel<true, false, true>), dim3(a.ntiles), dim3(kRowsBlock),
+                       lds, s, a);
+  } else if ((occ == 6 || occ == 8) && nt && !pipe) {
+    const void* fn = occ == 6
+                         ? reinterpret_cast<const void*>(rows_decode_kernel<true, false, false, false, 6>)
+                         : reinterpret_cast<const void*>(rows_decode_kernel<true, false, false, false, 8>);
+    if (lds > 64 * 1024) {
+      rc = hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)),
+                     "hipFuncSetAttribute");
+      if (rc != MDSX_OK) return rc;
+    }
+    if (occ == 6) {
+      mdsx::set_last_kernel("rows_decode_kernel<true, false, false, false, 6>");
+      hipLaunchKernelGGL((rows_decode_kernel<true, false, false, false, 6>), dim3(a.ntiles),
+                         dim3(kRowsBlock), lds, s, a);
+    } else {
+      mdsx::set_last_kernel("rows_decode_kernel<true, false, false, false, 8>");
+      hipLaunchKernelGGL((rows_decode_kernel<true, false, false, false, 8>), dim3(a.ntiles),
+                         dim3(kRowsBlock), lds, s, a);
+    }
   } else {
-    mdsx::set_last_kernel("rows_decode_kernel<false>");
-    hipLaunchKernelGGL((rows_decode_kernel<false>), dim3(a.ntiles), dim3(kRowsBlock), lds, s, a);
+    MDSX_ROWS_CASE(true, false)
+    MDSX_ROWS_CASE(false, false)
+    MDSX_ROWS_CASE(true, true)
+    MDSX_ROWS_CASE(false, true)
   }
+#undef MDSX_ROWS_CASE
   rc = hip_check(hipGetLastError(), "rows_decode_kernel launch");
   if (rc != MDSX_OK) return rc;
   return launch_huge_rows(a, nt, s);

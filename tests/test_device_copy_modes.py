@@ -50,6 +50,12 @@ MODES = {
     'rows_small': 'rows=2,rmin=1000000000',  # a 2 KiB stage: windows and HBM-direct samples
     'rows_xcd': 'rows=-1,rmin=1000000000,xcdr=1',  # row-parallel tiles in XCD-contiguous ranges
     'rows_temporal': 'rows=-1,rownt=0,rmin=1000000000',  # temporal loads / stores (default: nt)
+    # several tiles per workgroup through two stages, the next tile's DMA in flight
+    'rows_pipe': 'rows=-1,rpipe=4,rmin=1000000000',
+    'rows_pipe_small': 'rows=2,rpipe=3,rmin=1000000000',  # ... with windows and HBM-direct rows
+    'rows_pipe_one': 'rows=8,rpipe=1,rmin=1000000000',  # one tile per workgroup, two stages
+    'rows_occ6': 'rows=-1,rocc=6,rmin=1000000000',  # registers bounded for six waves per SIMD
+    'rows_occ8': 'rows=12,rocc=8,rmin=1000000000',  # ... eight, smaller tiles
     'gather': 'run=0,rows=0,gmin=1000000000',
     'group': 'run=0,rows=0,gmin=0,gmax=1000000000',
     'group_nt': 'run=0,rows=0,gmin=0,gmax=1000000000,strc=0',  # str rows streamed (non-temporal) too
