@@ -204,8 +204,11 @@ typedef __attribute__((address_space(1))) uint64_t gu64;
 // prefix (tiles before 0 read as an inclusive zero), retrying while a tile inside that span has
 // not published yet, and steps back W tiles when the window holds no inclusive prefix. The
 // batch's last tile writes the column totals (offsets[rows], totals).
+// `words` / `nunits`: the status words ([nvar][nunits]) and units (tiles, or scan chunks) of the
+// look-back.
 __device__ __forceinline__ void lookback_bases(const DevArgs& a, uint32_t tile, const int64_t* agg,
-                                               int64_t* base_out, uint32_t shard, int lane) {
+                                               int64_t* base_out, uint32_t shard, int lane,
+                                               uint64_t* words, uint32_t nunits) {
   const int nv = a.nvar;
   const int W = nv <= 1 ? 64 : nv <= 2 ? 32 : nv <= 4 ? 16 : 8;
   const int kk = lane & (W - 1);
@@ -214,7 +217,7 @@ __device__ __forceinline__ void lookback_bases(const DevArgs& a, uint32_t tile, 
   for (int g0 = 0; g0 < nv; g0 += 64 / W) {
     const int vi = g0 + lane / W;
     const bool mine = vi < nv;
-    gu64* st = (gu64*)(a.lookback + uint64_t(mine ? vi : 0) * a.ntiles);
+    gu64* st = (gu64*)(words + uint64_t(mine ? vi : 0) * nunits);
     const uint64_t ag = mine ? uint64_t(agg[vi]) : 0;
     if (mine && kk == 0)
       __hip_atomic_store(st + tile, (tile == 0 ? kLbInclusive : kLbAggregate) | ag,
@@ -249,7 +252,7 @@ __device__ __forceinline__ void lookback_bases(const DevArgs& a, uint32_t tile, 
         __hip_atomic_store(st + tile, kLbInclusive | (base + ag), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
       base_out[vi] = int64_t(base);
-      if (tile + 1 == a.ntiles) {  // the batch's last tile: column totals
+      if (tile + 1 == nunits) {  // the batch's last unit: column totals
         for (int c = 0; c < a.ncols; ++c)
           if (a.cols[c].var_index == vi) a.cols[c].offsets[a.rows] = int64_t(base + ag);
         if (a.totals) a.totals[vi] = int64_t(base + ag);

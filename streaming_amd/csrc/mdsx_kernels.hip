@@ -158,9 +158,6 @@ __global__ __launch_bounds__(kBlock) void scan_apply_kernel(const DevArgs a) {
     base += x[j];
   }
 }
-
-
-
 // ---------------------------------------------------------------------------------------------
 // Long ragged rows through an LDS-DMA ring (kSlots > 0 in decode_kernel). Each wave streams its
 // rows' source bytes into a private ring of kSlots 1 KiB slots with global_load_lds_dwordx4 (no
@@ -391,7 +388,7 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(const DevArgs a) {
       if (t == 0) s_agg[vi] = tot;
     }
     __syncthreads();
-    if (wave == 0) lookback_bases(a, tile, s_agg, s_base, v.shard_idx, lane);
+    if (wave == 0) lookback_bases(a, tile, s_agg, s_base, v.shard_idx, lane, a.lookback, a.ntiles);
     __syncthreads();
     if (!v.table_ok) return;  // block-uniform; published its zero aggregates above
   }

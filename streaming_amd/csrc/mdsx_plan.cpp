@@ -203,7 +203,7 @@ void apply_tuning(mdsx_plan* p) {
       p->ring_slots = int(v);
     } else if (key == "sdbg" && v >= 0) {
       p->stage_debug = int(v);
-    } else if (key == "run" && (v == 0 || v == 4 || v == 8 || v == 16)) {
+    } else if (key == "run" && (v == 0 || v == 4 || v == 7 || v == 8 || v == 16)) {
       p->run_slots = int(v);
     } else if (key == "rmin" && v >= 0) {
       p->run_min = v;
@@ -337,7 +337,7 @@ int mdsx_plan_create(const char* const* encodings, const int64_t* column_sizes, 
   // (scan + decode, three boxes, interleaved in one process each): 5.37 / 4.94 / 4.88 TB/s
   // against 4.69 / 4.62 / 4.60 for the round-2 streaming decode (4 KiB ring, temporal);
   // 16 KiB rings lose half the waves per CU (3.8-3.9 TB/s) (profiles/r03/ab/).
-  p->run_slots = p->nvar > 0 ? 8 : 0;
+  p->run_slots = p->nvar > 0 ? 7 : 0;
   p->seg = 1;
   p->run_nt = 1;
   // ... and shorter samples through the row-parallel decode (mdsx_rows.hip), its tiles and stage

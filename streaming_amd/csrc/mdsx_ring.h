@@ -2,8 +2,8 @@
 // and lean paths; mdsx_win.hip: the windowed decode of short samples), and small wave helpers.
 //
 // A wave streams a contiguous byte range of the batch (a run of consecutive samples of one
-// shard) through a private ring of S 1 KiB slots in LDS: stream byte p lives at ring byte
-// p % (S KiB), and a 64-byte mirror of the ring's first bytes sits behind it so that a 16-byte
+// shard) through a private ring of S 1 KiB slots in LDS (S any size; a power of two makes the
+// modulo a mask): stream byte p lives at ring byte p % (S KiB), and a 64-byte mirror of the ring's first bytes sits behind it so that a 16-byte
 // read crossing the ring's end is one contiguous read. Slots are loaded with
 // global_load_lds_dwordx4 (1 KiB per wave-instruction, no VGPR destination) issued from inline
 // asm, so the compiler neither counts nor waits for them: the wave waits with an explicit
@@ -21,18 +21,26 @@ namespace mdsx_kernels {
 
 constexpr uint32_t kMirror = 64;
 
+// Ring byte of stream byte p. p may have wrapped below 0 by less than a ring (a value's first
+// chunk read from before the stream start, bytes then replaced by the carried ones): the ring
+// size is added first, so the modulo of a ring that does not divide 2^32 stays consistent.
+template <int S>
+__device__ __forceinline__ uint32_t ring_pos(uint32_t p) {
+  return (p + S * 1024u) % (S * 1024u);
+}
+
 // 16 stream bytes at stream byte p: one ds_read_b128 at any byte address (gfx950 reads LDS
 // unaligned; the 16-byte realignment costs no instructions).
 template <int S>
 __device__ __forceinline__ uint4 ring16(const lds_u8* ring, uint32_t p) {
-  const u32x4 v = *(const MDSX_L u32x4*)(ring + (p & (S * 1024u - 1u)));
+  const u32x4 v = *(const MDSX_L u32x4*)(ring + ring_pos<S>(p));
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
 // u32 at stream byte p (any alignment).
 template <int S>
 __device__ __forceinline__ uint32_t ring_u32(const lds_u8* ring, uint32_t p) {
-  return *(const MDSX_L uint32_t*)(ring + (p & (S * 1024u - 1u)));
+  return *(const MDSX_L uint32_t*)(ring + ring_pos<S>(p));
 }
 
 // s_waitcnt vmcnt(m), m the largest of 0, 1, 2, 4, 8, 16, 32 not above n (three compares).
@@ -69,8 +77,9 @@ template <int S, bool kNT>
 __device__ __forceinline__ void pump(Stream& st, uint32_t ring_lds, uint32_t low, int lane) {
   while (st.issued < st.nslots && st.issued < low + S) {
     const uint32_t k = st.issued * 64u + uint32_t(lane);
-    glds16<kNT>(st.base + min(k, st.nq - 1), ring_lds + ((st.issued & (S - 1)) << 10));
-    if (lane == int(st.issued & (S - 1))) st.op_at = st.ops;
+    const uint32_t slot = st.issued % uint32_t(S);
+    glds16<kNT>(st.base + min(k, st.nq - 1), ring_lds + (slot << 10));
+    if (lane == int(slot)) st.op_at = st.ops;
     ++st.ops;
     ++st.issued;
   }
@@ -85,9 +94,8 @@ __device__ __forceinline__ void ensure(Stream& st, const lds_u8* ring, uint32_t 
   const uint32_t upto = min(hi >> 10, st.nslots - 1);
   if (upto < st.landed) return;  // waited for already
   st.landed = upto + 1;
-  wait_vm_coarse(st.ops - uint32_t(__builtin_amdgcn_readlane(int(st.op_at), int(upto & (S - 1)))) -
-                 1u);
-  const uint32_t j0 = upto & ~uint32_t(S - 1);
+  wait_vm_coarse(st.ops - uint32_t(__builtin_amdgcn_readlane(int(st.op_at), int(upto % S))) - 1u);
+  const uint32_t j0 = upto - upto % uint32_t(S);  // the slot at ring position 0
   if (j0 != st.mirrored) {
     st.mirrored = j0;
     if (lane < int(kMirror / 4))

@@ -342,6 +342,7 @@ int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
 #define MDSX_SEG_W(WV)         \
   MDSX_SEG_CASE(4, true, WV)   \
   MDSX_SEG_CASE(4, false, WV)  \
+  MDSX_SEG_CASE(7, true, WV)   \
   MDSX_SEG_CASE(8, true, WV)   \
   MDSX_SEG_CASE(8, false, WV)  \
   MDSX_SEG_CASE(16, true, WV)  \
@@ -351,7 +352,7 @@ int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
     MDSX_SEG_W(4)
 #undef MDSX_SEG_W
 #undef MDSX_SEG_CASE
-    return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode ring of 4, 8 or 16 KiB");
+    return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode ring of 4, 7, 8 or 16 KiB");
   }
 #define MDSX_RUN_CASE(S, NT)                                                              \
   if (a.run_slots == S && bool(plan->run_nt) == NT) {                                     \
@@ -368,12 +369,13 @@ int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
   }
   MDSX_RUN_CASE(4, true)
   MDSX_RUN_CASE(4, false)
+  MDSX_RUN_CASE(7, true)
   MDSX_RUN_CASE(8, true)
   MDSX_RUN_CASE(8, false)
   MDSX_RUN_CASE(16, true)
   MDSX_RUN_CASE(16, false)
 #undef MDSX_RUN_CASE
-  return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode ring of 4, 8 or 16 KiB");
+  return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode ring of 4, 7, 8 or 16 KiB");
 }
 
 }  // namespace mdsx_kernels

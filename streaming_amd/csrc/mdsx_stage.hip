@@ -13,7 +13,8 @@
 // (mdsx_kernels.hip). (A single-pass form -- the scan chained into this pass by a decoupled
 // look-back over workgroups in ticket order -- measured no faster on config C and 16 % slower on
 // short rows: with thousands of workgroups starting together the inclusive prefixes propagate
-// one block at a time.)
+// one block at a time. The three scan kernels as one look-back launch over 4096-entry chunks:
+// 0.2 % slower on config C, 1 % on short rows, round 4.)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

@@ -39,6 +39,8 @@ MODES = {
     # the general path for the others, in the same launch
     'seg4': 'run=4,seg=1,rmin=0,rkb=4',
     'seg8': 'run=8,seg=1,rmin=0',
+    'seg7': 'run=7,seg=1,rmin=0',  # a 7 KiB ring (not a power of two: modulo addressing)
+    'run7': 'run=7,rmin=0',  # ... the general path through it
     'seg16': 'run=16,seg=1,rmin=0,rkb=1024',
     'seg8_nt': 'run=8,seg=1,rmin=0,rnt=1',
     'seg16_64k': 'run=16,seg=1,rmin=0,rkb=64',
