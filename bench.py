@@ -75,6 +75,10 @@ def parse_args(argv=None):
     ap.add_argument('--no-verify', action='store_true')
     ap.add_argument('--no-copy-probe', dest='copy_probe', action='store_false',
                     help='skip the same-run copy-ceiling measurement')
+    ap.add_argument('--dist', action='store_true',
+                    help='set up the process group even for one rank (nccl = RCCL on the GPU): '
+                         'runs the barrier / max-over-ranks / gather collectives of the N > 1 '
+                         'path on a one-GPU box')
     ap.add_argument('--dry-run', action='store_true',
                     help='no GPU: exercise the launcher, process group (gloo) and shard '
                     'ownership only (CPU test hook)')
@@ -123,8 +127,13 @@ def init_dist(args):
     world, rank, local = info.world_size, info.rank, info.local_rank
     if world != args.gpus:
         raise SystemExit(f'bench.py: --gpus {args.gpus} but WORLD_SIZE={world}')
+    if (world > 1 or args.dist) and world == 1:  # --dist on one rank: its own rendezvous
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        os.environ.setdefault('MASTER_PORT', str(_free_port()))
+        os.environ.setdefault('RANK', '0')
+        os.environ.setdefault('WORLD_SIZE', '1')
     if args.dry_run:
-        if world > 1:
+        if world > 1 or args.dist:
             torch.distributed.init_process_group('gloo')
         return world, rank, local, torch.device('cpu')
     if torch.cuda.device_count() < local + 1:
@@ -132,18 +141,22 @@ def init_dist(args):
                          f'{torch.cuda.device_count()} visible')
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
-    if world > 1:
+    if world > 1 or args.dist:
         torch.distributed.init_process_group('nccl', device_id=dev)
     return world, rank, local, dev
 
 
+def _dist_on() -> bool:
+    return torch.distributed.is_available() and torch.distributed.is_initialized()
+
+
 def barrier(world):
-    if world > 1:
+    if _dist_on():
         torch.distributed.barrier()
 
 
 def gather_objects(world, obj):
-    if world == 1:
+    if not _dist_on():
         return [obj]
     out = [None] * world
     torch.distributed.all_gather_object(out, obj)
@@ -449,7 +462,7 @@ def dry_run(args, world, rank):
     barrier(world)
     if rank == 0:
         print(json.dumps({'dry_run': True, 'n_gpus': world, 'ownership': lines}), flush=True)
-    if world > 1:
+    if _dist_on():
         torch.distributed.destroy_process_group()
 
 
@@ -493,7 +506,7 @@ def main(argv=None):
         if 'C' in results and configs[0] != 'C':
             line['config_c'] = results['C']
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if _dist_on():
         torch.distributed.destroy_process_group()
     return 0
 

@@ -43,8 +43,9 @@ class LocalDataset(Array, Dataset):
         device: CUDA device for decoding (default: current device).
         decoded_cache_bytes (int, optional): bound on the decoded shards this dataset's readers
             keep in device memory (per device, split over the DataLoader workers), and on their
-            host copies (LRU; :mod:`streaming_amd.cache`). Default: the process-wide cache
-            (``MDSX_DECODED_CACHE_BYTES``, 16 GiB).
+            host copies (LRU; :mod:`streaming_amd.cache`). The most recently used shard of each
+            device is always kept, so 0 keeps exactly one decoded shard per device. Default: the
+            process-wide cache (``MDSX_DECODED_CACHE_BYTES``, 16 GiB).
     """
 
     def __init__(self, local: str, split: Optional[str] = None,
