@@ -157,7 +157,18 @@ def main():
     phases = {}
     for v, dec in decs.items():  # sdbg bit 16: the staged decode's cycles per phase, per tile
         dbg = [int(kv[5:], 0) for kv in v.split('#')[0].split(',') if kv.startswith('sdbg=')]
-        if dbg and dbg[0] & 64:  # the row-parallel decode's phase stamps (mdsx_rows.hip)
+        if dbg and dbg[0] & 64 and 'run=' in v:  # the lean streaming decode's wave stamps
+            dec.run()
+            torch.cuda.synchronize()
+            ntile = int(dec.batch.tile_shard.numel())
+            off = src_abs_offset(dec.plan.num_var, ntile, int(dec.batch.buffer.numel()))
+            raw = dec.workspace[off:off + 24 * ntile].cpu().view(torch.int64).view(ntile, 3)
+            raw = raw.double()
+            phases[v] = dict(zip(['first_sample_landed', 'later_ring_waits', 'wave_total'],
+                                 [round(x) for x in raw.mean(dim=0).tolist()]))
+            phases[v]['median'] = [round(x) for x in raw.median(dim=0).values.tolist()]
+            phases[v]['waves'] = ntile
+        elif dbg and dbg[0] & 64:  # the row-parallel decode's phase stamps (mdsx_rows.hip)
             dec.run()
             torch.cuda.synchronize()
             ntile = int(dec.batch.tile_shard.numel())

@@ -224,6 +224,19 @@ constexpr int kDppRowRor15 = 0x12F;  // lane i <- lane (i + 1) mod 16 of its row
 // Lane i gets lane i + 1's chunk (lane 63: zeros; every caller replaces it).
 __device__ __forceinline__ uint4 shfl_down1(const uint4 v) { return dpp_mov4<kDppWaveShl1>(v); }
 
+// Inclusive prefix sum over the 64 lanes of a wave by DPP (no LDS round trips): row_shr 1, 2, 4,
+// 8 within each row of 16 lanes, then row_bcast:15 (lane 15 of rows 0 and 2 into rows 1 and 3)
+// and row_bcast:31 (lane 31 into rows 2 and 3). Lanes reading outside their row get 0.
+__device__ __forceinline__ uint32_t wave_incl_dpp(uint32_t x) {
+  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x111, 0xF, 0xF, true));  // row_shr:1
+  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x112, 0xF, 0xF, true));  // row_shr:2
+  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x114, 0xF, 0xF, true));  // row_shr:4
+  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x118, 0xF, 0xF, true));  // row_shr:8
+  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x142, 0xA, 0xF, false));  // row_bcast:15
+  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x143, 0xC, 0xF, false));  // row_bcast:31
+  return x;
+}
+
 __device__ __forceinline__ uint4 readlane0(const uint4 v) {
   return make_uint4(__builtin_amdgcn_readlane(v.x, 0), __builtin_amdgcn_readlane(v.y, 0),
                     __builtin_amdgcn_readlane(v.z, 0), __builtin_amdgcn_readlane(v.w, 0));

@@ -310,7 +310,16 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
     // ---- 2. column boundaries of this thread's sample (mds/reader.py:111-125)
     const bool mine = t >= ga && t < gb;
     const uint32_t sp = b - lo_al;  // stage position of the sample (not direct)
+    // the column table lane-distributed (lane c: column c), read by readlane in the uniform
+    // column loops below instead of an LDS round trip per column; up to four size heads read at
+    // once (one unaligned ds_read_b128)
+    const int lvi = lane < ncols ? int(cols[lane].var_index) : -1;
+    const uint32_t lrb = lane < ncols ? cols[lane].row_bytes : 0u;
+    uint4 h4 = make_uint4(0, 0, 0, 0);
+    if (mine && in_range && !direct && nvar <= 4) h4 = lds_read16(stage + sp);
     auto head = [&](int vi) -> uint32_t {
+      if (!direct && nvar <= 4)
+        return vi == 0 ? h4.x : vi == 1 ? h4.y : vi == 2 ? h4.z : h4.w;
       return direct ? load_u32_any(frame + b + 4u * uint32_t(vi))
                     : lds_u32(stage + sp + 4u * uint32_t(vi));
     };
@@ -319,8 +328,8 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
     if (ok && need > e - b) ok = false;
     if (ok) {
       for (int c = 0; c < ncols; ++c) {
-        const int vi = cols[c].var_index;
-        need += vi >= 0 ? head(vi) : cols[c].row_bytes;
+        const int vi = __builtin_amdgcn_readlane(lvi, c);
+        need += vi >= 0 ? head(vi) : uint32_t(__builtin_amdgcn_readlane(int(lrb), c));
       }
       if (need > e - b) ok = false;
     }
@@ -329,17 +338,17 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
     {
       uint32_t rel = 4u * uint32_t(nvar);
       for (int c = 0; c < ncols; ++c) {
-        const MDSX_L DevCol& col = cols[c];
-        const int vi = col.var_index;
-        const uint32_t len = ok ? (vi >= 0 ? head(vi) : col.row_bytes) : 0u;
+        const int vi = __builtin_amdgcn_readlane(lvi, c);
+        const uint32_t rb = uint32_t(__builtin_amdgcn_readlane(int(lrb), c));
+        const uint32_t len = ok ? (vi >= 0 ? head(vi) : rb) : 0u;
         if (mine) {
           T.rec[c * TR + t].len = len;
           T.rec[c * TR + t].src = (direct ? 0u : sp) + rel;
-          if (vi < 0) T.rec[c * TR + t].dst = uint32_t(t - ga) * col.row_bytes;
+          if (vi < 0) T.rec[c * TR + t].dst = uint32_t(t - ga) * rb;
         }
         if (vi < 0 && t == 0) {
-          s_wbase[c] = (row0 + uint64_t(ga)) * col.row_bytes;
-          s_wlen[c] = uint32_t(gb - ga) * col.row_bytes;
+          s_wbase[c] = (row0 + uint64_t(ga)) * rb;
+          s_wlen[c] = uint32_t(gb - ga) * rb;
         }
         rel += len;
       }
@@ -360,16 +369,10 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
       // each half sums at most the window's bytes (< 2^32): no carry between the halves
       const int64_t x = int64_t(len1 | (len2 << 32));
       if (TR <= 64) {  // block-uniform: every sample of the tile is in wave 0 -- no barriers
-        int64_t incl = x;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const int64_t y = __shfl_up(incl, o);
-          if (lane >= o) incl += y;
-        }
-        excl = incl - x;
-        total = int64_t((uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint64_t(incl) >> 32), 63)))
-                         << 32) |
-                        uint32_t(__builtin_amdgcn_readlane(int(incl), 63)));
+        const uint32_t i1 = wave_incl_dpp(uint32_t(len1)), i2 = wave_incl_dpp(uint32_t(len2));
+        excl = int64_t((uint64_t(i2 - uint32_t(len2)) << 32) | (i1 - uint32_t(len1)));
+        total = int64_t((uint64_t(uint32_t(__builtin_amdgcn_readlane(int(i2), 63))) << 32) |
+                        uint32_t(__builtin_amdgcn_readlane(int(i1), 63)));
       } else {
         excl = block_exclusive_scan<!kFence>(x, s_wsum, &total);
       }

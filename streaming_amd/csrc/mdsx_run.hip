@@ -146,9 +146,20 @@ __host__ __device__ __forceinline__ uint32_t seg_cols_lds(int ncols) {
 }
 
 // W waves per workgroup (one run each): fewer waves per workgroup waste less LDS per CU.
-template <int S, bool kNT, int W>
+// Measurement only (kProf, MDSX_TUNE sdbg bit 64): shader-clock stamps per wave (run), written
+// to src_abs[3 tile + k]: k 0 the wave's start to its first sample landed, 1 the later samples'
+// ring waits, 2 the whole wave.
+__device__ __forceinline__ uint64_t seg_clock() {
+  uint64_t c;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(c)::"memory");
+  return c;
+}
+
+template <int S, bool kNT, int W, bool kProf = false>
 __global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint64_t t_start = kProf ? seg_clock() : 0;
+  uint64_t t_wait = 0, t_first = 0;
   const int t = threadIdx.x, lane = t & 63;
   const int wave = W == 1 ? 0 : __builtin_amdgcn_readfirstlane(t >> 6);
   MDSX_L DevCol* s_cols = (MDSX_L DevCol*)smem;
@@ -235,7 +246,14 @@ __global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) 
     const uint32_t e = uint32_t(__builtin_amdgcn_readlane(int(ob), j + 1));
     const uint32_t size = e - b;
     const uint32_t sp = uint32_t(shard + b - sbase);  // stream position of the sample
+    uint64_t t_w0 = 0;
+    if constexpr (kProf) t_w0 = seg_clock();
     ensure<S, kNT>(st, ring, ring_lds, sp, sp + size + 15u, lane);  // ALL of the sample's bytes
+    if constexpr (kProf) {
+      const uint64_t now = seg_clock();
+      if (j == 0) t_first = now - t_start;
+      else t_wait += now - t_w0;
+    }
     // column geometry, lane c: size head (ragged) or row size (fixed), place by prefix sum
     uint32_t len = 0;
     if (lane < ncols) len = vi >= 0 ? ring_u32<S>(ring, sp + 4u * uint32_t(vi)) : rb;
@@ -310,6 +328,13 @@ __global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) 
     if (col.kind == MDSX_KIND_STR && col.flags && lane < n)
       *gp(col.flags + row0 + lane) = fbuf[v * TR + lane];
   }
+  if constexpr (kProf) {
+    if (lane == 0) {
+      a.src_abs[3ull * tile] = t_first;
+      a.src_abs[3ull * tile + 1] = t_wait;
+      a.src_abs[3ull * tile + 2] = seg_clock() - t_start;
+    }
+  }
 }
 
 }  // namespace
@@ -343,10 +368,18 @@ int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
   MDSX_SEG_CASE(4, true, WV)   \
   MDSX_SEG_CASE(4, false, WV)  \
   MDSX_SEG_CASE(7, true, WV)   \
+  MDSX_SEG_CASE(7, false, WV)  \
   MDSX_SEG_CASE(8, true, WV)   \
   MDSX_SEG_CASE(8, false, WV)  \
   MDSX_SEG_CASE(16, true, WV)  \
   MDSX_SEG_CASE(16, false, WV)
+    if (plan->stage_debug & 64) {  // measurement only: the per-wave stamps (7 KiB ring, nt, 2)
+      if (a.run_slots != 7 || !plan->run_nt || W != 2)
+        return mdsx::fail(MDSX_E_ARG, "mdsx: seg stamps: run=7, rnt=1, swg=2 only");
+      mdsx::set_last_kernel("seg_decode_kernel<7, true, 2, true>");
+      hipLaunchKernelGGL((seg_decode_kernel<7, true, 2, true>), dim3(sgrid), dim3(128), slds, s, a);
+      return hip_check(hipGetLastError(), "seg_decode_kernel launch");
+    }
     MDSX_SEG_W(1)
     MDSX_SEG_W(2)
     MDSX_SEG_W(4)
@@ -370,6 +403,7 @@ int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
   MDSX_RUN_CASE(4, true)
   MDSX_RUN_CASE(4, false)
   MDSX_RUN_CASE(7, true)
+  MDSX_RUN_CASE(7, false)
   MDSX_RUN_CASE(8, true)
   MDSX_RUN_CASE(8, false)
   MDSX_RUN_CASE(16, true)
