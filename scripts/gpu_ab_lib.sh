@@ -1,7 +1,8 @@
 #!/bin/bash
 # A/B of two library builds on one box: parity tests on the new build, then tune_decode runs of
 # each build alternated (MDSX_LIBRARY selects the build per process). BASE: the other build's path.
-# CARGS: tune_decode arguments; VARS: its variants.
+# NEWLIB: the build to test (default: the in-tree one). CARGS: tune_decode arguments; VARS: its
+# variants.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/${TAG:-ab}
@@ -14,7 +15,9 @@ if [ -z "$NOTEST" ]; then
 fi
 for i in 1 2; do
   for lib in new base; do
-    if [ $lib = base ]; then export MDSX_LIBRARY=$BASE; else unset MDSX_LIBRARY; fi
+    if [ $lib = base ]; then export MDSX_LIBRARY=$BASE
+    elif [ -n "$NEWLIB" ]; then export MDSX_LIBRARY=$NEWLIB
+    else unset MDSX_LIBRARY; fi
     timeout -k 10 300 python3 scripts/tune_decode.py ${CARGS:---config C --shards 64} --rounds 3 --variants ${VARS:-run=4} > "$OUT/$lib$i.json" 2> "$OUT/$lib$i.err" || { tail -20 "$OUT/$lib$i.err"; exit 1; }
     python3 -c "
 import json; d = json.load(open('$OUT/$lib$i.json'))

@@ -15,5 +15,6 @@ for i in $(seq 1 ${REPS:-2}); do
   timeout -k 10 300 python3 -u scripts/tune_decode.py ${CARGS:---config C --shards 64} --rounds ${ROUNDS:-4} --variants $VARIANTS > "$OUT/r$i.json" 2> "$OUT/r$i.err" || { tail -20 "$OUT/r$i.err"; exit 1; }
   python3 -c "
 import json; d = json.load(open('$OUT/r$i.json'))
-for k, v in d['results'].items(): print('r$i', k, round(v['GBps']), round(v['median_ms'], 4))"
+for k, v in d['results'].items(): print('r$i', k, round(v['GBps']), round(v['median_ms'], 4))
+for k, v in d.get('phase_cycles_per_tile', {}).items(): print('r$i', k, 'phase medians', v.get('median'))"
 done

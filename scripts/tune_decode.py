@@ -173,9 +173,10 @@ def main():
             torch.cuda.synchronize()
             ntile = int(dec.batch.tile_shard.numel())
             off = src_abs_offset(dec.plan.num_var, ntile, int(dec.batch.buffer.numel()))
-            raw = dec.workspace[off:off + 32 * ntile].cpu().view(torch.int64).view(ntile, 4)
+            raw = dec.workspace[off:off + 64 * ntile].cpu().view(torch.int64).view(ntile, 8)[:, :7]
             med = raw.double().median(dim=0).values.tolist()
-            phases[v] = dict(zip(['dma_wait', 'geometry_scan_map', 'write', 'flags'],
+            phases[v] = dict(zip(['dma_wait', 'heads_bounds', 'value_records',
+                                  'scan_offsets_maps', 'geometry_barrier', 'write', 'flags'],
                                  [round(x) for x in raw.double().mean(dim=0).tolist()]))
             phases[v]['median'] = [round(x) for x in med]
             phases[v]['tiles'] = ntile

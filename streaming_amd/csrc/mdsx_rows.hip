@@ -90,9 +90,10 @@ __device__ __forceinline__ void rows_barrier() {
   else lds_barrier();
 }
 
-// Measurement only (MDSX_TUNE sdbg bit 64): shader-clock time of each phase of a tile (DMA wait,
-// column geometry + scan + chunk maps, column writes, flags), written by thread 0 of each tile's
-// workgroup to src_abs[4 tile + k] (the huge-row list's space; plain stores, no shared counter).
+// Measurement only (MDSX_TUNE sdbg bit 64): shader-clock time of each phase of a tile (DMA wait;
+// size heads + bounds; value records; scan + offsets + chunk maps; the barrier after them; column
+// writes; flags), written by thread 0 of each tile's workgroup to src_abs[8 tile + k] (the
+// huge-row list's space; plain stores, no shared counter).
 __device__ __forceinline__ uint64_t shader_clock() {
   uint64_t c;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(c)::"memory");
@@ -100,7 +101,7 @@ __device__ __forceinline__ uint64_t shader_clock() {
 }
 __device__ __forceinline__ void prof_mark(const DevArgs& a, uint32_t tile, int k, uint64_t& ts) {
   const uint64_t now = shader_clock();
-  if (threadIdx.x == 0) a.src_abs[4ull * tile + k] = now - ts;
+  if (threadIdx.x == 0) a.src_abs[8ull * tile + k] = now - ts;
   ts = now;
 }
 
@@ -334,6 +335,7 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
       if (need > e - b) ok = false;
     }
     if (mine && in_range && !ok) report_decode(a, MDSX_E_BOUNDS, shard_idx, int(r0 + t), -1);
+    if constexpr (prof) prof_mark(a, tile, 1, ts);
     // ---- 3. value lengths and stage positions; fixed columns' window output
     {
       uint32_t rel = 4u * uint32_t(nvar);
@@ -353,6 +355,7 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
         rel += len;
       }
     }
+    if constexpr (prof) prof_mark(a, tile, 2, ts);
     // ragged lengths scanned across the window onto each column's base, two columns per scan;
     // offsets; chunk maps
     for (int c0 = 0; c0 < ncols;) {
@@ -410,8 +413,9 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
       const uint32_t slot = atomicAdd(count, 1u);
       a.src_abs[slot] = (uint64_t(tile) << 32) | uint32_t(t);
     }
+    if constexpr (prof) prof_mark(a, tile, 3, ts);
     rows_barrier<kFence>();
-    if constexpr (prof) prof_mark(a, tile, 1, ts);
+    if constexpr (prof) prof_mark(a, tile, 4, ts);
     if constexpr (kPipe) {
       // the next clean tile's bytes and offsets, into the other stage (last read by the tile
       // before this one, whose readers passed this tile's first barrier), while this one's
@@ -438,6 +442,12 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
       // kFlat: the columns' output chunks as one index space -- consecutive threads take
       // consecutive chunks across the column ends, so a tile's writes take the fewest rounds of
       // the (latency-bound) chunk loop; lane c counts column c's chunks. Else a loop per column.
+      // The column ends are read across lanes (v_readlane) inside the loop. Where the compiler
+      // spills that register (the 64-VGPR bound, kOcc 8), the reload writes only the active lanes
+      // and a lane that left the divergent loop would read back stale: there the loop's trip
+      // count is wave-uniform (every lane active at the reads; 3-4 % slower at kOcc 6, which
+      // keeps the ends in a register -- checked in its ISA).
+      constexpr bool kUniform = kOcc >= 8;
       uint32_t cincl = 0, total = 0;
       if constexpr (kFlat) {
         uint32_t cn = 0;
@@ -454,18 +464,20 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
                                     : (a.stage_debug & 2) ? 0u
                                     : uint32_t(((((reinterpret_cast<uint64_t>(cols[cl].data) +
                                                    s_wbase[cl]) & 15) + s_wlen[cl] + 15) >> 4));
-        for (uint32_t kg = uint32_t(t); kg < kend; kg += kRowsBlock) {
+        for (uint32_t kw = uint32_t(kUniform ? t - lane : t); kw < kend; kw += kRowsBlock) {
+        const uint32_t kg = kUniform ? kw + uint32_t(lane) : kw;
         // the chunk's column c and its index k inside the column
         int c = cl;
         uint32_t c0 = 0;
         if constexpr (kFlat) {
           // uniform loop of scalar reads of the column ends (v_readlane ignores the exec mask;
-          // a lane shuffle would read the ends of lanes that left the loop as zeros)
+          // a lane shuffle would read inactive lanes as zeros)
           for (int j = 0; j + 1 < ncols; ++j) {
             const uint32_t e = uint32_t(__builtin_amdgcn_readlane(int(cincl), j));
             if (kg >= e) c = j + 1, c0 = e;
           }
         }
+        if (kUniform && kg >= kend) continue;
         const uint32_t k = kg - c0;
         const MDSX_L DevCol& col = cols[c];
         const int base = c * TR;
@@ -572,7 +584,7 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
       }
       rows_barrier<kFence>();  // every piece's UTF-8 mark is in (a next tile's DMA may be in flight)
     }
-    if constexpr (prof) prof_mark(a, tile, 2, ts);
+    if constexpr (prof) prof_mark(a, tile, 5, ts);
     // ---- 5. flags (a sample listed for the huge-row kernel: set there when its value fails)
     if (mine) {
       for (int c = 0; c < ncols; ++c) {
@@ -581,7 +593,7 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
           *gp(col.flags + row0 + t) = uint8_t((T.bad[c * 8 + (t >> 5)] >> (t & 31)) & 1u);
       }
     }
-    if constexpr (prof) prof_mark(a, tile, 3, ts);
+    if constexpr (prof) prof_mark(a, tile, 6, ts);
     ga = gb;
   }
   if constexpr (kPipe) rows_barrier<kFence>();  // this tile's readers of the tables and its stage are done
