@@ -500,6 +500,10 @@ def main(argv=None):
             'parity': 'bit-exact vs encoded source columns' if not args.no_verify else 'skipped',
             'config': head['config'],
             'per_rank': head['per_rank'],
+            # the timing barrier / max-over-ranks / report gather: a torch.distributed process
+            # group ('nccl' = RCCL on ROCm) when one is up, else none (one process, no group)
+            'process_group': (f'{torch.distributed.get_backend()}, {world} rank(s)'
+                              if _dist_on() else None),
             'roofline': head['roofline'],
             'cpu_baseline': head['cpu_baseline'],
         }

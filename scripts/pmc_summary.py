@@ -48,11 +48,21 @@ def configs(line):
     return res
 
 
+def named(kernel, name):
+    """Whether the dispatch / stats name `name` is the bench's kernel: the bench reports the
+    template arguments it chose (`seg_decode_kernel<7, true, 2>`), the symbol also carries the
+    defaulted ones (`seg_decode_kernel<7, true, 2, false>`)."""
+    name = name.replace('(anonymous namespace)::', '')
+    if kernel in name:
+        return True
+    k = kernel[:-1] if kernel.endswith('>') else kernel
+    return k + ', ' in name or k + ',' in name
+
+
 def counter(out, sub, name, kernel):
     vals = []
     for r in rows(out, f'{sub}/**/*counter_collection.csv'):
-        if kernel in r.get('Kernel_Name', '').replace('(anonymous namespace)::', '') and \
-                r.get('Counter_Name') == name:
+        if named(kernel, r.get('Kernel_Name', '')) and r.get('Counter_Name') == name:
             vals.append(float(r['Counter_Value']))
     return vals
 
@@ -76,7 +86,7 @@ def main(out):
             'kernel': kernel,
             'src_sha': cfg['roofline'].get('src_sha'),
             'algorithmic_bytes_per_launch': cfg['roofline']['algorithmic_bytes_per_launch'],
-            'kernel_stats': [r for r in stats if kernel in r['Name']],
+            'kernel_stats': [r for r in stats if named(kernel, r['Name'])],
         }
         # the bench's timed launches: the kernel's last `steps` dispatches of this workload in
         # the trace (warm-up and verification launches come before them), against the bench
@@ -84,7 +94,7 @@ def main(out):
         durs = [int(r['End_Timestamp']) - int(r['Start_Timestamp'])
                 for r in sorted(rows(out, 'trace/**/*kernel_trace.csv'),
                                 key=lambda r: int(r['Start_Timestamp']))
-                if kernel in r['Kernel_Name'].replace('(anonymous namespace)::', '')]
+                if named(kernel, r['Kernel_Name'])]
         steps = int(lines[0].get('steps', 20))
         if len(durs) >= steps:
             # the config's own launches: B's come first in the trace, C's after them
