@@ -70,6 +70,28 @@ def _compile(src: str, obj: str, verbose: bool) -> None:
     subprocess.run(cmd, check=True)
 
 
+def _compile_device(src: str, obj: str, verbose: bool) -> None:
+    """The device code alone (for the ISA check below)."""
+    cmd = [hipcc(), f'--offload-arch={ARCH}', *FLAGS, '-I', os.path.join(ROOT, 'include'),
+           '--cuda-device-only', '--no-gpu-bundle-output', '-c', src, '-o', obj]
+    if verbose:
+        print(' '.join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+
+
+def _check_cross_lane_reads(obj: str) -> None:
+    """Refuse a build whose row-parallel decode reads a spilled register across lanes
+    (streaming_amd/isa_check.py)."""
+    from streaming_amd import isa_check
+    rocm = os.environ.get('ROCM_PATH', '/opt/rocm')
+    text = subprocess.run([os.path.join(rocm, 'lib', 'llvm', 'bin', 'llvm-objdump'), '-d', obj],
+                          capture_output=True, text=True, check=True).stdout
+    bad = isa_check.check(text)
+    if bad:
+        raise RuntimeError('mdsx build: cross-lane reads of spilled registers in ' +
+                           '; '.join(f'{name} (v{regs})' for name, regs in bad))
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     """Compile every source to an object in parallel, then link libmdsx.so (in-tree)."""
     os.makedirs(os.path.dirname(OUTPUT), exist_ok=True)
@@ -83,9 +105,14 @@ def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(objdir, exist_ok=True)
     objs = [os.path.join(objdir, os.path.basename(s) + '.o') for s in SOURCES]
     from concurrent.futures import ThreadPoolExecutor
-    with ThreadPoolExecutor(max_workers=max(1, min(len(SOURCES), os.cpu_count() or 1))) as pool:
-        for f in [pool.submit(_compile, s, o, verbose) for s, o in zip(SOURCES, objs)]:
+    rows_dev = os.path.join(objdir, 'mdsx_rows.device.o')
+    with ThreadPoolExecutor(max_workers=max(1, min(len(SOURCES) + 1, os.cpu_count() or 1))) as pool:
+        jobs = [pool.submit(_compile, s, o, verbose) for s, o in zip(SOURCES, objs)]
+        jobs.append(pool.submit(_compile_device, os.path.join(HERE, 'csrc', 'mdsx_rows.hip'),
+                                rows_dev, verbose))
+        for f in jobs:
             f.result()
+    _check_cross_lane_reads(rows_dev)
     tmp = OUTPUT + '.tmp'
     cmd = [hipcc(), f'--offload-arch={ARCH}', '-shared', '-fPIC', '-o', tmp, *objs]
     if verbose:
