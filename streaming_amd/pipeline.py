@@ -124,11 +124,11 @@ class ShardPipeline:
         depth: staging/device slots in flight (2 = double buffering). Default: enough slots
             for every worker thread to have a shard to read or decompress, ``ceil(workers /
             shards_per_batch) + 1`` and at least 2 (a slot is refilled only after its H2D copy,
-            so with 16 threads and 8-shard batches two slots leave half the threads idle), one
-            more when shards are compressed (decompression times vary shard to shard; a spare
-            slot absorbs a slow one: config E, 16 threads, 8-shard batches, 2M samples: 16.5
-            GiB/s at depth 2, 24.2 at depth 3, 24.9 at depth 4 with a third of depth 3's
-            pass-to-pass spread).
+            so with 16 threads and 8-shard batches two slots leave half the threads idle), two
+            more when shards are compressed (decompression times vary shard to shard; spare
+            slots absorb a slow one: config E, 16 threads, 8-shard batches, 2M samples: 16.5
+            GiB/s at depth 2, 24.2 at depth 3 (15-24 % pass-to-pass spread), 24.1-24.9 at depth
+            4 (6-18 %), 25.0 at depth 5 (3-4 %)).
         workers: host threads reading / decompressing shards.
         device: CUDA device.
         validate_hash: check every shard against its index.json ``raw_data.hashes[algo]``
@@ -165,7 +165,7 @@ class ShardPipeline:
         if depth is None:
             depth = max(2, -(-max(1, workers) // self.per) + 1)
             if any(s.compression for s in self.shards):
-                depth += 1
+                depth += 2
         self.depth = max(1, depth)
         dev = torch.device(device or 'cuda')
         if dev.index is None:
