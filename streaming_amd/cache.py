@@ -128,6 +128,17 @@ class DecodedShardCache:
             self._entries.move_to_end(key)
             return hit[0]
 
+    def lookup(self, key: int) -> Optional[Any]:
+        """The value for ``key`` if it is cached (a hit, made the most recently used), else None
+        (not counted as a miss: the caller goes on to :meth:`get_or_create`)."""
+        with self._lock:
+            hit = self._entries.get(key)
+            if hit is None:
+                return None
+            self._entries.move_to_end(key)
+            self.hits += 1
+            return hit[0]
+
     def get_or_create(self, key: int, create: Callable[[], tuple]) -> Any:
         """The value for ``key``, made by ``create() -> (value, device bytes[, device])`` on a
         miss.

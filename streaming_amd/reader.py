@@ -202,6 +202,7 @@ class _HostShard:
     def __init__(self, plan: Plan, decoded: DecodedBatch) -> None:
         self.fixed: dict[str, np.ndarray] = {}
         self.ragged: dict[str, tuple[np.ndarray, np.ndarray]] = {}
+        self.getters: Optional[list] = None  # MDSReader._getters, built on first use
         self.nbytes = 0
         for col in plan.columns:
             out = decoded.columns[col.name]
@@ -315,7 +316,10 @@ class MDSReader(JointReader):
         return get_plan(self.column_names, self.column_encodings, self.column_sizes)
 
     def _filename(self) -> str:
-        return self._path(self.raw_data.basename)
+        name = self.__dict__.get('_fname')
+        if name is None:  # (the directory and basename are fixed at construction)
+            name = self._fname = self._path(self.raw_data.basename)
+        return name
 
     def read_shard_bytes(self) -> bytes:
         """The raw shard file (FileNotFoundError if it is not in the local cache)."""
@@ -411,16 +415,45 @@ class MDSReader(JointReader):
                              f'sample ({need} > {len(data)} bytes).')
 
     def _materialize(self, host: _HostShard, idx: int) -> dict[str, Any]:
-        sample: dict[str, Any] = {}
+        getters = host.getters
+        if getters is None:
+            getters = host.getters = self._getters(host)
+        return {name: get(idx) for name, get in getters}
+
+    def _getters(self, host: _HostShard) -> list[tuple[str, Any]]:
+        """Per column, a function of the sample index returning its reference value (the
+        branches of :meth:`_value` resolved once per host shard, the fixed columns viewed as
+        their dtype once): the per-sample cost is one call per column."""
+        out = []
         for col, enc, info in zip(self.plan.columns, self.column_encodings, self._infos):
+            name = info.name if info is not None else None
             if col.is_fixed:
-                raw = host.fixed[col.name][idx]
-                sample[col.name] = self._value(enc, info, raw, fixed=True)
+                raw = host.fixed[col.name]
+                if info is not None and info.dtype is not None and info.size == raw.shape[1]:
+                    if name == 'int':
+                        typed = raw.view(info.dtype).reshape(-1)
+                        get = (lambda t: lambda i: int(t[i]))(typed)
+                    elif info.shape == ():
+                        get = raw.view(info.dtype).reshape(-1).__getitem__
+                    else:
+                        get = raw.view(info.dtype).reshape((raw.shape[0], ) +
+                                                           tuple(info.shape)).__getitem__
+                else:
+                    get = (lambda r, e, f: lambda i: self._value(e, f, r[i], fixed=True))(
+                        raw, enc, info)
             else:
                 values, offsets = host.ragged[col.name]
-                data = values[offsets[idx]:offsets[idx + 1]].tobytes()
-                sample[col.name] = self._value(enc, info, data, fixed=False)
-        return sample
+                offs = offsets.tolist()  # (python ints: cheaper slicing than numpy scalars)
+                if name == 'bytes':
+                    get = (lambda v, o: lambda i: v[o[i]:o[i + 1]].tobytes())(values, offs)
+                elif name == 'str':
+                    get = (lambda v, o: lambda i: v[o[i]:o[i + 1]].tobytes().decode('utf-8'))(
+                        values, offs)
+                else:
+                    get = (lambda v, o, e, f: lambda i: self._value(
+                        e, f, v[o[i]:o[i + 1]].tobytes(), fixed=False))(values, offs, enc, info)
+            out.append((col.name, get))
+        return out
 
     @staticmethod
     def _value(encoding: str, info, raw, fixed: bool) -> Any:
@@ -452,7 +485,7 @@ class MDSReader(JointReader):
             raise IndexError(
                 f'Relative sample index {idx} is not present in the {self.raw_data.basename} file.')
         os.stat(self._filename())  # FileNotFoundError once evicted, as the reference's open()
-        entry = self._decode_entry()
+        entry = self.cache.lookup(self._key) or self._decode_entry()
         if entry.status.code != 0:
             self._check_row(entry, idx)
         host = entry.host

@@ -7,6 +7,8 @@ one ``searchsorted`` over the shard boundaries instead of span lists; batched lo
 
 from __future__ import annotations
 
+from bisect import bisect_right
+
 import numpy as np
 from numpy.typing import NDArray
 
@@ -24,12 +26,13 @@ class Spanner:
         self.span_size = span_size
         self.num_samples = int(self.shard_sizes.sum())
         self.shard_bounds = np.concatenate([np.zeros(1, np.int64), self.shard_sizes.cumsum()])
+        self._bounds = self.shard_bounds.tolist()  # (per-sample lookups: bisect on python ints)
 
     def __getitem__(self, index: int) -> tuple[int, int]:
         if not (0 <= index < self.num_samples):
             raise IndexError(f'Invalid sample index `{index}`: 0 <= {index} < {self.num_samples}')
-        shard = int(np.searchsorted(self.shard_bounds, index, side='right')) - 1
-        return shard, int(index - self.shard_bounds[shard])
+        shard = bisect_right(self._bounds, index) - 1
+        return shard, int(index) - self._bounds[shard]
 
     def locate(self, indices: NDArray[np.int64]) -> tuple[NDArray[np.int64], NDArray[np.int64]]:
         """Vectorised ``__getitem__``: (shard ids, indices inside the shards)."""
