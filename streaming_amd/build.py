@@ -80,16 +80,17 @@ def _compile_device(src: str, obj: str, verbose: bool) -> None:
 
 
 def _check_cross_lane_reads(obj: str) -> None:
-    """Refuse a build whose row-parallel decode reads a spilled register across lanes
-    (streaming_amd/isa_check.py)."""
+    """Refuse a build whose row-parallel decode reads a register across lanes where the exec mask
+    may be partial (streaming_amd/isa_check.py)."""
     from streaming_amd import isa_check
     rocm = os.environ.get('ROCM_PATH', '/opt/rocm')
     text = subprocess.run([os.path.join(rocm, 'lib', 'llvm', 'bin', 'llvm-objdump'), '-d', obj],
                           capture_output=True, text=True, check=True).stdout
     bad = isa_check.check(text)
     if bad:
-        raise RuntimeError('mdsx build: cross-lane reads of spilled registers in ' +
-                           '; '.join(f'{name} (v{regs})' for name, regs in bad))
+        raise RuntimeError('mdsx build: cross-lane reads under a possibly partial exec mask in ' +
+                           '; '.join(f'{name} (at {", ".join(hex(a) for a in addrs)})'
+                                     for name, addrs in bad))
 
 
 def build(force: bool = False, verbose: bool = False) -> str:

@@ -56,6 +56,7 @@ struct mdsx_plan {
   int xcd_order = 3;       // bits: decodes whose XCDs each take a contiguous range of tiles
                            // (profiles/r03/xcd_order/): 1 the lean path (+3 % on config C), 2 the
                            // register decode (+1.1 % on config B); not 4, the row-parallel (-1 %)
+  int seg_var = 0;         // lean path, measurement variants (MDSX_TUNE sv, bits; mdsx_run.hip)
   int seg_waves = 2;       // lean path: waves (runs) per workgroup (1, 2 or 4; 2: 18 waves per CU,
                            // +4 % on 3-5 KB samples, profiles/r03/seg_waves/)
   int rows_kb = 0;         // row-parallel decode of shorter samples: LDS stage in KiB (0: off,
@@ -95,7 +96,7 @@ inline bool use_rows_decode(const mdsx_plan* p, uint64_t bytes, uint64_t rows) {
 inline uint64_t rows_lds_bytes_est(const mdsx_plan* p, uint64_t stage, uint64_t tr) {
   const uint64_t nstage = p->rows_pipe > 0 ? 2 : 1;
   return 192 * nstage + stage * nstage + tr * uint64_t(p->ncols) * 16 + uint64_t(p->ncols) * 32 +
-         uint64_t(p->nvar) * (stage / 16 + 4) + uint64_t(p->ncols) * 64 + 64;
+         uint64_t(p->nvar) * (stage / 16 + 4) + uint64_t(p->ncols) * 72 + 64;
 }
 
 // The stage a tile of tr samples of per_row bytes needs: (1 + 1/slack) of its average bytes plus

@@ -221,6 +221,8 @@ void apply_tuning(mdsx_plan* p) {
       p->rows_nt = v ? 1 : 0;
     } else if (key == "swg" && (v == 1 || v == 2 || v == 4)) {
       p->seg_waves = int(v);
+    } else if (key == "sv" && v >= 0 && v <= 15) {
+      p->seg_var = int(v);
     } else if (key == "seg") {
       p->seg = v ? 1 : 0;
     } else if (key == "xcd" || key == "xcdb" || key == "xcdr") {

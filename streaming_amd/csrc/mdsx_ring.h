@@ -60,6 +60,19 @@ __device__ __forceinline__ void wait_vm_coarse(uint32_t n) {
   }
 }
 
+// s_waitcnt vmcnt(n) for n <= 16 exactly (larger n: 16).
+__device__ __forceinline__ void wait_vm_exact16(uint32_t n) {
+  switch (n) {
+#define MDSX_VMW(k) \
+  case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    MDSX_VMW(0) MDSX_VMW(1) MDSX_VMW(2) MDSX_VMW(3) MDSX_VMW(4) MDSX_VMW(5) MDSX_VMW(6)
+    MDSX_VMW(7) MDSX_VMW(8) MDSX_VMW(9) MDSX_VMW(10) MDSX_VMW(11) MDSX_VMW(12) MDSX_VMW(13)
+    MDSX_VMW(14) MDSX_VMW(15)
+#undef MDSX_VMW
+    default: asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  }
+}
+
 // The wave's stream: chunks [0, nq) from base, in slots of 64 chunks.
 struct Stream {
   const uint4* base;

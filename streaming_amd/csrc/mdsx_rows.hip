@@ -76,7 +76,7 @@ __host__ __device__ __forceinline__ size_t rows_lds_tables(uint32_t cap, int TR,
          size_t(TR) * size_t(ncols) * 16 + size_t(ncols) * 32 + size_t(nvar) * rows_map_len(cap);
 }
 __host__ __device__ __forceinline__ size_t rows_lds_colstate(int ncols) {
-  return size_t(ncols) * (sizeof(DevCol) + 8 + 8 + 4 + 4);
+  return size_t(ncols) * (sizeof(DevCol) + 8 + 8 + 4 + 4 + 4);
 }
 __host__ __device__ __forceinline__ size_t rows_lds_bytes(uint32_t cap, int TR, int ncols,
                                                           int nvar, int nstage = 1) {
@@ -169,6 +169,7 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
   MDSX_L uint64_t* s_wbase = s_base + ncols;  // the window's first output byte (rel. data)
   MDSX_L uint32_t* s_wlen = (MDSX_L uint32_t*)(s_wbase + ncols);  // the window's output bytes
   MDSX_L uint32_t* s_skip = s_wlen + ncols;  // the tile's bytes exceed the column capacity
+  MDSX_L uint32_t* s_ends = s_skip + ncols;  // the write loop's column ends (wide schemas)
   for (int c = t; c < ncols; c += kRowsBlock) s_cols[c] = a.cols[c];
   const MDSX_L DevCol* cols = s_cols;
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(
@@ -327,13 +328,16 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
     bool ok = mine && in_range;
     uint64_t need = 4ull * uint64_t(nvar);
     if (ok && need > e - b) ok = false;
-    if (ok) {
-      for (int c = 0; c < ncols; ++c) {
-        const int vi = __builtin_amdgcn_readlane(lvi, c);
-        need += vi >= 0 ? head(vi) : uint32_t(__builtin_amdgcn_readlane(int(lrb), c));
-      }
-      if (need > e - b) ok = false;
+    // (the column facts are read across lanes here, where every lane is active; only the size
+    // heads are read under the per-sample condition)
+    for (int c = 0; c < ncols; ++c) {
+      const int vi = __builtin_amdgcn_readlane(lvi, c);
+      const uint32_t rbc = uint32_t(__builtin_amdgcn_readlane(int(lrb), c));
+      uint32_t add = rbc;
+      if (vi >= 0) add = ok ? head(vi) : 0u;
+      need += add;
     }
+    if (ok && need > e - b) ok = false;
     if (mine && in_range && !ok) report_decode(a, MDSX_E_BOUNDS, shard_idx, int(r0 + t), -1);
     if constexpr (prof) prof_mark(a, tile, 1, ts);
     // ---- 3. value lengths and stage positions; fixed columns' window output
@@ -442,20 +446,26 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
       // kFlat: the columns' output chunks as one index space -- consecutive threads take
       // consecutive chunks across the column ends, so a tile's writes take the fewest rounds of
       // the (latency-bound) chunk loop; lane c counts column c's chunks. Else a loop per column.
-      // The column ends are read across lanes (v_readlane) inside the loop. Where the compiler
-      // spills that register (the 64-VGPR bound, kOcc 8), the reload writes only the active lanes
-      // and a lane that left the divergent loop would read back stale: there the loop's trip
-      // count is wave-uniform (every lane active at the reads; 3-4 % slower at kOcc 6, which
-      // keeps the ends in a register -- checked in its ISA).
-      constexpr bool kUniform = kOcc >= 8;
-      uint32_t cincl = 0, total = 0;
+      // The loop is divergent (a lane leaves it after its last chunk), so nothing inside it reads
+      // across lanes: a VGPR's inactive lanes are not preserved by the compiler (a spill reload or
+      // a copy under a partial exec mask writes the active lanes only -- a 64-VGPR build faulted
+      // reading the column ends with v_readlane inside the loop). The column ends
+      // are read here, every lane active, into scalar registers (up to kEnds of them) or, for
+      // wider schemas, into LDS (streaming_amd/isa_check.py checks the built code).
+      constexpr int kEnds = 8;
+      uint32_t total = 0;
+      uint32_t ends[kEnds];
       if constexpr (kFlat) {
         uint32_t cn = 0;
         if (lane < ncols && !s_skip[lane]) {
           const uint64_t w = reinterpret_cast<uint64_t>(cols[lane].data) + s_wbase[lane];
           cn = uint32_t(((w & 15) + s_wlen[lane] + 15) >> 4);
         }
-        cincl = wave_incl_u32(cn, lane, ncols);
+        const uint32_t cincl = wave_incl_u32(cn, lane, ncols);
+#pragma unroll
+        for (int j = 0; j < kEnds; ++j)
+          ends[j] = j + 1 < ncols ? uint32_t(__builtin_amdgcn_readlane(int(cincl), j)) : ~0u;
+        if (ncols > kEnds + 1 && lane < ncols) s_ends[lane] = cincl;  // (this wave reads its own)
         total = (a.stage_debug & 2) ? 0u : uint32_t(__builtin_amdgcn_readlane(int(cincl), ncols - 1));
       }
       for (int cl = 0; cl < (kFlat ? 1 : ncols); ++cl) {
@@ -464,20 +474,23 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
                                     : (a.stage_debug & 2) ? 0u
                                     : uint32_t(((((reinterpret_cast<uint64_t>(cols[cl].data) +
                                                    s_wbase[cl]) & 15) + s_wlen[cl] + 15) >> 4));
-        for (uint32_t kw = uint32_t(kUniform ? t - lane : t); kw < kend; kw += kRowsBlock) {
-        const uint32_t kg = kUniform ? kw + uint32_t(lane) : kw;
+        for (uint32_t kw = uint32_t(t); kw < kend; kw += kRowsBlock) {
+        const uint32_t kg = kw;
         // the chunk's column c and its index k inside the column
         int c = cl;
         uint32_t c0 = 0;
         if constexpr (kFlat) {
-          // uniform loop of scalar reads of the column ends (v_readlane ignores the exec mask;
-          // a lane shuffle would read inactive lanes as zeros)
-          for (int j = 0; j + 1 < ncols; ++j) {
-            const uint32_t e = uint32_t(__builtin_amdgcn_readlane(int(cincl), j));
-            if (kg >= e) c = j + 1, c0 = e;
+          if (ncols <= kEnds + 1) {  // uniform: the ends in scalar registers
+#pragma unroll
+            for (int j = 0; j < kEnds; ++j)
+              if (kg >= ends[j]) c = j + 1, c0 = ends[j];
+          } else {
+            for (int j = 0; j + 1 < ncols; ++j) {
+              const uint32_t e = s_ends[j];
+              if (kg >= e) c = j + 1, c0 = e;
+            }
           }
         }
-        if (kUniform && kg >= kend) continue;
         const uint32_t k = kg - c0;
         const MDSX_L DevCol& col = cols[c];
         const int base = c * TR;

@@ -42,6 +42,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cstdint>
 
 #include "mdsx_decode.h"
@@ -98,10 +99,15 @@ __host__ __device__ __forceinline__ uint32_t seg_wave_lds(int S, int TR, int nva
 // byte of the column (bytes below it belong to the run before). `carry` (uniform): in, the partly
 // filled chunk at d & ~15; out, the one at (d + len) & ~15. Returns (utf8) whether the value is
 // not well-formed UTF-8 (wave-uniform).
-template <int S, bool kNT>
-__device__ __forceinline__ bool seg_copy(const lds_u8* ring, uint64_t base, uint32_t cst,
-                                         uint32_t d, uint32_t len, uint32_t p, bool utf8,
-                                         bool zero, uint4& carry, uint32_t& ops, int lane) {
+// Measurement variants (kV bits, MDSX_TUNE sv): 2 releases the ring slots a value's 1 KiB step
+// has consumed after each step (not after the whole value), so the next sample's slots go in
+// flight while the value is still being written; 4 waits per 1 KiB step (not once per sample).
+template <int S, bool kNT, int kV = 0>
+__device__ __forceinline__ bool seg_copy(Stream& st, const lds_u8* ring, uint32_t ring_lds,
+                                         uint64_t base, uint32_t cst, uint32_t d, uint32_t len,
+                                         uint32_t p, bool utf8, bool zero, uint4& carry,
+                                         int lane) {
+  uint32_t& ops = st.ops;
   const uint32_t head = d & 15u, dbeg = d - head, dend = d + len;
   const uint32_t nch = (dend - dbeg + 15u) >> 4;  // chunks touched
   const uint32_t nfull = (dend - dbeg) >> 4;      // chunks completed by this value
@@ -115,6 +121,9 @@ __device__ __forceinline__ bool seg_copy(const lds_u8* ring, uint64_t base, uint
   uint4 last = carry;
   for (uint32_t g = 0; g < nch; g += 64) {  // wave-uniform
     const uint32_t kk = g + uint32_t(lane);
+    const uint32_t gend = min(s0 + 16u * (g + 64u), p + len);  // this step's stream bytes end
+    if constexpr ((kV & 4) != 0)
+      if (!zero) ensure<S, kNT>(st, ring, ring_lds, g ? s0 + 16u * g : p, gend - 1u, lane);
     uint4 val = zero ? z4 : ring16<S>(ring, s0 + 16u * kk);
     if (g == 0 && head && lane == 0) val = splice_lo(carry, val, head);
     const bool skip0 = shared0 && g == 0;
@@ -135,14 +144,16 @@ __device__ __forceinline__ bool seg_copy(const lds_u8* ring, uint64_t base, uint
       prev_w = __builtin_amdgcn_readlane(vout.w, 63);
     }
     if (tail && nch - 1 - g < 64u) last = readlane4(val, int(nch - 1 - g));
+    if constexpr ((kV & 2) != 0) pump<S, kNT>(st, ring_lds, gend >> 10, lane);
   }
   carry = last;
   return utf8 ? __any(bad) != 0 : false;
 }
 
-// The column table of a lean-path workgroup, ahead of the waves' LDS (dynamic, ncols entries).
+// The column table of a lean-path workgroup, ahead of the waves' LDS (dynamic, ncols entries;
+// 256-byte pieces: the early prologue copies it with one 4-byte LDS-DMA load per lane and piece).
 __host__ __device__ __forceinline__ uint32_t seg_cols_lds(int ncols) {
-  return (uint32_t(ncols) * uint32_t(sizeof(DevCol)) + 15u) & ~15u;
+  return (uint32_t(ncols) * uint32_t(sizeof(DevCol)) + 255u) & ~255u;
 }
 
 // W waves per workgroup (one run each): fewer waves per workgroup waste less LDS per CU.
@@ -155,7 +166,27 @@ __device__ __forceinline__ uint64_t seg_clock() {
   return c;
 }
 
-template <int S, bool kNT, int W, bool kProf = false>
+// The run's bytes: one range starting on a 128-byte line, its first S KiB in flight at once.
+template <int S, bool kNT>
+__device__ __forceinline__ uint64_t seg_stream_start(Stream& st, const TileRun& r, uint64_t batch,
+                                                     uint32_t ring_lds, int lane) {
+  const uint64_t sbase = (batch + r.stream) & ~uint64_t(127);
+  st.base = reinterpret_cast<const uint4*>(sbase);
+  st.nq = uint32_t((batch + r.stream + r.bytes - sbase + 15) >> 4);
+  st.nslots = (st.nq + 63) >> 6;
+  st.issued = 0;
+  st.op_at = 0;
+  st.mirrored = 0xffffffffu;
+  st.landed = 0;
+  pump<S, kNT>(st, ring_lds, 0, lane);
+  return sbase;
+}
+
+// kV (measurement variants, MDSX_TUNE sv; 0 the default): bit 1 -- the early prologue: the run's
+// record loaded and its ring loads issued before the column table is in LDS (each wave copies the
+// table itself by LDS-DMA and waits for exactly those loads; no workgroup barrier), so a wave's
+// first sample waits for two dependent memory round trips instead of three; bits 2 and 4: seg_copy.
+template <int S, bool kNT, int W, bool kProf = false, int kV = 0>
 __global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint64_t t_start = kProf ? seg_clock() : 0;
@@ -163,18 +194,44 @@ __global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) 
   const int t = threadIdx.x, lane = t & 63;
   const int wave = W == 1 ? 0 : __builtin_amdgcn_readfirstlane(t >> 6);
   MDSX_L DevCol* s_cols = (MDSX_L DevCol*)smem;
-  for (int c = t; c < a.ncols; c += 64 * W) s_cols[c] = a.cols[c];
-  __syncthreads();
-  const MDSX_L DevCol* cols = (const MDSX_L DevCol*)s_cols;
   // XCD-contiguous runs: the line two neighbouring runs share (read: a run starts on a 128-byte
   // line; written: partial output chunks) meets in one L2
   const uint32_t blk = (a.xcd_order & kXcdSeg) ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
   const uint32_t tile = blk * W + uint32_t(wave);
-  if (tile >= a.ntiles) return;  // wave-uniform; no barrier below
   const int TR = a.tile_rows;
   const int ncols = a.ncols, nvar = a.nvar;
   uint8_t* wl = smem + seg_cols_lds(ncols) + size_t(wave) * seg_wave_lds(S, TR, nvar, a.seg_small);
-  const TileRun r = a.tile_run[tile];
+  const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((const MDSX_L uint8_t*)wl)));
+  const uint64_t batch = reinterpret_cast<uint64_t>(a.batch);
+  Stream st;
+  st.ops = 0;
+  uint64_t sbase = 0;
+  TileRun r;
+  if constexpr ((kV & 1) != 0) {
+    if (tile >= a.ntiles) return;  // wave-uniform; no barrier below
+    const uint32_t cbytes = uint32_t(ncols) * uint32_t(sizeof(DevCol));
+    // the table in the kernel-argument segment (DevArgs is the kernel's only argument; taking
+    // a.cols's address would copy the argument block to scratch)
+    const uint8_t* csrc = (const uint8_t*)__builtin_amdgcn_kernarg_segment_ptr() +
+                          offsetof(DevArgs, cols);
+    const uint32_t cl = __builtin_amdgcn_readfirstlane(
+        static_cast<uint32_t>(reinterpret_cast<uintptr_t>((const MDSX_L uint8_t*)smem)));
+    for (uint32_t q = 0; q < cbytes; q += 256u) {  // identical bytes from every wave
+      glds4(csrc + q + 4u * uint32_t(lane), cl + q);
+      ++st.ops;
+    }
+    r = a.tile_run[tile];
+    if (r.fast & 2) sbase = seg_stream_start<S, kNT>(st, r, batch, ring_lds, lane);
+    wait_vm_exact16(st.issued);  // the table's loads landed (issued before the ring's)
+  } else {
+    for (int c = t; c < a.ncols; c += 64 * W) s_cols[c] = a.cols[c];
+    __syncthreads();
+    if (tile >= a.ntiles) return;  // wave-uniform; no barrier below
+    r = a.tile_run[tile];
+    if (r.fast & 2) sbase = seg_stream_start<S, kNT>(st, r, batch, ring_lds, lane);
+  }
+  const MDSX_L DevCol* cols = (const MDSX_L DevCol*)s_cols;
   if (!(r.fast & 2)) {
     run_body<S, kNT>(a, cols, tile, r, wl, lane);
     return;
@@ -183,23 +240,7 @@ __global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) 
   MDSX_L uint32_t* obuf = (MDSX_L uint32_t*)(wl + S * 1024 + kMirror);  // [nvar][TR]
   MDSX_L uint8_t* fbuf = (MDSX_L uint8_t*)(wl + S * 1024 + kMirror + nvar * TR * 4);  // [nvar][TR]
   MDSX_L uint8_t* sbuf = (MDSX_L uint8_t*)(wl + run_wave_lds(S, TR, nvar));  // small columns
-  const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(
-      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((const MDSX_L uint8_t*)wl)));
-
-  // the run's bytes: one range starting on a 128-byte line, its first S KiB in flight at once
-  const uint64_t batch = reinterpret_cast<uint64_t>(a.batch);
   const uint64_t shard = batch + (r.offs - 4ull - 4ull * r.r0);  // the shard file's first byte
-  const uint64_t sbase = (batch + r.stream) & ~uint64_t(127);
-  Stream st;
-  st.base = reinterpret_cast<const uint4*>(sbase);
-  st.nq = uint32_t((batch + r.stream + r.bytes - sbase + 15) >> 4);
-  st.nslots = (st.nq + 63) >> 6;
-  st.issued = 0;
-  st.ops = 0;
-  st.op_at = 0;
-  st.mirrored = 0xffffffffu;
-  st.landed = 0;
-  pump<S, kNT>(st, ring_lds, 0, lane);
   const int n = int(r.nrows);
   const uint64_t row0 = r.row0;
   // lane j holds offsets[r0 + j] (j <= n)
@@ -248,7 +289,10 @@ __global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) 
     const uint32_t sp = uint32_t(shard + b - sbase);  // stream position of the sample
     uint64_t t_w0 = 0;
     if constexpr (kProf) t_w0 = seg_clock();
-    ensure<S, kNT>(st, ring, ring_lds, sp, sp + size + 15u, lane);  // ALL of the sample's bytes
+    if constexpr ((kV & 4) != 0)  // the heads; every value's bytes are waited for step by step
+      ensure<S, kNT>(st, ring, ring_lds, sp, sp + min(size, hv) + 3u, lane);
+    else
+      ensure<S, kNT>(st, ring, ring_lds, sp, sp + size + 15u, lane);  // ALL of the sample's bytes
     if constexpr (kProf) {
       const uint64_t now = seg_clock();
       if (j == 0) t_first = now - t_start;
@@ -265,28 +309,39 @@ __global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) 
     if (!ok && lane == 0) report_decode(a, MDSX_E_BOUNDS, int(r.shard), int(r.r0 + j), -1);
     const uint32_t pos = sp + hv + incl - lc;  // stream position of the column's value
     const uint32_t clen = ok ? len : (vi >= 0 ? 0u : rb);
-    if (small)
-      lds_put(sbuf + soff + uint32_t(j) * rb, ok ? ring16<S>(ring, pos) : make_uint4(0, 0, 0, 0),
-              rb);
+    if constexpr ((kV & 4) == 0) {
+      if (small)
+        lds_put(sbuf + soff + uint32_t(j) * rb,
+                ok ? ring16<S>(ring, pos) : make_uint4(0, 0, 0, 0), rb);
+    }
     if (vi >= 0) {
       obuf[vi * TR + j] = cur;
       if ((meta >> 8) & 1u) fbuf[vi * TR + j] = 0;
     }
-    // the wide columns, in column order = stream order
-    uint64_t wm = wide_mask;
+    // the wide columns (kV bit 4: and the small ones), in column order = stream order
+    uint64_t wm = (kV & 4) ? (wide_mask | small_mask) : wide_mask;
     while (wm) {
       const int c = __builtin_ctzll(wm);
       wm &= wm - 1;
+      const uint32_t p = uint32_t(__builtin_amdgcn_readlane(int(pos), c));
+      if constexpr ((kV & 4) != 0) {
+        if ((small_mask >> c) & 1ull) {
+          const uint32_t w = uint32_t(__builtin_amdgcn_readlane(int(rb), c));
+          if (ok) ensure<S, kNT>(st, ring, ring_lds, p, p + w - 1u, lane);
+          const uint4 v = ok ? ring16<S>(ring, p) : make_uint4(0, 0, 0, 0);
+          if (lane == c) lds_put(sbuf + soff + uint32_t(j) * w, v, w);
+          continue;
+        }
+      }
       const uint32_t l = uint32_t(__builtin_amdgcn_readlane(int(clen), c));
       if (l == 0) continue;
       const uint32_t d = uint32_t(__builtin_amdgcn_readlane(int(cur), c));
-      const uint32_t p = uint32_t(__builtin_amdgcn_readlane(int(pos), c));
       const uint32_t mc = uint32_t(__builtin_amdgcn_readlane(int(meta), c));
       const uint32_t cs = uint32_t(__builtin_amdgcn_readlane(int(cst), c));
       uint4 cy = (d & 15u) ? readlane4(carry, c) : make_uint4(0, 0, 0, 0);
       const bool utf8 = (mc >> 8) & 1u;
-      const bool bad = seg_copy<S, kNT>(ring, readlane64(base, c), cs, d, l, p, utf8, !ok, cy,
-                                        st.ops, lane);
+      const bool bad = seg_copy<S, kNT, kV>(st, ring, ring_lds, readlane64(base, c), cs, d, l, p,
+                                            utf8, !ok, cy, lane);
       if (lane == c) {
         cur = d + l;
         carry = cy;
@@ -373,6 +428,21 @@ int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
   MDSX_SEG_CASE(8, false, WV)  \
   MDSX_SEG_CASE(16, true, WV)  \
   MDSX_SEG_CASE(16, false, WV)
+    if (plan->seg_var) {  // measurement variants (7 KiB ring, nt, 2 waves)
+      if (a.run_slots != 7 || !plan->run_nt || W != 2)
+        return mdsx::fail(MDSX_E_ARG, "mdsx: seg variants: run=7, rnt=1, swg=2 only");
+#define MDSX_SEG_V(V)                                                                         \
+  if (plan->seg_var == V) {                                                                   \
+    mdsx::set_last_kernel("seg_decode_kernel<7, true, 2, false, " #V ">");                   \
+    hipLaunchKernelGGL((seg_decode_kernel<7, true, 2, false, V>), dim3(sgrid), dim3(128), slds, \
+                       s, a);                                                                 \
+    return hip_check(hipGetLastError(), "seg_decode_kernel launch");                          \
+  }
+      MDSX_SEG_V(1) MDSX_SEG_V(2) MDSX_SEG_V(3) MDSX_SEG_V(4) MDSX_SEG_V(5) MDSX_SEG_V(6)
+      MDSX_SEG_V(7)
+#undef MDSX_SEG_V
+      return mdsx::fail(MDSX_E_ARG, "mdsx: seg variant out of range");
+    }
     if (plan->stage_debug & 64) {  // measurement only: the per-wave stamps (7 KiB ring, nt, 2)
       if (a.run_slots != 7 || !plan->run_nt || W != 2)
         return mdsx::fail(MDSX_E_ARG, "mdsx: seg stamps: run=7, rnt=1, swg=2 only");

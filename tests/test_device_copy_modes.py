@@ -47,6 +47,11 @@ MODES = {
     'seg8_wg1': 'run=8,seg=1,rmin=0,swg=1',  # one wave (run) per workgroup
     'seg8_wg4': 'run=8,seg=1,rmin=0,swg=4',  # four (the default is two)
     'seg8_xcd0': 'run=8,seg=1,rmin=0,xcd=0',  # runs in launch order (default: XCD-contiguous ranges)
+    # the lean path's measured variants (mdsx_run.hip kV): early prologue, per-step slot release,
+    # per-step waits
+    'seg7_v1': 'run=7,seg=1,rmin=0,sv=1',
+    'seg7_v3': 'run=7,seg=1,rmin=0,sv=3',
+    'seg7_v7': 'run=7,seg=1,rmin=0,sv=7',
     'rows': 'rows=32,rmin=1000000000',  # the row-parallel decode (mdsx_rows.hip) for every size
     'rows_auto': 'rows=-1,rmin=1000000000',  # ... its tiles and stage sized per batch
     'rows_small': 'rows=2,rmin=1000000000',  # a 2 KiB stage: windows and HBM-direct samples

@@ -28,6 +28,8 @@ MODES = {
     'seg': 'run=4,seg=1,rmin=0,rkb=8',  # ... its lean path where a sample fits the 4 KiB ring
     'seg16': 'run=16,seg=1,rmin=0,rkb=64',
     'seg7': 'run=7,seg=1,rmin=0,rkb=12',  # a ring of 7 slots (modulo addressing)
+    'seg7_v7': 'run=7,seg=1,rmin=0,rkb=12,sv=7',  # ... its early prologue, per-step release / waits
+    'seg7_v3': 'run=7,seg=1,rmin=0,sv=3',  # ... early prologue and per-step release, 2-sample runs
     'seg_wg4': 'run=8,seg=1,rmin=0,swg=4',  # four waves per workgroup (the default is two)
     'rows_small': 'rows=2,rmin=1000000000',  # row-parallel, 2 KiB stage (windows, huge rows)
     'rows_pipe': 'rows=4,rpipe=5,rmin=1000000000',  # ... two stages, next tile's DMA in flight
