@@ -161,6 +161,15 @@ def gen_config_a(ref: str):
     return {'number': 'int', 'words': 'str'}, samples, {'size_limit': 10240}
 
 
+def gen_config_a2(ref: str):
+    """A second stream of config A's schema (multi-stream loader order, make_loader_fixtures)."""
+    sys.path.insert(0, os.path.join(ref, 'regression'))
+    mod = importlib.import_module('synthetic_dataset')
+    ds = mod.NumberAndSayDataset(num_samples=3_000, seed=4242)
+    samples = list(ds)
+    return {'number': 'int', 'words': 'str'}, samples, {'size_limit': 10240}
+
+
 def gen_sequence():
     samples = [{'id': f'{i:06}', 'sample': 3 * i} for i in range(117)]
     return {'id': 'str', 'sample': 'int'}, samples, {'size_limit': 1 << 8}
@@ -432,6 +441,7 @@ def main() -> None:
     specs = {
         'kat': (gen_kat, True),
         'config_a': (lambda: gen_config_a(args.reference), False),
+        'config_a2': (lambda: gen_config_a2(args.reference), False),
         'sequence': (gen_sequence, True),
         'config_b_small': (gen_config_b_small, False),
         'config_c_small': (gen_config_c_small, False),

@@ -40,20 +40,45 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
+# Two streams of config A's schema (config_a: 10 000 samples, config_a2: 3 000), each drawn by a
+# proportion of the epoch (stream.py:92-140: config_a sub-sampled, config_a2 repeated).
+TWO_STREAMS = [('config_a', {'proportion': 0.6}), ('config_a2', {'proportion': 0.4})]
+_MS = dict(shuffle=True, shuffle_algo='py1e', shuffle_seed=23, num_canonical_nodes=2,
+           batch_size=16, shuffle_block_size=1000)
+
 SETTINGS = [
     # name, StreamingDataset kwargs, ranks (one node), DataLoader workers, resume after batches
+    # [, streams: (golden dir, Stream kwargs) -- default the one local dir config_a]
     ('py1e_r1w2', dict(shuffle=True, shuffle_algo='py1e', shuffle_seed=17, num_canonical_nodes=2,
                        batch_size=16, shuffle_block_size=1000), 1, 2, 21),
     ('noshuffle_r1w3', dict(shuffle=False, num_canonical_nodes=1, batch_size=16), 1, 3, 10),
     ('py1s_r2w2', dict(shuffle=True, shuffle_algo='py1s', shuffle_seed=5, num_canonical_nodes=4,
                        batch_size=8, shuffle_block_size=2048), 2, 2, 25),
+    # round 5: multi-stream datasets under every batching method (batching/__init__.py:21-26)
+    ('ms_random_r1w2', dict(_MS, batching_method='random'), 1, 2, 15, TWO_STREAMS),
+    ('ms_stratified_r1w2', dict(_MS, batching_method='stratified'), 1, 2, 12, TWO_STREAMS),
+    ('ms_per_stream_r1w2', dict(_MS, batching_method='per_stream'), 1, 2, 10, TWO_STREAMS),
+    ('ms_device_per_stream_r2w2', dict(_MS, batching_method='device_per_stream', batch_size=8),
+     2, 2, 20, TWO_STREAMS),
+    # replication: two ranks see the same samples (dataset.py:370-374, world.py:117-148)
+    ('repl2_r2w2', dict(shuffle=True, shuffle_algo='py1s', shuffle_seed=5, num_canonical_nodes=2,
+                        batch_size=8, shuffle_block_size=2048, replication=2), 2, 2, 25),
+    ('ms_repl2_r2w2', dict(_MS, batching_method='per_stream', batch_size=8, replication=2), 2, 2,
+     20, TWO_STREAMS),
 ]
 
 
 def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(('127.0.0.1', 0))
-        return s.getsockname()[1]
+    """A free port below the kernel's ephemeral range (32768+), where no OS-assigned socket can
+    take it before the reference's rank 0 binds its TCP store."""
+    for port in range(24000 + 100 * (os.getpid() % 50), 32000):
+        with socket.socket() as s:
+            try:
+                s.bind(('127.0.0.1', port))
+            except OSError:
+                continue
+            return port
+    raise RuntimeError('no free port')
 
 
 def run_rank(spec: dict) -> None:
@@ -63,12 +88,17 @@ def run_rank(spec: dict) -> None:
     from streaming.base.batching import generate_work
     from streaming.base.dataloader import StreamingDataLoader
     from streaming.base.dataset import StreamingDataset
+    from streaming.base.stream import Stream
     from streaming.base.util import clean_stale_shared_memory
     from streaming.base.world import World
 
     rank, ranks, workers = spec['rank'], spec['ranks'], spec['workers']
     clean_stale_shared_memory()
-    ds = StreamingDataset(local=spec['local'], **spec['kwargs'])
+    if spec['streams']:
+        streams = [Stream(local=os.path.join(spec['local'], d), **kw) for d, kw in spec['streams']]
+        ds = StreamingDataset(streams=streams, **spec['kwargs'])
+    else:
+        ds = StreamingDataset(local=spec['local'], **spec['kwargs'])
     bs = spec['kwargs']['batch_size']
     loader = StreamingDataLoader(ds, batch_size=bs, num_workers=workers)
     if spec['state'] is not None:
@@ -84,7 +114,10 @@ def run_rank(spec: dict) -> None:
             state = loader.state_dict()
     epoch, sie = (0, 0) if spec['state'] is None else (spec['state']['epoch'],
                                                        spec['state']['sample_in_epoch'])
-    world = World(1, ranks, workers, rank * workers)
+    # the partition World of this rank's W loader workers (replication: the replicated rank,
+    # dataset.py:370-374), as device_iter lays it out (streaming_amd/plugin.py _loader_work)
+    pw = ds._parallel_rank_world
+    world = World(pw.num_nodes, pw.ranks_per_node, workers, pw.rank * workers)
     ids = generate_work(ds.batching_method, ds, world, epoch, sie)
     np.save(spec['ids_out'], ids.astype(np.int64), allow_pickle=False)
     with open(spec['out'], 'w') as f:
@@ -92,13 +125,14 @@ def run_rank(spec: dict) -> None:
                    'state': state}, f)
 
 
-def run_phase(args, name, kwargs, ranks, workers, resume_batches, local, state, work):
+def run_phase(args, name, kwargs, ranks, workers, resume_batches, local, state, work,
+              streams=None):
     port = _free_port()
     procs, outs = [], []
     for rank in range(ranks):
         out = os.path.join(work, f'{name}.{rank}.{"resume" if state else "start"}.json')
         spec = {'reference': args.reference, 'rank': rank, 'ranks': ranks, 'workers': workers,
-                'local': local, 'kwargs': kwargs, 'state': state,
+                'local': local, 'kwargs': kwargs, 'state': state, 'streams': streams,
                 'resume_batches': resume_batches, 'out': out, 'ids_out': out + '.npy'}
         env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(ranks), LOCAL_RANK=str(rank),
                    LOCAL_WORLD_SIZE=str(ranks), MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port),
@@ -122,6 +156,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--reference', default='/root/reference')
     ap.add_argument('--rank-spec', default=None)
+    ap.add_argument('--only', default='', help='comma-separated settings to (re)record; the '
+                    'others are kept from the existing fixture')
     args = ap.parse_args()
     if args.rank_spec:
         run_rank(json.loads(args.rank_spec))
@@ -129,19 +165,35 @@ def main():
     out_dir = os.path.join(HERE, 'order')
     os.makedirs(out_dir, exist_ok=True)
     arrays, meta = {}, {'dataset': 'config_a', 'settings': []}
+    only = set(filter(None, args.only.split(',')))
+    if only:
+        arrays = dict(np.load(os.path.join(out_dir, 'loader.npz'), allow_pickle=False))
+        with open(os.path.join(out_dir, 'loader.json')) as f:
+            meta = json.load(f)
+        meta['settings'] = [e for e in meta['settings'] if e['name'] not in only]
+        arrays = {k: v for k, v in arrays.items() if k.split('.')[0] not in only}
     work = tempfile.mkdtemp(prefix='loader_')
     try:
-        for name, kwargs, ranks, workers, resume_batches in SETTINGS:
+        for name, kwargs, ranks, workers, resume_batches, *rest in SETTINGS:
+            if only and name not in only:
+                continue
+            streams = rest[0] if rest else None
             local = os.path.join(work, name)
-            shutil.copytree(os.path.join(HERE, 'config_a'), local)
+            if streams:
+                for d, _ in streams:
+                    shutil.copytree(os.path.join(HERE, d), os.path.join(local, d))
+            else:
+                shutil.copytree(os.path.join(HERE, 'config_a'), local)
             start = run_phase(args, name, kwargs, ranks, workers, resume_batches, local, None,
-                              work)
+                              work, streams)
             state = start[0]['state']
             assert all(r['state'] == state for r in start), [r['state'] for r in start]
             resumed = run_phase(args, name, kwargs, ranks, workers, resume_batches, local, state,
-                                work)
+                                work, streams)
             entry = {'name': name, 'kwargs': kwargs, 'ranks': ranks, 'workers': workers,
                      'resume_batches': resume_batches, 'state_dict': state, 'per_rank': []}
+            if streams:
+                entry['streams'] = [{'dir': d, 'kwargs': kw} for d, kw in streams]
             for rank, (a, b) in enumerate(zip(start, resumed)):
                 arrays[f'{name}.r{rank}.start'] = a['ids']
                 arrays[f'{name}.r{rank}.resume'] = b['ids']
@@ -154,6 +206,8 @@ def main():
                   flush=True)
     finally:
         shutil.rmtree(work, ignore_errors=True)
+    order = [name for name, *_ in SETTINGS]
+    meta['settings'].sort(key=lambda e: order.index(e['name']) if e['name'] in order else 99)
     np.savez_compressed(os.path.join(out_dir, 'loader.npz'), **arrays)
     with open(os.path.join(out_dir, 'loader.json'), 'w') as f:
         json.dump(meta, f, indent=1, sort_keys=True)

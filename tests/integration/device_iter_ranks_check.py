@@ -9,7 +9,11 @@ StreamingDataLoader(num_workers=2) on this rank (tests/golden/order/loader.json,
 py1s_r2w2), then a checkpoint after the fixture's batch count through DeviceBatches.state_dict.
 Phase ``resume``: a new dataset after load_state_dict of that state. Prints one JSON line.
 
-    python tests/integration/device_iter_ranks_check.py <reference dir> <local dir> <phase> [state]
+    python tests/integration/device_iter_ranks_check.py <reference dir> <local dir> <setting>
+        <phase> [state]
+
+``<setting>``: a two-rank setting of tests/golden/order/loader.json; ``<local dir>`` holds the
+copy of its streams' golden dirs (config_a itself for a one-stream setting).
 """
 import hashlib
 import json
@@ -24,7 +28,7 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, 'tests', 'golden'))
 
 
-def main(ref: str, local: str, phase: str, state_json: str = '') -> None:
+def main(ref: str, local: str, name: str, phase: str, state_json: str = '') -> None:
     from make_golden import boot_reference
     boot_reference(ref)
     from streaming.base.dataset import StreamingDataset
@@ -35,14 +39,23 @@ def main(ref: str, local: str, phase: str, state_json: str = '') -> None:
     from streaming_amd.plugin import DeviceBatches, device_iter, register_device_stream
 
     rank = int(os.environ['RANK'])
-    register_device_stream('mdsx')
+    DeviceStream = register_device_stream('mdsx')
     with open(os.path.join(REPO, 'tests', 'golden', 'order', 'loader.json')) as f:
-        st = {s['name']: s for s in json.load(f)['settings']}['py1s_r2w2']
+        st = {s['name']: s for s in json.load(f)['settings']}[name]
     pr = st['per_rank'][rank]
     bs, W = st['kwargs']['batch_size'], st['workers']
-    with open(os.path.join(local, 'index.json')) as f:
-        infos = json.load(f)['shards']
-    readers = [OracleMDSReader(local, None, info) for info in infos]
+    dirs = [os.path.join(local, e['dir']) for e in st.get('streams', [])] or [local]
+    readers = []
+    for d in dirs:
+        with open(os.path.join(d, 'index.json')) as f:
+            readers += [OracleMDSReader(d, None, info) for info in json.load(f)['shards']]
+
+    def dataset():
+        if st.get('streams'):  # two streams, each a device stream (the plugin's Stream subclass)
+            return StreamingDataset(streams=[
+                DeviceStream(local=os.path.join(local, e['dir']), **e['kwargs'])
+                for e in st['streams']], **st['kwargs'])
+        return StreamingDataset(local=local, stream_name='mdsx', **st['kwargs'])
 
     class OracleGather(DeviceSampleGather):
 
@@ -62,11 +75,11 @@ def main(ref: str, local: str, phase: str, state_json: str = '') -> None:
     clean_stale_shared_memory()  # collective under WORLD_SIZE=2: every rank calls it
     res = {'rank': rank}
     if phase == 'start':
-        ds = StreamingDataset(local=local, stream_name='mdsx', **st['kwargs'])
+        ds = dataset()
         d, sizes = run(device_iter(ds, bs, num_workers=W, gather=OracleGather(ds.shards)))
         res['start'] = d == pr['iter_start_sha256']
         res['start_sizes'] = sizes == pr['start_batch_sizes']
-        ds2 = StreamingDataset(local=local, stream_name='mdsx', **st['kwargs'])
+        ds2 = dataset()
         batches = DeviceBatches(ds2, bs, num_workers=W, gather=OracleGather(ds2.shards))
         it = iter(batches)
         for _ in range(st['resume_batches']):
@@ -76,7 +89,7 @@ def main(ref: str, local: str, phase: str, state_json: str = '') -> None:
         res['state'] = state
         ds2._iterator.exit()
     else:
-        ds = StreamingDataset(local=local, stream_name='mdsx', **st['kwargs'])
+        ds = dataset()
         ds.load_state_dict(json.loads(state_json))
         d, sizes = run(device_iter(ds, bs, num_workers=W, gather=OracleGather(ds.shards)))
         res['resume'] = d == pr['iter_resume_sha256']

@@ -41,7 +41,7 @@ def main(ref: str, scratch: str) -> None:
             h.update(w.encode('utf-8'))
         return h.hexdigest()
 
-    register_device_stream('mdsx')
+    DeviceStream = register_device_stream('mdsx')
     with open(os.path.join(REPO, 'tests', 'golden', 'order', 'config_a.json')) as f:
         settings = {s['name']: s for s in json.load(f)['settings']}
     out = {}
@@ -99,23 +99,38 @@ def main(ref: str, scratch: str) -> None:
     # against the reference's StreamingDataLoader(num_workers=W), start, checkpoint and resume
     with open(os.path.join(REPO, 'tests', 'golden', 'order', 'loader.json')) as f:
         loaders = {s['name']: s for s in json.load(f)['settings']}
-    for name in ('py1e_r1w2', 'noshuffle_r1w3'):
+    one_rank = [n for n, st in loaders.items() if st['ranks'] == 1]
+    for name in one_rank:
         st = loaders[name]
         pr = st['per_rank'][0]
         bs, W = st['kwargs']['batch_size'], st['workers']
         clean_stale_shared_memory()
         local = os.path.join(scratch, name)
-        shutil.copytree(os.path.join(REPO, 'tests', 'golden', 'config_a'), local)
-        with open(os.path.join(local, 'index.json')) as f:
-            infos = json.load(f)['shards']
-        OracleGather.readers = [OracleMDSReader(local, None, info) for info in infos]
+        dirs = [e['dir'] for e in st.get('streams', [])]
+        readers = []
+        for d in dirs or ['config_a']:
+            dst = os.path.join(local, d) if dirs else local
+            shutil.copytree(os.path.join(REPO, 'tests', 'golden', d), dst)
+            with open(os.path.join(dst, 'index.json')) as f:
+                readers += [OracleMDSReader(dst, None, info) for info in json.load(f)['shards']]
+        OracleGather.readers = readers
+
+        def dataset():
+            if dirs:  # two streams, each a device stream (the plugin's Stream subclass)
+                return StreamingDataset(streams=[
+                    DeviceStream(local=os.path.join(local, e['dir']), **e['kwargs'])
+                    for e in st['streams']], **st['kwargs'])
+            return StreamingDataset(local=local, stream_name='mdsx', **st['kwargs'])
+
         res = {}
-        ds = StreamingDataset(local=local, stream_name='mdsx', **st['kwargs'])
+        ds = dataset()
+        res['device_readers'] = all(type(s).__module__ == 'streaming_amd.reader'
+                                    for s in ds.shards)
         numbers, words, sizes = run(device_iter(ds, bs, num_workers=W,
                                                 gather=OracleGather(ds.shards)))
         res['start'] = digest(numbers, words) == pr['iter_start_sha256']
         res['start_sizes'] = sizes == pr['start_batch_sizes']
-        ds2 = StreamingDataset(local=local, stream_name='mdsx', **st['kwargs'])
+        ds2 = dataset()
         batches = DeviceBatches(ds2, bs, num_workers=W, gather=OracleGather(ds2.shards))
         it = iter(batches)
         for _ in range(st['resume_batches']):
@@ -125,7 +140,7 @@ def main(ref: str, scratch: str) -> None:
         ds2._iterator.exit()
         del it, batches, ds2, ds
         clean_stale_shared_memory()
-        ds3 = StreamingDataset(local=local, stream_name='mdsx', **st['kwargs'])
+        ds3 = dataset()
         ds3.load_state_dict(state)
         numbers, words, sizes = run(device_iter(ds3, bs, num_workers=W,
                                                 gather=OracleGather(ds3.shards)))

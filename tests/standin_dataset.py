@@ -55,6 +55,14 @@ class World:
     def detect_workers(self) -> 'World':  # no DataLoader worker processes here
         return World(self.num_nodes, self.ranks_per_node, 1, self.rank)
 
+    def replicate(self, replication: int) -> 'World':
+        """world.py:117-148: the World of the replication group this rank iterates as."""
+        rank = self.rank // replication
+        num_ranks = self.num_ranks // replication
+        worker = rank * self.workers_per_rank + self.worker_of_rank
+        num_nodes = num_ranks // self.ranks_per_node if num_ranks % self.ranks_per_node == 0 else 1
+        return World(num_nodes, num_ranks // num_nodes, self.workers_per_rank, worker)
+
 
 def generate_work(batching_method, dataset, world, epoch, sample_in_epoch):
     """batching/__init__.py:28-45: the stand-in returns the epoch's recorded 5-D id array."""
@@ -63,19 +71,23 @@ def generate_work(batching_method, dataset, world, epoch, sample_in_epoch):
 
 class StandInDataset:
 
-    def __init__(self, shards, work, epoch_work=None, world=(1, 1, 0), batch_size=None) -> None:
+    def __init__(self, shards, work, epoch_work=None, world=(1, 1, 0), batch_size=None,
+                 replication=None, batching_method='random') -> None:
         """``work(epoch, sample_in_epoch)``: this worker's flattened ids (``-1`` padding kept);
         ``epoch_work(world, epoch, sample_in_epoch)``: ``generate_work``'s 5-D array for a World
-        (multi-worker iteration); ``world``: (nodes, ranks per node, rank)."""
+        (multi-worker iteration); ``world``: (nodes, ranks per node, rank); ``replication``: as
+        StreamingDataset's (dataset.py:370-374: the parallel rank World replicated)."""
         self.shards = shards
         self._work = work
         self._epoch_work = epoch_work
         self.batch_size = batch_size
-        self.batching_method = 'random'
-        self.replication = None
+        self.batching_method = batching_method
+        self.replication = replication
         self._shard_access_times = np.zeros(len(shards), np.uint64)
         nodes, rpn, rank = world
-        self._unique_rank_world = self._parallel_rank_world = World(nodes, rpn, 1, rank)
+        self._unique_rank_world = World(nodes, rpn, 1, rank)
+        self._parallel_rank_world = (self._unique_rank_world.replicate(replication)
+                                     if replication is not None else World(nodes, rpn, 1, rank))
         self.next_epoch = 0
         self._resume = None
         self.prepared = []

@@ -82,18 +82,32 @@ def test_device_iter_reprepares_an_evicted_shard(tmp_path):
     assert len(numbers) == 10_000 and 0 in standin.prepared
 
 
-@pytest.mark.parametrize('name,rank', [('py1e_r1w2', 0), ('noshuffle_r1w3', 0), ('py1s_r2w2', 0),
-                                       ('py1s_r2w2', 1)])
+def _loader_cases():
+    from tests.test_plugin_iter import CASES
+    return CASES
+
+
+@pytest.mark.parametrize('name,rank', _loader_cases())
 def test_device_iter_multi_worker_loader(name, rank):
     """device_iter(num_workers=W): the W worker partitions gathered on the GPU and interleaved as
     torch's DataLoader returns them give, on each rank, the samples and batch sizes the REAL
     reference's StreamingDataLoader(num_workers=W) yielded (tests/golden/order/loader.json), and
-    DeviceBatches checkpoints (this rank's count times the ranks) and resumes as it does."""
-    from tests.test_plugin_iter import _standin, loader_settings
+    DeviceBatches checkpoints (this rank's count times the ranks, // replication) and resumes as
+    it does -- on one stream and on two streams drawn by proportion under every batching method
+    (random, stratified, per_stream, device_per_stream), and with replication=2."""
+    from tests.test_plugin_iter import _standin, loader_settings, stream_dirs
     st = loader_settings()[name]
     pr = st['per_rank'][rank]
     bs, W = st['kwargs']['batch_size'], st['workers']
-    ds = LocalDataset(gu.GOLDEN + '/config_a', decoded_cache_bytes=1 << 20)
+    shards = []
+    for d in stream_dirs(st):  # the dataset's shards: stream by stream, as StreamingDataset's
+        shards += LocalDataset(gu.GOLDEN + '/' + d, decoded_cache_bytes=1 << 20).shards
+
+    class _DS:
+        pass
+
+    ds = _DS()
+    ds.shards = shards
     standin = _standin(name, rank, ds.shards)
     numbers, words, sizes = _rows(device_iter(standin, bs, num_workers=W))
     assert sizes == pr['start_batch_sizes']

@@ -45,11 +45,41 @@ def test_loader_batches_reproduce_the_reference_loader(name, rank, tag):
     st = loader_settings()[name]
     pr = st['per_rank'][rank]
     ids = loader_ids()[f'{name}.r{rank}.{tag}']
-    batches = loader_batches(ids, 0, rank, st['workers'], st['kwargs']['batch_size'])
+    prank = _parallel_rank(st, rank)
+    batches = loader_batches(ids, 0, prank, st['workers'], st['kwargs']['batch_size'])
     flat = np.concatenate(batches)
-    numbers, words = oracle_rows()
+    numbers, words = stream_rows(st)
     assert [len(b) for b in batches] == pr[f'{tag}_batch_sizes']
     assert digest(numbers[flat], [words[i] for i in flat]) == pr[f'iter_{tag}_sha256']
+
+
+def stream_dirs(st):
+    """The golden dirs of a loader setting's streams, in the dataset's shard order."""
+    return [s['dir'] for s in st.get('streams', [])] or ['config_a']
+
+
+def _parallel_rank(st, rank):
+    """The rank a replicated rank iterates as (world.py:117-148, one node)."""
+    return rank // (st['kwargs'].get('replication') or 1)
+
+
+_ROWS = {}
+
+
+def stream_rows(st):
+    """(number, words) of every sample of the setting's streams in global id order (oracle)."""
+    key = tuple(stream_dirs(st))
+    if key not in _ROWS:
+        numbers, words = [], []
+        for d in key:
+            for info in gu.index(d)['shards']:
+                r = OracleMDSReader(os.path.join(gu.GOLDEN, d), None, info)
+                for i in range(info['samples']):
+                    s = r.get_item(i)
+                    numbers.append(s['number'])
+                    words.append(s['words'])
+        _ROWS[key] = (np.array(numbers, np.int64), words)
+    return _ROWS[key]
 
 
 class OracleGather:
@@ -71,24 +101,29 @@ class OracleGather:
         return [self.shards[int(s)].get_item(int(i)) for s, i in zip(shard, loc)]
 
 
-def _readers():
-    d = os.path.join(gu.GOLDEN, 'config_a')
-    return [OracleMDSReader(d, None, info) for info in gu.index('config_a')['shards']]
+def _readers(dirs=('config_a', )):
+    return [OracleMDSReader(os.path.join(gu.GOLDEN, d), None, info) for d in dirs
+            for info in gu.index(d)['shards']]
 
 
 def _standin(name, rank, readers):
+    """A stand-in whose generate_work returns what the reference's recorded for this setting's
+    World (the replicated one under ``replication``)."""
     st = loader_settings()[name]
     ids = loader_ids()
     resume_at = st['state_dict']['sample_in_epoch']
+    rep = st['kwargs'].get('replication')
 
     def epoch_work(world, epoch, sample_in_epoch):
-        assert world.workers_per_rank == st['workers'] and world.rank == rank
-        assert world.num_ranks == st['ranks'] and epoch == 0
+        assert world.workers_per_rank == st['workers']
+        assert world.rank == _parallel_rank(st, rank)
+        assert world.num_ranks == st['ranks'] // (rep or 1) and epoch == 0
         assert sample_in_epoch in (0, resume_at)
         return ids[f'{name}.r{rank}.{"start" if sample_in_epoch == 0 else "resume"}']
 
     return StandInDataset(readers, None, epoch_work, world=(1, st['ranks'], rank),
-                          batch_size=st['kwargs']['batch_size'])
+                          batch_size=st['kwargs']['batch_size'], replication=rep,
+                          batching_method=st['kwargs'].get('batching_method', 'random'))
 
 
 def _digest(batches):
@@ -102,7 +137,7 @@ def test_device_iter_workers_start_checkpoint_resume(name, rank):
     st = loader_settings()[name]
     pr = st['per_rank'][rank]
     bs, W = st['kwargs']['batch_size'], st['workers']
-    readers = _readers()
+    readers = _readers(stream_dirs(st))
     ds = _standin(name, rank, readers)
     batches = list(device_iter(ds, bs, num_workers=W, gather=OracleGather(readers)))
     assert [len(b) for b in batches] == pr['start_batch_sizes']
@@ -121,6 +156,28 @@ def test_device_iter_workers_start_checkpoint_resume(name, rank):
     resumed = list(device_iter(ds, bs, num_workers=W, gather=OracleGather(readers)))
     assert [len(b) for b in resumed] == pr['resume_batch_sizes']
     assert _digest(resumed) == pr['iter_resume_sha256']
+
+
+def test_replicated_ranks_see_the_same_samples():
+    """replication=2 over two ranks: the reference's loaders yielded the same samples on both
+    ranks of a replication group, and so do the recorded partitions device_iter lays out."""
+    for name, st in loader_settings().items():
+        if not st['kwargs'].get('replication'):
+            continue
+        a, b = st['per_rank']
+        assert a['iter_start_sha256'] == b['iter_start_sha256'], name
+        assert a['iter_resume_sha256'] == b['iter_resume_sha256'], name
+        ids = loader_ids()
+        assert np.array_equal(ids[f'{name}.r0.start'], ids[f'{name}.r1.start']), name
+
+
+def test_multi_stream_batching_methods_recorded():
+    """The loader fixture covers every batching method the reference dispatches
+    (batching/__init__.py:21-26) on a two-stream dataset, and replication."""
+    sts = loader_settings().values()
+    methods = {st['kwargs'].get('batching_method', 'random') for st in sts if st.get('streams')}
+    assert methods == {'random', 'stratified', 'per_stream', 'device_per_stream'}
+    assert any(st['kwargs'].get('replication') == 2 for st in sts)
 
 
 def test_state_dict_divides_by_replication():

@@ -57,28 +57,35 @@ def test_device_iter_follows_the_reference_iteration(tmp_path):
         assert all(r.values()), (name, r)
 
 
-def _free_port():
+_PORT_BASE = 20000  # below the kernel's ephemeral range (32768+): no OS-assigned port lands here
+_PORTS_PER_WORKER = 200
+
+
+def _worker_port():
+    """A free port from this pytest worker's own range (PYTEST_XDIST_WORKER gwN: ports
+    20000 + 200 N ...): no other worker and no ephemeral socket picks from it, so the port the
+    reference's rank 0 binds for its TCP-store rendezvous (dataset.py:431 -> distributed.py:128)
+    cannot be taken between this check and that bind."""
     import socket
-    with socket.socket() as s:
-        s.bind(('127.0.0.1', 0))
-        return s.getsockname()[1]
+    w = os.environ.get('PYTEST_XDIST_WORKER', 'gw0')
+    idx = int(w[2:]) if w[2:].isdigit() else 0
+    lo = _PORT_BASE + _PORTS_PER_WORKER * (idx % 60)
+    for port in range(lo, lo + _PORTS_PER_WORKER):
+        with socket.socket() as s:
+            try:
+                s.bind(('127.0.0.1', port))
+            except OSError:  # in TIME_WAIT after an earlier run of this worker
+                continue
+            return port
+    raise RuntimeError(f'no free port in {lo}..{lo + _PORTS_PER_WORKER}')
 
 
-def _ranks(script, args, tries=2):
-    """Run the two ranks; a run whose ranks hang is killed and started once more on a new port --
-    a wrong result is never retried. (Observed under pytest-xdist: the reference's
-    init_process_group waiting in the TCP store rendezvous, dataset.py:431 -> distributed.py:128,
-    the port picked by _free_port() taken by another process before rank 0 bound it.)"""
-    for attempt in range(tries):
-        try:
-            return _ranks_once(script, args)
-        except subprocess.TimeoutExpired:
-            if attempt + 1 == tries:
-                raise
+def _ranks(script, args):
+    return _ranks_once(script, args)
 
 
 def _ranks_once(script, args):
-    port = _free_port()
+    port = _worker_port()
     procs = []
     for rank in range(2):
         env = dict(os.environ, PYTHONDONTWRITEBYTECODE='1', HIP_VISIBLE_DEVICES='',
@@ -100,18 +107,31 @@ def _ranks_once(script, args):
     return outs
 
 
-def test_device_iter_two_ranks_two_workers(tmp_path):
+def _two_rank_settings():
+    with open(os.path.join(HERE, 'golden', 'order', 'loader.json')) as f:
+        return [s['name'] for s in json.load(f)['settings'] if s['ranks'] == 2]
+
+
+@pytest.mark.parametrize('name', _two_rank_settings())
+def test_device_iter_two_ranks_two_workers(tmp_path, name):
     """Two ranks (RANK / WORLD_SIZE, gloo on 127.0.0.1), each device_iter(num_workers=2) over the
     real StreamingDataset: each rank's samples equal what the reference's
     StreamingDataLoader(num_workers=2) yielded on that rank, and DeviceBatches.state_dict (this
-    rank's count times the ranks, dataloader.py:74-84) checkpoints and resumes as the reference."""
+    rank's count times the ranks, // replication, dataloader.py:74-84) checkpoints and resumes as
+    the reference -- one stream; two streams under device_per_stream / per_stream batching; and
+    replication=2 (both ranks of the group the same samples)."""
     import shutil
+    with open(os.path.join(HERE, 'golden', 'order', 'loader.json')) as f:
+        st = {s['name']: s for s in json.load(f)['settings']}[name]
     local = tmp_path / 'a'
-    shutil.copytree(os.path.join(HERE, 'golden', 'config_a'), local)
+    for e in st.get('streams', []):
+        shutil.copytree(os.path.join(HERE, 'golden', e['dir']), local / e['dir'])
+    if not st.get('streams'):
+        shutil.copytree(os.path.join(HERE, 'golden', 'config_a'), local)
     script = os.path.join(HERE, 'integration', 'device_iter_ranks_check.py')
-    start = _ranks(script, [REF, str(local), 'start'])
+    start = _ranks(script, [REF, str(local), name, 'start'])
     for r in start:
         assert r['start'] and r['start_sizes'] and r['state_dict'], r
-    resumed = _ranks(script, [REF, str(local), 'resume', json.dumps(start[0]['state'])])
+    resumed = _ranks(script, [REF, str(local), name, 'resume', json.dumps(start[0]['state'])])
     for r in resumed:
         assert r['resume'] and r['resume_sizes'], r
