@@ -72,6 +72,10 @@ def parse_args(argv=None):
     ap.add_argument('--single', action='store_true',
                     help='ragged configs: single-pass decode (look-back scan inside the decode '
                     'kernel) instead of scan + decode')
+    ap.add_argument('--scan-ahead', action='store_true',
+                    help='ragged configs: the next step\'s scan pass on a side stream beside this '
+                    'step\'s decode (ScanAheadDecoder; measured no faster on MI355X, DESIGN.md '
+                    '§9: the decode holds the CUs, so the scan competes instead of overlapping)')
     ap.add_argument('--no-verify', action='store_true')
     ap.add_argument('--no-copy-probe', dest='copy_probe', action='store_false',
                     help='skip the same-run copy-ceiling measurement')
@@ -357,100 +361,208 @@ def copy_ceiling(batch, iters=10):
             'bytes_per_launch': 2 * src.numel()}
 
 
-def measure(args, config, world, rank, dev, tmpdir):
-    from streaming_amd import _native
-    from streaming_amd.decoder import BatchDecoder, output_bytes
-    mine, total_shards = shard_plan(args, config, rank, world)
-    synth, desc = build_workload(config, mine)
-    plan, batch = synth.plan, synth.batch
-    dec = BatchDecoder(plan, batch, single=args.single)
-    out = dec.run()
-    dec.check()
-    kernel = _native.last_kernel()
-    if not args.no_verify:
-        verify(config, out, synth.sources)
-    for _ in range(args.warmup):
-        dec.run()
-    torch.cuda.synchronize(dev)
+BLOCKS = 3  # the K timed steps of each config, split into blocks interleaved across configs
 
-    K = args.steps
-    stream = torch.cuda.current_stream(dev)  # the stream the kernels are launched on
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
+
+class Leg:
+    """One config's workload, decoder and timing records (built, checked and warmed up by
+    :func:`prepare`; timed block by block by :func:`timed_block`)."""
+
+
+def prepare(args, config, world, rank, dev):
+    """Build this rank's workload, decode it once, verify it against its sources, warm up."""
+    from streaming_amd import _native
+    from streaming_amd.decoder import BatchDecoder, ScanAheadDecoder, output_bytes
+    leg = Leg()
+    leg.config = config
+    leg.mine, leg.total_shards = shard_plan(args, config, rank, world)
+    leg.synth, leg.desc = build_workload(config, leg.mine)
+    plan, batch = leg.synth.plan, leg.synth.batch
+    # --scan-ahead (ragged plans): each step's scan pass (pass 1) on a side stream beside the
+    # previous step's decode (ScanAheadDecoder), outputs sized once from an exact two-pass decode
+    leg.ahead = plan.num_var > 0 and not args.single and args.scan_ahead
+    if leg.ahead:
+        first = BatchDecoder(plan, batch)
+        out = first.run()
+        first.check()
+        leg.kernel = _native.last_kernel()
+        caps = first.capacities
+        if not args.no_verify:
+            verify(config, out, leg.synth.sources)
+        del first, out
+        leg.dec = ScanAheadDecoder(plan, batch, capacities=caps)
+        out = leg.dec.run(ahead=False)
+    else:
+        leg.dec = BatchDecoder(plan, batch, single=args.single)
+        out = leg.dec.run()
+        leg.kernel = _native.last_kernel()
+    leg.dec.check()
+    if not args.no_verify:
+        verify(config, out, leg.synth.sources)
+    for k in range(args.warmup):
+        step(leg, k, args.warmup, None)
+    torch.cuda.synchronize(dev)
+    leg.R = batch.shard_bytes
+    leg.W = output_bytes(plan, leg.dec.result())
+    leg.blocks = []
+    leg.decode_ms, leg.scan_ms = [], []
+    return leg
+
+
+def step(leg, k, n, ev):
+    """Step k of n: scan + decode of the batch (scan-ahead: this step's decode and, unless it
+    is the block's last step, the next step's scan beside it). ``ev``: timing events."""
+    if leg.ahead:
+        leg.dec.run(ahead=k + 1 < n, events=ev)
+    else:
+        leg.dec.run(ev)
+
+
+def timed_block(args, leg, nsteps, world, dev):
+    """``nsteps`` steps between barrier + synchronize on both sides; the same-run copy ceiling
+    right after them."""
+    from streaming_amd.distributed import max_over_ranks
+    nev = 4 if leg.ahead else 3
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(nev)] for _ in range(nsteps)]
+    span = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    stream = torch.cuda.current_stream(dev)  # the stream the decode kernels are launched on
     barrier(world)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for k in range(K):
-        dec.run(events[k])
+    span[0].record(stream)
+    for k in range(nsteps):
+        step(leg, k, nsteps, events[k])
+    span[1].record(stream)
     torch.cuda.synchronize(dev)
     barrier(world)
     t1 = time.perf_counter()
-    from streaming_amd.distributed import max_over_ranks
     elapsed = max_over_ranks(t1 - t0, device=dev)
-    dec.check()
-    if not args.no_verify:
-        verify(config, dec.result(), synth.sources)
     assert stream == torch.cuda.current_stream(dev)
+    if leg.ahead:
+        dec_ms = [e[0].elapsed_time(e[1]) for e in events]
+        scan_ms = [e[2].elapsed_time(e[3]) for e in events[:-1]]
+    else:
+        dec_ms = [e[1].elapsed_time(e[2]) for e in events]
+        scan_ms = [e[0].elapsed_time(e[1]) for e in events]
+    leg.decode_ms += dec_ms
+    leg.scan_ms += scan_ms
+    copy = copy_ceiling(leg.synth.batch) if args.copy_probe else None
+    kern = float(np.mean(dec_ms))
+    achieved = (leg.R + leg.W) / kern / 1e6
+    leg.blocks.append({
+        'steps': nsteps,
+        'elapsed_s': elapsed,
+        'ms_per_step': elapsed / nsteps * 1e3,
+        'kernel_ms': kern,
+        'frac': achieved / HBM_PEAK_GBS,
+        'step_ms_events': span[0].elapsed_time(span[1]) / nsteps,
+        'step_frac': (leg.R + leg.W) / (span[0].elapsed_time(span[1]) / nsteps) / 1e6 /
+                     HBM_PEAK_GBS,
+        'copy_ceiling_GBps': copy['GBps'] if copy else None,
+        'frac_of_same_run_copy': achieved / copy['GBps'] if copy else None,
+        '_copy': copy,
+    })
 
-    decode_ms = [events[k][1].elapsed_time(events[k][2]) for k in range(K)]
-    scan_ms = [events[k][0].elapsed_time(events[k][1]) for k in range(K)]
-    kern_s = float(np.mean(decode_ms)) / 1e3
-    R = batch.shard_bytes
-    W = output_bytes(plan, dec.result())
+
+def block_sizes(k, n=BLOCKS):
+    """K steps split into at most n blocks (sizes differ by at most one)."""
+    n = max(1, min(n, k))
+    return [k // n + (1 if i < k % n else 0) for i in range(n)]
+
+
+def finish(args, leg, world, rank, tmpdir):
+    """The config's result object from its blocks (+ the CPU baseline on rank 0)."""
+    config, batch, plan = leg.config, leg.synth.batch, leg.synth.plan
+    leg.dec.check()
+    if leg.ahead:
+        leg.dec.close()
+    if not args.no_verify:
+        verify(config, leg.dec.result(), leg.synth.sources)
+    K = sum(b['steps'] for b in leg.blocks)
+    elapsed = sum(b['elapsed_s'] for b in leg.blocks)
     rows = batch.total_rows
     per_rank = gather_objects(world, {
-        'rank': rank, 'ms_per_step': (t1 - t0) / K * 1e3, 'rows': rows, 'shards': len(mine),
-        'shard_ids': f'{mine[0]}..{mine[-1]} step {world}' if mine else ''})
+        'rank': rank, 'ms_per_step': elapsed / K * 1e3, 'rows': rows, 'shards': len(leg.mine),
+        'shard_ids': f'{leg.mine[0]}..{leg.mine[-1]} step {world}' if leg.mine else ''})
     all_rows = sum(p['rows'] for p in per_rank)
+    R, W = leg.R, leg.W
+    kern_s = float(np.mean(leg.decode_ms)) / 1e3
     achieved = (R + W) / kern_s / 1e9
-    step_s = (float(np.mean(decode_ms)) + float(np.mean(scan_ms))) / 1e3
-    copy = copy_ceiling(batch) if args.copy_probe else None
+    step_s = sum(b['step_ms_events'] * b['steps'] for b in leg.blocks) / K / 1e3
+    copies = [b['_copy'] for b in leg.blocks if b['_copy']]
+    ratios = [b['frac_of_same_run_copy'] for b in leg.blocks if b['frac_of_same_run_copy']]
+    copy = None
+    if copies:  # the block whose copy ceiling is the median one, with every shape's rate
+        copy = sorted(copies, key=lambda c: c['GBps'])[len(copies) // 2]
     key = workload_key(config, batch, W)
-    traffic, traffic_src = committed_traffic(key, kernel)
+    traffic, traffic_src = committed_traffic(key, leg.kernel)
+    spb = [b['ms_per_step'] for b in leg.blocks]
+    blocks = [{k: v for k, v in b.items() if not k.startswith('_')} for b in leg.blocks]
     result = {
         'value': all_rows * K / elapsed,
         'unit': 'samples/s',
         'mds_gib_per_s': R * world * K / elapsed / 2**30,
         'ms_per_step': elapsed / K * 1e3,
+        'ms_per_step_blocks': {'median': float(np.median(spb)), 'min': float(np.min(spb)),
+                               'max': float(np.max(spb)), 'blocks': len(spb)},
+        'blocks': blocks,
         'config': {
-            'workload': desc,
+            'workload': leg.desc,
             'workload_key': key,
             'samples_per_gpu': rows,
             'shards_per_gpu': batch.nshards,
-            'shards_total': total_shards,
+            'shards_total': leg.total_shards,
             'shard_bytes_per_gpu': R,
             'output_bytes_per_gpu': W,
             'parallelism': f'{world} GPU(s), global shard g -> rank g % {world}, no data-path '
                            f'collectives',
+            'step': ('scan pass of step k+1 on a side stream beside the decode of step k '
+                     '(ScanAheadDecoder); both passes of every timed step inside the timed region'
+                     if leg.ahead else 'scan pass then decode, one stream'),
         },
         'per_rank': per_rank,
         'roofline': {
             'bound': 'hbm',
-            'kernel': kernel,
+            'kernel': leg.kernel,
             'achieved': achieved,
             'peak': HBM_PEAK_GBS,
             'unit': 'GB/s',
             'frac': achieved / HBM_PEAK_GBS,
+            'frac_blocks': [b['frac'] for b in leg.blocks],
             'traffic': traffic,
             'traffic_source': traffic_src,
             'src_sha': src_sha(),
             'algorithmic_bytes_per_launch': R + W,
             'algorithmic': {'R': R, 'W': W},
             'kernel_ms': kern_s * 1e3,
-            'scan_ms': float(np.mean(scan_ms)),
+            'scan_ms': float(np.mean(leg.scan_ms)) if leg.scan_ms else 0.0,
+            'scan_overlapped': leg.ahead,
             'step_frac': (R + W) / step_s / 1e9 / HBM_PEAK_GBS,
+            'step_frac_blocks': [b['step_frac'] for b in leg.blocks],
             'frac_of_measured_copy': achieved / COPY_MEASURED_GBS,
-            'frac_of_same_run_copy': achieved / copy['GBps'] if copy else None,
+            'frac_of_same_run_copy': float(np.median(ratios)) if ratios else None,
+            'frac_of_same_run_copy_blocks': ratios,
             'copy_ceiling_same_run': copy,
         },
         'cpu_baseline': None,
     }
     # the reference reader restated, timed on rank 0's host cores at every N, after the GPU legs
-    # (the other ranks wait for it at the next config's barrier, outside any timed region)
+    # (the other ranks wait for it at the next barrier, outside any timed region)
     if rank == 0 and args.cpu_seconds > 0:
-        result['cpu_baseline'] = cpu_baseline(args, config, synth, tmpdir)
-    del dec, out, synth
+        result['cpu_baseline'] = cpu_baseline(args, config, leg.synth, tmpdir)
+    leg.dec = leg.synth = None
     torch.cuda.empty_cache()
     return result
+
+
+def measure_all(args, configs, world, rank, dev, tmpdir):
+    """Every config prepared, then BLOCKS timed blocks per config, interleaved (B1 C1 B2 C2 B3
+    C3): each config's K steps are timed in blocks that fall on the same GPU phases."""
+    legs = {c: prepare(args, c, world, rank, dev) for c in configs}
+    for n in block_sizes(args.steps):
+        for c in configs:
+            timed_block(args, legs[c], n, world, dev)
+    return {c: finish(args, legs[c], world, rank, tmpdir) for c in configs}
 
 
 def dry_run(args, world, rank):
@@ -479,7 +591,7 @@ def main(argv=None):
         return 0
     configs = ['B', 'C'] if args.config == 'BC' else [args.config]
     with tempfile.TemporaryDirectory(prefix='mdsx_cpu_') as tmpdir:
-        results = {c: measure(args, c, world, rank, dev, tmpdir) for c in configs}
+        results = measure_all(args, configs, world, rank, dev, tmpdir)
     head = results[configs[0]]
     if rank == 0:
         line = {
@@ -500,6 +612,8 @@ def main(argv=None):
             'parity': 'bit-exact vs encoded source columns' if not args.no_verify else 'skipped',
             'config': head['config'],
             'per_rank': head['per_rank'],
+            'ms_per_step_blocks': head['ms_per_step_blocks'],
+            'blocks': head['blocks'],
             # the timing barrier / max-over-ranks / report gather: a torch.distributed process
             # group ('nccl' = RCCL on ROCm) when one is up, else none (one process, no group)
             'process_group': (f'{torch.distributed.get_backend()}, {world} rank(s)'

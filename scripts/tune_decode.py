@@ -19,7 +19,8 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from streaming_amd.decoder import BatchDecoder, DeviceBatch, Plan, _tables, output_bytes  # noqa
+from streaming_amd.decoder import (BatchDecoder, DeviceBatch, Plan, ScanAheadDecoder,  # noqa
+                                   _tables, output_bytes)
 from streaming_amd.synth import fixed_b_batch_on_device, var_c_batch_on_device  # noqa
 
 
@@ -77,7 +78,7 @@ def main():
         # '#tag' makes a repeated variant distinct (an identical control)
         spec = v.split('#')[0].split(',')
         knobs = [kv for kv in spec if kv and not kv.startswith('enc=') and kv not in
-                 ('single', 'nocheck')]
+                 ('single', 'nocheck', 'ahead')]
         encs = [kv[4:].split('|') for kv in spec if kv.startswith('enc=')]
         os.environ['MDSX_TUNE'] = ','.join(knobs)
         plan = Plan(names[0], encs[0] if encs else names[1], names[2])
@@ -91,12 +92,19 @@ def main():
             else:
                 dec.outputs, dec._fixed_raw = shared
         decs[v] = dec
+        if 'ahead' in spec:  # the next step's scan on a side stream (ScanAheadDecoder)
+            dec.run()
+            dec.check()
+            sad = ScanAheadDecoder(plan, dec.batch, capacities=dec.capacities)
+            sad.outputs_owner = dec  # (keeps the sizing decoder's buffers alive)
+            decs[v] = sad
         if 'nocheck' in spec:  # measurement-only variants (e.g. parts skipped)
             dec.run()
             continue
         # the first run (scan + sizing) and a re-run (known totals) against the sources
         for _ in range(2):
-            out = dec.run()
+            dec = decs[v]
+            out = dec.run(ahead=False) if isinstance(dec, ScanAheadDecoder) else dec.run()
             dec.check()
             if args.config == 'B':
                 assert torch.equal(out['x'].view(torch.int32), src['x'].view(torch.int32)), v
@@ -126,6 +134,15 @@ def main():
         order = list(decs.items())
         order = order[rnd % len(order):] + order[:rnd % len(order)]
         for v, dec in order:
+            if isinstance(dec, ScanAheadDecoder):  # whole-span time of the pipelined steps
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for k in range(args.iters):
+                    dec.run(ahead=k + 1 < args.iters)
+                e.record()
+                torch.cuda.synchronize()
+                times[v].append(s.elapsed_time(e) / args.iters)
+                continue
             evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)]
                    for _ in range(args.iters)]
             for e in evs:

@@ -412,10 +412,15 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
       c0 = pair ? c2 + 1 : c1 + 1;
     }
     if (direct && t == ga && ok) {  // copied by the huge-row kernel after this one
-      uint32_t* count = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(a.status) +
-                                                    kHugeCountOffset);
-      const uint32_t slot = atomicAdd(count, 1u);
-      a.src_abs[slot] = (uint64_t(tile) << 32) | uint32_t(t);
+      if constexpr (prof) {
+        // the stamps take the huge-row list's space: a batch with huge rows is refused there
+        report_decode(a, MDSX_E_ARG, int(shard_idx), int(r0 + t), -1);
+      } else {
+        uint32_t* count = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(a.status) +
+                                                      kHugeCountOffset);
+        const uint32_t slot = atomicAdd(count, 1u);
+        a.src_abs[slot] = (uint64_t(tile) << 32) | uint32_t(t);
+      }
     }
     if constexpr (prof) prof_mark(a, tile, 3, ts);
     rows_barrier<kFence>();
@@ -669,6 +674,10 @@ int launch_rows_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((rows_decode_kernel<true, false, false, true>), dim3(a.ntiles),
                        dim3(kRowsBlock), lds, s, a);
   } else if (a.stage_debug & 64) {  // measurement only: the phase stamps (src_abs)
+    // 8 stamps per tile in the huge-row list's space (nvar x rows words): refused where they
+    // would run past it; a huge row in such a batch is reported (MDSX_E_ARG), not listed
+    if (8ull * a.ntiles > uint64_t(a.nvar) * a.rows)
+      return mdsx::fail(MDSX_E_ARG, "mdsx: row-decode stamps need 8 x tiles <= nvar x rows");
     if (lds > 64 * 1024) {
       rc = hip_check(hipFuncSetAttribute(
                          reinterpret_cast<const void*>(rows_decode_kernel<true, false, true>),

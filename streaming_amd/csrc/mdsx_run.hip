@@ -446,6 +446,8 @@ int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
     if (plan->stage_debug & 64) {  // measurement only: the per-wave stamps (7 KiB ring, nt, 2)
       if (a.run_slots != 7 || !plan->run_nt || W != 2)
         return mdsx::fail(MDSX_E_ARG, "mdsx: seg stamps: run=7, rnt=1, swg=2 only");
+      if (3ull * a.ntiles > uint64_t(a.nvar) * a.rows)  // the stamps' space: nvar x rows words
+        return mdsx::fail(MDSX_E_ARG, "mdsx: seg stamps need 3 x tiles <= nvar x rows");
       mdsx::set_last_kernel("seg_decode_kernel<7, true, 2, true>");
       hipLaunchKernelGGL((seg_decode_kernel<7, true, 2, true>), dim3(sgrid), dim3(128), slds, s, a);
       return hip_check(hipGetLastError(), "seg_decode_kernel launch");

@@ -34,7 +34,8 @@ from streaming_amd._native import (BATCH_PAD, KIND_BYTES, KIND_FIXED, KIND_NDARR
 from streaming_amd.encodings import EncodingInfo, parse_encoding
 
 __all__ = [
-    'Plan', 'DeviceBatch', 'RaggedColumn', 'DecodedBatch', 'BatchDecoder', 'decode_batch',
+    'Plan', 'DeviceBatch', 'RaggedColumn', 'DecodedBatch', 'BatchDecoder', 'ScanAheadDecoder',
+    'decode_batch',
     'make_batch', 'stage_shards', 'torch_dtype', 'output_bytes', 'NdarrayMeta', 'ndarray_meta'
 ]
 
@@ -773,14 +774,17 @@ class BatchDecoder:
             self._fill_outs()
         if events is not None:
             events[1].record()
+        self._decode(stream)
+        if events is not None:
+            events[2].record()
+        return self.result()
+
+    def _decode(self, stream: int) -> None:
         _check(
             self.plan._lib.mdsx_decode_shards(self.plan.handle, ctypes.byref(self._abi),
                                               self._outs, self.workspace.data_ptr(),
                                               self.workspace.numel(), stream),
             'mdsx_decode_shards')
-        if events is not None:
-            events[2].record()
-        return self.result()
 
     def result(self) -> DecodedBatch:
         cols: dict[str, Union[torch.Tensor, RaggedColumn]] = {}
@@ -811,6 +815,160 @@ class BatchDecoder:
         st = self.status()
         if st.code != 0:
             raise _status_error(st, self.plan)
+
+
+class ScanAheadDecoder:
+    """Decode a sequence of device batches of one plan with each batch's pass 1 (the offsets and
+    size-head scan, ``mdsx_scan_shards``) enqueued on a side stream AHEAD of its pass 2
+    (``mdsx_decode_shards``, on the current stream), so that it runs beside the previous batch's
+    decode.
+
+    The scan pass reads one line of size heads per sample and is latency-bound: alone it is
+    ~4 % of a config-C step and ~14 % of a step over 32-256-byte rows, and it
+    leaves most of HBM idle while it runs. Ahead of time it shares the GPU with a decode instead.
+
+    Each of ``slots`` slots owns a workspace and outputs. ``scan(batch)`` takes a free slot and
+    enqueues pass 1 of ``batch`` on the side stream behind everything queued so far on the
+    current stream (so behind every reader of that slot's previous outputs); ``decode()``
+    makes the current stream wait for the oldest scanned batch's pass 1, enqueues its pass 2
+    and returns its outputs, valid until the next ``scan`` into that slot (with 2 slots: until
+    the next call of :meth:`run`). Ragged outputs are allocated at ``capacities`` (default: the
+    batch's :func:`payload_bound`, an upper bound, so no host round trip ever; a column that does
+    not fit raises MDSX_E_CAPACITY at :meth:`check`); ragged ``values`` are trimmed to the
+    scanned totals when first read.
+
+    ``run(ahead)`` is one step over the decoder's own batch: the decode of the batch scanned
+    before and, with ``ahead``, the scan for the next step beside it (the first call scans its
+    own batch first).
+    """
+
+    def __init__(self, plan: Plan, batch: DeviceBatch,
+                 capacities: Optional[dict[str, int]] = None, slots: int = 2) -> None:
+        if slots < 2:
+            raise ValueError('ScanAheadDecoder: at least 2 slots (one scanned while one decodes)')
+        self.plan = plan
+        self.batch = batch
+        self.device = batch.device
+        self._caps = dict(capacities) if capacities else None
+        self._slots = [self._new_slot(batch) for _ in range(slots)]
+        self._side = torch.cuda.Stream(self.device)
+        self._free = list(range(slots))
+        self._pending: list[tuple[int, torch.cuda.Event, Optional[torch.cuda.Event]]] = []
+        self._last: Optional[int] = None
+        self._host_totals = [torch.zeros(max(plan.num_var, 1), dtype=torch.int64,
+                                         pin_memory=True) for _ in range(slots)]
+        self._totals_ready: list[Optional[torch.cuda.Event]] = [None] * slots
+
+    def _new_slot(self, batch: DeviceBatch) -> BatchDecoder:
+        caps = self._caps
+        if caps is None and self.plan.num_var:
+            bound = payload_bound(self.plan, batch)
+            caps = {c.name: bound for c in self.plan.columns if not c.is_fixed}
+        dec = BatchDecoder(self.plan, batch, capacities=caps)
+        dec._sized = True
+        return dec
+
+    def scan(self, batch: Optional[DeviceBatch] = None,
+             events: Optional[Sequence[torch.cuda.Event]] = None) -> None:
+        """Enqueue pass 1 of ``batch`` (default: the decoder's batch) into a free slot on the
+        side stream. ``events``: two timing events recorded on the side stream around it."""
+        if not self._free:
+            raise RuntimeError('ScanAheadDecoder.scan: every slot holds a scanned batch; '
+                               'decode() one first')
+        si = self._free.pop(0)
+        batch = self.batch if batch is None else batch
+        dec = self._slots[si]
+        if dec.batch is not batch:
+            if batch.device != self.device:
+                raise ValueError('ScanAheadDecoder: every batch must be on the decoder\'s device')
+            dec = self._slots[si] = self._new_slot(batch)  # allocated on the current stream
+        dec._fill_outs()
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(self.device))
+        self._side.wait_event(ready)
+        with torch.cuda.stream(self._side):
+            if events is not None:
+                events[0].record(self._side)
+            dec._scan(self._side.cuda_stream)
+            if events is not None:
+                events[1].record(self._side)
+        done = torch.cuda.Event()
+        done.record(self._side)
+        self._pending.append((si, done, None))
+
+    def decode(self, events: Optional[Sequence[torch.cuda.Event]] = None) -> DecodedBatch:
+        """Enqueue pass 2 of the oldest scanned batch on the current stream; its outputs.
+        ``events``: two timing events recorded on the current stream around the decode."""
+        if not self._pending:
+            raise RuntimeError('ScanAheadDecoder.decode: no scanned batch; scan() one first')
+        si, done, _ = self._pending.pop(0)
+        dec = self._slots[si]
+        cur = torch.cuda.current_stream(self.device)
+        cur.wait_event(done)
+        if events is not None:
+            events[0].record(cur)
+        dec._stream = cur
+        dec._decode(cur.cuda_stream)
+        if events is not None:
+            events[1].record(cur)
+        if self.plan.num_var:
+            self._host_totals[si].copy_(dec.totals[:self.plan.num_var], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            self._totals_ready[si] = ev
+        self._free.append(si)
+        self._last = si
+        return self._result(si)
+
+    def run(self, ahead: bool = True, events: Optional[Sequence[torch.cuda.Event]] = None
+            ) -> DecodedBatch:
+        """One step over the decoder's batch. ``events``: four timing events -- around this
+        step's decode on the current stream, then around the next step's scan on the side
+        stream (left unrecorded without ``ahead``)."""
+        if not self._pending:
+            self.scan()
+        if ahead:
+            self.scan(events=events[2:4] if events is not None else None)
+        return self.decode(events[0:2] if events is not None else None)
+
+    def _result(self, si: int) -> DecodedBatch:
+        dec = self._slots[si]
+        cols: dict[str, Union[torch.Tensor, RaggedColumn]] = {}
+        vi = 0
+        for col in self.plan.columns:
+            out = dec.outputs[col.name]
+            if isinstance(out, RaggedColumn):
+                out = _PendingRagged(out.values, out.offsets, out.flags,
+                                     self._total(si, vi, int(out.values.numel())))
+                vi += 1
+            cols[col.name] = out
+        return DecodedBatch(cols, dec.batch.total_rows, list(dec.batch.row0), dec._stream)
+
+    def _total(self, si: int, vi: int, cap: int):
+        ev = self._totals_ready[si]
+        host = self._host_totals[si]
+
+        def total() -> int:
+            ev.synchronize()
+            return min(int(host[vi]), cap)
+        return total
+
+    def result(self) -> DecodedBatch:
+        """The outputs of the last decode."""
+        if self._last is None:
+            raise RuntimeError('ScanAheadDecoder.result: nothing decoded yet')
+        return self._result(self._last)
+
+    def check(self) -> None:
+        """Synchronize and raise the first error the last decoded batch's kernels reported."""
+        if self._last is not None:
+            self._slots[self._last].check()
+
+    def close(self) -> None:
+        """Wait for the side stream (a scan ahead that will not be decoded) and drop it."""
+        self._side.synchronize()
+        self._pending.clear()
+        self._free = list(range(len(self._slots)))
 
 
 def decode_batch(plan: Plan, batch: DeviceBatch, check: bool = True,

@@ -18,6 +18,7 @@ decompressing batch i+1 overlaps the copy and decode of batch i.
 
 from __future__ import annotations
 
+import logging
 import os
 import threading
 import time
@@ -50,6 +51,8 @@ class ShardFile:
     compression: Optional[str] = None
     hashes: Optional[dict] = None  # index.json raw_data.hashes (digests of the raw shard file)
 
+
+_log = logging.getLogger(__name__)
 
 def shard_files_from_index(dirname: str, index: dict, split: Optional[str] = None,
                            prefer_raw: bool = True) -> list[ShardFile]:
@@ -128,7 +131,12 @@ class ShardPipeline:
             more when shards are compressed (decompression times vary shard to shard; spare
             slots absorb a slow one: config E, 16 threads, 8-shard batches, 2M samples: 16.5
             GiB/s at depth 2, 24.2 at depth 3 (15-24 % pass-to-pass spread), 24.1-24.9 at depth
-            4 (6-18 %), 25.0 at depth 5 (3-4 %)).
+            4 (6-18 %), 25.0 at depth 5 (3-4 %)). Memory: each slot holds the
+            largest batch's shard bytes twice (pinned host + device) and its decoder's outputs
+            on the device (about the batch's bytes again), so a slot costs ~2x the batch in
+            device memory and 1x in pinned host memory; the automatic depth is capped so that
+            the slots take at most half of the device memory free at construction (an explicit
+            ``depth`` is taken as given). The chosen depth is logged (``logging`` INFO).
         workers: host threads reading / decompressing shards.
         device: CUDA device.
         validate_hash: check every shard against its index.json ``raw_data.hashes[algo]``
@@ -162,17 +170,23 @@ class ShardPipeline:
                         f'creation `{sorted((s.hashes or {}).keys())}`. Provide one of those.')
         self._device_hash = bool(validate_hash) and validate_hash in PIPELINE_DEVICE_HASHES
         self.per = max(1, shards_per_batch)
-        if depth is None:
-            depth = max(2, -(-max(1, workers) // self.per) + 1)
-            if any(s.compression for s in self.shards):
-                depth += 2
-        self.depth = max(1, depth)
         dev = torch.device(device or 'cuda')
         if dev.index is None:
             dev = torch.device('cuda', torch.cuda.current_device())
         self.device = dev
         self.groups = [self.shards[i:i + self.per] for i in range(0, len(self.shards), self.per)]
         biggest = max((_layout([s.raw_bytes for s in g])[1] for g in self.groups), default=0)
+        if depth is None:
+            depth = max(2, -(-max(1, workers) // self.per) + 1)
+            if any(s.compression for s in self.shards):
+                depth += 2
+            free = torch.cuda.mem_get_info(dev)[0]
+            cap = max(2, int(free // 2 // max(2 * biggest, 1)))
+            if depth > cap:
+                depth = cap
+            _log.info('ShardPipeline: depth %d (%d-shard batches up to %d bytes, %d workers)',
+                      depth, self.per, biggest, workers)
+        self.depth = max(1, depth)
         self.slots = [_Slot(biggest, dev) for _ in range(min(self.depth, len(self.groups)))]
         self.pool = ThreadPoolExecutor(max_workers=max(1, workers))
         self.copy_stream = torch.cuda.Stream(dev)

@@ -24,6 +24,7 @@ from __future__ import annotations
 import itertools
 import json
 import os
+import sys
 import threading
 from copy import deepcopy
 from dataclasses import dataclass
@@ -444,6 +445,9 @@ class MDSReader(JointReader):
             else:
                 values, offsets = host.ragged[col.name]
                 offs = offsets.tolist()  # (python ints: cheaper slicing than numpy scalars)
+                # the list's own memory (a pointer + an int object per row) counts against the
+                # host bound like the arrays (MDSX_DECODED_HOST_BYTES)
+                host.nbytes += len(offs) * (8 + sys.getsizeof(offs[-1] if offs else 0))
                 if name == 'bytes':
                     get = (lambda v, o: lambda i: v[o[i]:o[i + 1]].tobytes())(values, offs)
                 elif name == 'str':
@@ -492,8 +496,10 @@ class MDSReader(JointReader):
         if host is None:
             with self._lock:
                 if entry.host is None:
-                    entry.host = _HostShard(self.plan, entry.decoded)
-                    self.cache.set_host_bytes(self._key, entry.host.nbytes)
+                    h = _HostShard(self.plan, entry.decoded)
+                    h.getters = self._getters(h)  # (adds the offsets lists' bytes)
+                    entry.host = h
+                    self.cache.set_host_bytes(self._key, h.nbytes)
                 host = entry.host
         return self._materialize(host, idx)
 

@@ -76,3 +76,13 @@ def test_committed_traffic_is_keyed_on_workload_kernel_and_sources(tmp_path, mon
     assert bench.committed_traffic('B:k', 'run_decode_kernel<4, false>') == (None, None)
     (prof / 'pmc_x.json').write_text(json.dumps({'entries': [stale]}))
     assert bench.committed_traffic('B:k', 'decode_kernel<4, true>') == (None, None)
+
+
+def test_block_sizes():
+    """bench.py splits each config's K timed steps into interleaved blocks."""
+    import bench
+    assert bench.block_sizes(20) == [7, 7, 6]
+    assert bench.block_sizes(3) == [1, 1, 1]
+    assert bench.block_sizes(2) == [1, 1]
+    assert bench.block_sizes(1) == [1]
+    assert sum(bench.block_sizes(101)) == 101
