@@ -72,6 +72,12 @@ def main(ref: str, local: str, name: str, phase: str, state_json: str = '') -> N
                 h.update(r['words'].encode('utf-8'))
         return h.hexdigest(), sizes
 
+    # One process group for the whole run. Without it each StreamingDataset.__init__ creates one
+    # and destroys it again (distributed.py:114-128 maybe_init_dist, dataset.py:431): a second
+    # dataset in the same process then rendezvouses on the same MASTER_PORT while rank 0's store
+    # of the first is being torn down, and rank 1 can connect to the dying one ("Failed to recv").
+    import torch.distributed as dist
+    dist.init_process_group('gloo')
     clean_stale_shared_memory()  # collective under WORLD_SIZE=2: every rank calls it
     res = {'rank': rank}
     if phase == 'start':
@@ -94,6 +100,8 @@ def main(ref: str, local: str, name: str, phase: str, state_json: str = '') -> N
         d, sizes = run(device_iter(ds, bs, num_workers=W, gather=OracleGather(ds.shards)))
         res['resume'] = d == pr['iter_resume_sha256']
         res['resume_sizes'] = sizes == pr['resume_batch_sizes']
+    dist.barrier()
+    dist.destroy_process_group()
     print(json.dumps(res))
 
 

@@ -63,9 +63,10 @@ _PORTS_PER_WORKER = 200
 
 def _worker_port():
     """A free port from this pytest worker's own range (PYTEST_XDIST_WORKER gwN: ports
-    20000 + 200 N ...): no other worker and no ephemeral socket picks from it, so the port the
-    reference's rank 0 binds for its TCP-store rendezvous (dataset.py:431 -> distributed.py:128)
-    cannot be taken between this check and that bind."""
+    20000 + 200 N ...): no other worker and no ephemeral socket picks from it, so the port rank 0
+    binds for its TCP-store rendezvous cannot be taken between this check and that bind. (The
+    ranks' hangs of earlier rounds had a second cause, fixed in the rank script: each
+    StreamingDataset creating and destroying its own process group on the same port.)"""
     import socket
     w = os.environ.get('PYTEST_XDIST_WORKER', 'gw0')
     idx = int(w[2:]) if w[2:].isdigit() else 0
