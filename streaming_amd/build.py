@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SOURCES = [
     os.path.join(HERE, 'csrc', name)
-    for name in ('mdsx_kernels.hip', 'mdsx_stage.hip', 'mdsx_run.hip', 'mdsx_rows.hip',
+    for name in ('mdsx_kernels.hip', 'mdsx_stage.hip', 'mdsx_run.hip', 'mdsx_rows.hip', 'mdsx_srows.hip',
                  'mdsx_encode.hip', 'mdsx_hash.hip', 'mdsx_plan.cpp')
 ]
 HEADERS = [os.path.join(HERE, 'csrc', name)

@@ -31,6 +31,7 @@ struct ColumnSpec {
 int fail(int code, const std::string& msg);
 // Template name of the last decode kernel this thread launched (mdsx_last_kernel).
 void set_last_kernel(const std::string& name);
+const std::string& last_kernel_name();
 
 }  // namespace mdsx
 
@@ -69,6 +70,10 @@ struct mdsx_plan {
                            // else 4)
   int rows_pipe = 0;       // row-parallel decode: tiles per workgroup, the next tile's DMA in
                            // flight while one is written (two stages; 0: one tile, one stage)
+  int srows = 0;           // row-parallel batches: the streaming row-parallel decode first
+                           // (mdsx_srows.hip; the row-parallel kernel takes the tiles it lists)
+  int srows_kb = 8;        // its per-wave ring in KiB (6, 8 or 12); windows of <= (kb - 2) KiB
+  int srows_tile_kb = 40;  // its tiles: about this many KiB of samples (<= 256 rows)
   int gather_chunks = 2;  // 16-byte chunks per lane in the ragged gather (tile = 4 KiB x this)
   int gather_min = 256;   // ragged columns averaging fewer bytes per row use the gather kernel
   int group_max = 1024;   // ... fewer than this (and >= gather_min): four rows per wave
@@ -110,10 +115,12 @@ inline uint64_t rows_auto_stage(uint64_t per_row, uint64_t tr, uint64_t slack = 
 // stage -- rows_kb, or by default 20 KiB for samples under 512 bytes (per-sample work dominates:
 // five workgroups per CU) and 40 KiB above (three workgroups of larger tiles; measured)
 // -- with the workgroup's LDS within the CU's 160 KiB.
-inline int rows_tile_rows(const mdsx_plan* p, uint64_t per_row) {
+// target_kb > 0 (the streaming row-parallel decode's tiles): that many KiB of samples instead.
+inline int rows_tile_rows(const mdsx_plan* p, uint64_t per_row, int target_kb = 0) {
   if (per_row == 0) per_row = 1;
-  const uint64_t target = p->rows_kb > 0 ? uint64_t(p->rows_kb) * 1024
-                                         : (per_row < 512 ? 20 : 40) * 1024ull;
+  const uint64_t target = target_kb > 0  ? uint64_t(target_kb) * 1024
+                          : p->rows_kb > 0 ? uint64_t(p->rows_kb) * 1024
+                                           : (per_row < 512 ? 20 : 40) * 1024ull;
   int tr = 1;
   while (tr < 256) {
     const uint64_t t2 = uint64_t(tr) * 2;

@@ -745,7 +745,8 @@ __global__ __launch_bounds__(kBlock) void gather_ragged_kernel(const DevArgs a) 
 
 // ---------------------------------------------------------------------------------------------
 struct Layout {
-  uint64_t tile_total, tile_prefix, chunk_sum, tile_run, src_abs, row_map, map_len, total;
+  uint64_t tile_total, tile_prefix, chunk_sum, tile_run, src_abs, row_map, tile_list, map_len,
+      total;
 };
 
 __host__ uint64_t round256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
@@ -764,7 +765,8 @@ Layout workspace_layout(const mdsx_plan* plan, const mdsx_batch* b) {
   L.tile_run = L.chunk_sum + round256(nv * (b->ntiles / kScanChunk + 1) * 8);
   L.src_abs = L.tile_run + round256(nv ? uint64_t(b->ntiles) * sizeof(TileRun) : 0);
   L.row_map = L.src_abs + round256(nv * b->rows * 8);
-  L.total = L.row_map + round256(nv * L.map_len * 4);
+  L.tile_list = L.row_map + round256(nv * L.map_len * 4);
+  L.total = L.tile_list + round256(nv ? uint64_t(b->ntiles) * 4 : 0);
   return L;
 }
 
@@ -793,6 +795,7 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   a->tile_run = reinterpret_cast<TileRun*>(ws + L.tile_run);
   a->src_abs = reinterpret_cast<uint64_t*>(ws + L.src_abs);
   a->row_map = reinterpret_cast<uint32_t*>(ws + L.row_map);
+  a->tile_list = reinterpret_cast<uint32_t*>(ws + L.tile_list);
   a->lookback = reinterpret_cast<uint64_t*>(ws + L.tile_total);  // single pass: no tile totals
   a->ticket = reinterpret_cast<uint32_t*>(ws + kTicketOffset);
   a->map_len = L.map_len;
@@ -820,6 +823,13 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   if (a->rows_bytes && rows_lds_bytes_est(plan, a->rows_bytes, uint64_t(tr)) > 160 * 1024)
     a->rows_bytes = 0;
   a->rows_pipe = a->rows_bytes ? uint32_t(plan->rows_pipe) : 0u;
+  // the streaming row-parallel decode: windows of at most (ring - 2) KiB; tiles with a larger
+  // sample (TileRun bit 1 clear, stage_totals_kernel) go to the row-parallel kernel
+  if (a->rows_bytes && plan->srows && !a->run_slots) {
+    a->srows_slots = uint32_t(plan->srows_kb);
+    a->seg_lim = a->srows_slots * 1024u - 2048u;
+    a->rows_pipe = 0;
+  }
   if (a->run_slots && tr > 32)
     return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode tiles hold at most 32 rows");
   // the staged and streaming decodes scan one total per tile; the register-copy decode one per

@@ -27,6 +27,7 @@ int fail(int code, const std::string& msg) {
 }
 
 void set_last_kernel(const std::string& name) { g_last_kernel = name; }
+const std::string& last_kernel_name() { return g_last_kernel; }
 
 namespace {
 
@@ -219,9 +220,15 @@ void apply_tuning(mdsx_plan* p) {
       p->rows_pipe = int(v);
     } else if (key == "rownt") {
       p->rows_nt = v ? 1 : 0;
+    } else if (key == "srows") {
+      p->srows = v ? 1 : 0;
+    } else if (key == "srkb" && (v == 6 || v == 8 || v == 12)) {
+      p->srows_kb = int(v);
+    } else if (key == "srtile" && v >= 4 && v <= 96) {
+      p->srows_tile_kb = int(v);
     } else if (key == "swg" && (v == 1 || v == 2 || v == 4)) {
       p->seg_waves = int(v);
-    } else if (key == "sv" && v >= 0 && v <= 15) {
+    } else if (key == "sv" && v >= 0 && v <= 31) {
       p->seg_var = int(v);
     } else if (key == "seg") {
       p->seg = v ? 1 : 0;
@@ -370,7 +377,8 @@ int mdsx_plan_tile_rows_for(const mdsx_plan* plan, uint64_t shard_bytes, uint64_
     while (tr < 32 && uint64_t(tr) * 2 * per_row <= uint64_t(plan->run_kb) * 1024) tr *= 2;
     return tr;
   }
-  if (use_rows_decode(plan, shard_bytes, rows)) return rows_tile_rows(plan, shard_bytes / rows);
+  if (use_rows_decode(plan, shard_bytes, rows))
+    return rows_tile_rows(plan, shard_bytes / rows, plan->srows ? plan->srows_tile_kb : 0);
   return plan->tile_rows;
 }
 

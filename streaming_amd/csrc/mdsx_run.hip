@@ -101,7 +101,8 @@ __host__ __device__ __forceinline__ uint32_t seg_wave_lds(int S, int TR, int nva
 // not well-formed UTF-8 (wave-uniform).
 // Measurement variants (kV bits, MDSX_TUNE sv): 2 releases the ring slots a value's 1 KiB step
 // has consumed after each step (not after the whole value), so the next sample's slots go in
-// flight while the value is still being written; 4 waits per 1 KiB step (not once per sample).
+// flight while the value is still being written; 4 waits per 1 KiB step (not once per sample);
+// 8 (ablation, outputs incomplete) stores no partial edge chunk.
 template <int S, bool kNT, int kV = 0>
 __device__ __forceinline__ bool seg_copy(Stream& st, const lds_u8* ring, uint32_t ring_lds,
                                          uint64_t base, uint32_t cst, uint32_t d, uint32_t len,
@@ -129,7 +130,8 @@ __device__ __forceinline__ bool seg_copy(Stream& st, const lds_u8* ring, uint32_
     const bool skip0 = shared0 && g == 0;
     if (kk < nfull && !(skip0 && lane == 0)) st16<kNT>(out + 16ull * kk, val);
     if (min(nfull, g + 64u) > g + (skip0 ? 1u : 0u)) ++ops;  // that store was issued
-    if (skip0 && nfull > 0) wave_edge_store(val, 0, out, base + cst, out + 16, lane);
+    if ((kV & 8) == 0)
+      if (skip0 && nfull > 0) wave_edge_store(val, 0, out, base + cst, out + 16, lane);
     if (utf8) {
       // this value's bytes only: the carried ones and those past its end zeroed
       uint4 vout = kk < nch ? val : z4;
@@ -352,7 +354,7 @@ __global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) 
     ++j;
   }
   // the partly filled last chunk of every wide column (bytes [max(cst, chunk), cur))
-  for (uint64_t m = wide_mask; m; m &= m - 1) {
+  for (uint64_t m = (kV & 8) ? 0ull : wide_mask; m; m &= m - 1) {
     const int c = __builtin_ctzll(m);
     const uint32_t cu = uint32_t(__builtin_amdgcn_readlane(int(cur), c));
     const uint32_t cs = uint32_t(__builtin_amdgcn_readlane(int(cst), c));
@@ -363,8 +365,9 @@ __global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) 
     const uint64_t bs = readlane64(base, c);
     wave_edge_store(carry, c, bs + C, bs + lo, bs + cu, lane);
   }
-  // the staged small fixed columns, one row per lane
-  for (uint64_t m = small_mask; m; m &= m - 1) {
+  // the staged small fixed columns, one row per lane (kV bit 16, ablation: none of the run's
+  // per-row outputs -- small columns, offsets, flags -- is written)
+  for (uint64_t m = (kV & 16) ? 0ull : small_mask; m; m &= m - 1) {
     const int c = __builtin_ctzll(m);
     const uint32_t w = cols[c].row_bytes;
     const uint32_t so = uint32_t(__builtin_amdgcn_readlane(int(soff), c));
@@ -373,7 +376,7 @@ __global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) 
               static_cast<uint8_t*>(cols[c].data) + (row0 + uint64_t(lane)) * w, w);
   }
   // the run's ragged offsets and str flags
-  for (int c = 0; c < ncols; ++c) {
+  for (int c = 0; c < ((kV & 16) ? 0 : ncols); ++c) {
     const MDSX_L DevCol& col = cols[c];
     const int v = col.var_index;
     if (v < 0) continue;
@@ -438,8 +441,8 @@ int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
                        s, a);                                                                 \
     return hip_check(hipGetLastError(), "seg_decode_kernel launch");                          \
   }
-      MDSX_SEG_V(1) MDSX_SEG_V(2) MDSX_SEG_V(3) MDSX_SEG_V(4) MDSX_SEG_V(5) MDSX_SEG_V(6)
-      MDSX_SEG_V(7)
+      MDSX_SEG_V(1) MDSX_SEG_V(2) MDSX_SEG_V(3) MDSX_SEG_V(4) MDSX_SEG_V(8) MDSX_SEG_V(16)
+      MDSX_SEG_V(24)
 #undef MDSX_SEG_V
       return mdsx::fail(MDSX_E_ARG, "mdsx: seg variant out of range");
     }

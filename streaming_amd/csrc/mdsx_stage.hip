@@ -31,7 +31,7 @@ namespace mdsx_kernels {
 // fit counts zero.
 __global__ __launch_bounds__(kBlock) void stage_totals_kernel(const DevArgs a) {
   __shared__ int64_t s_part[kBlock / 64][MDSX_MAX_COLUMNS];
-  __shared__ uint32_t s_bad[kBlock / 64];
+  __shared__ uint32_t s_bad[kBlock / 64], s_big[kBlock / 64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int TR = a.tile_rows;
   const uint32_t tile = blockIdx.x * uint32_t(kBlock / TR) + uint32_t(t / TR);
@@ -90,11 +90,11 @@ __global__ __launch_bounds__(kBlock) void stage_totals_kernel(const DevArgs a) {
       tile_bad = (bad & seg) != 0;  // this tile's lanes
       tile_big = (big & seg) != 0;
     } else {  // a tile spans TR / 64 waves
-      if (lane == 0) s_bad[wave] = bad != 0;
+      if (lane == 0) s_bad[wave] = bad != 0, s_big[wave] = big != 0;
       __syncthreads();
       tile_bad = false;
       for (int w = wave & ~(TR / 64 - 1); w < (wave & ~(TR / 64 - 1)) + TR / 64; ++w)
-        tile_bad = tile_bad || s_bad[w];
+        tile_bad = tile_bad || s_bad[w], tile_big = tile_big || s_big[w];
     }
     if (tile_ok && t % TR == 0) {
       TileRun r;

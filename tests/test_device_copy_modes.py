@@ -63,6 +63,10 @@ MODES = {
     'rows_pipe_one': 'rows=8,rpipe=1,rmin=1000000000',  # one tile per workgroup, two stages
     'rows_occ6': 'rows=-1,rocc=6,rmin=1000000000',  # registers bounded for six waves per SIMD
     'rows_occ8': 'rows=12,rocc=8,rmin=1000000000',  # ... eight, smaller tiles
+    # the streaming row-parallel decode (mdsx_srows.hip), the row-parallel kernel over the tiles
+    # it lists; a 6 KiB ring (4 KiB windows) with small tiles and a 2 KiB fallback stage
+    'srows': 'rows=-1,srows=1,rmin=1000000000',
+    'srows_small': 'rows=2,srows=1,srkb=6,srtile=8,rmin=1000000000',
     'gather': 'run=0,rows=0,gmin=1000000000',
     'group': 'run=0,rows=0,gmin=0,gmax=1000000000',
     'group_nt': 'run=0,rows=0,gmin=0,gmax=1000000000,strc=0',  # str rows streamed (non-temporal) too

@@ -33,6 +33,7 @@ MODES = {
     'seg_wg4': 'run=8,seg=1,rmin=0,swg=4',  # four waves per workgroup (the default is two)
     'rows_small': 'rows=2,rmin=1000000000',  # row-parallel, 2 KiB stage (windows, huge rows)
     'rows_pipe': 'rows=4,rpipe=5,rmin=1000000000',  # ... two stages, next tile's DMA in flight
+    'srows': 'rows=-1,srows=1,srkb=6,rmin=1000000000',  # streaming row-parallel + listed tiles
     'register': 'run=0,rows=0',  # the register decode (+ gather / groups per column)
 }
 # the single pass (mdsx_decode_shards_single), fresh and re-run with known totals
@@ -40,6 +41,7 @@ SINGLE_MODES = {
     'single': '',  # streaming / row-parallel batches: scan pass + decode, no host round trip
     'single_rows_small': 'rows=2,rmin=1000000000',  # ... row-parallel in windows, huge rows
     'single_rows_pipe': 'rows=4,rpipe=5,rmin=1000000000',  # ... two stages per workgroup
+    'single_srows': 'rows=-1,srows=1,rmin=1000000000',  # ... the streaming row-parallel decode
     'single_register': 'run=0,rows=0',  # the register decode's single-pass form (look-back)
 }
 

@@ -108,9 +108,9 @@ def test_workspace_bytes():
     r = lambda x: (x + 255) // 256 * 256
     # status block, per-tile totals and prefixes, chunk sums of their scan, the streaming
     # decode's 48-byte run records, per-row addresses (also the staged decode's huge-row list),
-    # row map
+    # row map, the streaming row-parallel decode's tile list
     want = 256 + 2 * r(2 * 100 * 8) + r(2 * (100 // 4096 + 1) * 8) + r(100 * 48) + \
-        r(2 * 6400 * 8) + r(2 * ((1 << 20) // 4096 + 8) * 4)
+        r(2 * 6400 * 8) + r(2 * ((1 << 20) // 4096 + 8) * 4) + r(100 * 4)
     assert lib.mdsx_workspace_bytes(plan.handle, ctypes.byref(b)) == want
     fixed = Plan(['id', 'x'], ['int32', 'ndarray:float32:1024'], [4, 4096])
     assert lib.mdsx_workspace_bytes(fixed.handle, ctypes.byref(b)) == 256
