@@ -72,7 +72,8 @@ struct mdsx_plan {
                            // flight while one is written (two stages; 0: one tile, one stage)
   int srows = 0;           // row-parallel batches: the streaming row-parallel decode first
                            // (mdsx_srows.hip; the row-parallel kernel takes the tiles it lists)
-  int srows_kb = 8;        // its per-wave ring in KiB (6, 8 or 12); windows of <= (kb - 2) KiB
+  int srows_kb = 8;        // its per-wave ring in KiB (6, 8 or 12)
+  int srows_lim_kb = 0;    // its windows: at most this many KiB (0: ring - 2)
   int srows_tile_kb = 40;  // its tiles: about this many KiB of samples (<= 256 rows)
   int gather_chunks = 2;  // 16-byte chunks per lane in the ragged gather (tile = 4 KiB x this)
   int gather_min = 256;   // ragged columns averaging fewer bytes per row use the gather kernel

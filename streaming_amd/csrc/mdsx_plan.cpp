@@ -224,11 +224,13 @@ void apply_tuning(mdsx_plan* p) {
       p->srows = v ? 1 : 0;
     } else if (key == "srkb" && (v == 6 || v == 8 || v == 12)) {
       p->srows_kb = int(v);
+    } else if (key == "srlim" && v >= 0 && v <= 10) {
+      p->srows_lim_kb = int(v);
     } else if (key == "srtile" && v >= 4 && v <= 96) {
       p->srows_tile_kb = int(v);
     } else if (key == "swg" && (v == 1 || v == 2 || v == 4)) {
       p->seg_waves = int(v);
-    } else if (key == "sv" && v >= 0 && v <= 31) {
+    } else if (key == "sv" && v >= 0 && v <= 63) {
       p->seg_var = int(v);
     } else if (key == "seg") {
       p->seg = v ? 1 : 0;

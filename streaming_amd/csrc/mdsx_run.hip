@@ -102,7 +102,8 @@ __host__ __device__ __forceinline__ uint32_t seg_wave_lds(int S, int TR, int nva
 // Measurement variants (kV bits, MDSX_TUNE sv): 2 releases the ring slots a value's 1 KiB step
 // has consumed after each step (not after the whole value), so the next sample's slots go in
 // flight while the value is still being written; 4 waits per 1 KiB step (not once per sample);
-// 8 (ablation, outputs incomplete) stores no partial edge chunk.
+// 8 (ablation, outputs incomplete) stores no partial edge chunk; 32 touches the run's lines
+// beyond the ring's first fill at the start (seg_decode_kernel).
 template <int S, bool kNT, int kV = 0>
 __device__ __forceinline__ bool seg_copy(Stream& st, const lds_u8* ring, uint32_t ring_lds,
                                          uint64_t base, uint32_t cst, uint32_t d, uint32_t len,
@@ -232,6 +233,25 @@ __global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) 
     if (tile >= a.ntiles) return;  // wave-uniform; no barrier below
     r = a.tile_run[tile];
     if (r.fast & 2) sbase = seg_stream_start<S, kNT>(st, r, batch, ring_lds, lane);
+  }
+  if constexpr ((kV & 32) != 0) {
+    // the run's 128-byte lines beyond the ring's first fill, touched now (one 4-byte LDS-DMA
+    // load each into a scratch word after the waves' LDS: the line lands in L2, nothing in a
+    // register), so that the later ring loads of this run hit L2
+    if (r.fast & 2) {
+      const uint32_t beyond = st.nq > uint32_t(S) * 64u ? st.nq - uint32_t(S) * 64u : 0u;
+      if (beyond) {
+        const uint32_t lines = min((beyond + 7u) >> 3, 64u);
+        const uint32_t scratch = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(
+            reinterpret_cast<uintptr_t>((const MDSX_L uint8_t*)(smem + seg_cols_lds(ncols) +
+                                                                 size_t(W) * seg_wave_lds(
+                                                                     S, TR, nvar, a.seg_small)))));
+        const uint8_t* line = reinterpret_cast<const uint8_t*>(st.base) + uint64_t(S) * 1024u +
+                              128u * uint32_t(lane < int(lines) ? lane : 0);
+        glds4(line, scratch);
+        ++st.ops;
+      }
+    }
   }
   const MDSX_L DevCol* cols = (const MDSX_L DevCol*)s_cols;
   if (!(r.fast & 2)) {
@@ -405,7 +425,8 @@ int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
   if (a.seg_lim) {
     const int W = plan->seg_waves;
     const size_t slds = seg_cols_lds(a.ncols) +
-                        size_t(W) * seg_wave_lds(a.run_slots, a.tile_rows, a.nvar, a.seg_small);
+                        size_t(W) * seg_wave_lds(a.run_slots, a.tile_rows, a.nvar, a.seg_small) +
+                        ((plan->seg_var & 32) ? 256u : 0u);  // (the touch variant's scratch)
     if (slds > 160 * 1024)
       return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode LDS exceeds 160 KiB");
     const unsigned sgrid = (a.ntiles + unsigned(W) - 1) / unsigned(W);
@@ -442,7 +463,7 @@ int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
     return hip_check(hipGetLastError(), "seg_decode_kernel launch");                          \
   }
       MDSX_SEG_V(1) MDSX_SEG_V(2) MDSX_SEG_V(3) MDSX_SEG_V(4) MDSX_SEG_V(8) MDSX_SEG_V(16)
-      MDSX_SEG_V(24)
+      MDSX_SEG_V(7) MDSX_SEG_V(24) MDSX_SEG_V(32) MDSX_SEG_V(33)
 #undef MDSX_SEG_V
       return mdsx::fail(MDSX_E_ARG, "mdsx: seg variant out of range");
     }
