@@ -71,7 +71,8 @@ struct mdsx_plan {
   int rows_pipe = 0;       // row-parallel decode: tiles per workgroup, the next tile's DMA in
                            // flight while one is written (two stages; 0: one tile, one stage)
   int srows = 0;           // row-parallel batches: the streaming row-parallel decode first
-                           // (mdsx_srows.hip; the row-parallel kernel takes the tiles it lists)
+                           // (mdsx_srows.hip; the row-parallel kernel takes the tiles it lists);
+                           // 1: the samples through a per-wave LDS ring, 2: read from L2
   int srows_kb = 8;        // its per-wave ring in KiB (6, 8 or 12)
   int srows_lim_kb = 0;    // its windows: at most this many KiB (0: ring - 2)
   int srows_tile_kb = 40;  // its tiles: about this many KiB of samples (<= 256 rows)

@@ -827,9 +827,12 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   // sample (TileRun bit 1 clear, stage_totals_kernel) go to the row-parallel kernel
   if (a->rows_bytes && plan->srows && !a->run_slots) {
     a->srows_slots = uint32_t(plan->srows_kb);
-    a->seg_lim = plan->srows_lim_kb > 0 && plan->srows_lim_kb + 2 <= plan->srows_kb
-                     ? uint32_t(plan->srows_lim_kb) * 1024u
-                     : a->srows_slots * 1024u - 2048u;
+    if (plan->srows == 2)  // read from L2: windows of <= srows_lim_kb (default 16) KiB
+      a->seg_lim = uint32_t(plan->srows_lim_kb > 0 ? std::min(plan->srows_lim_kb, 32) : 16) * 1024u;
+    else
+      a->seg_lim = plan->srows_lim_kb > 0 && plan->srows_lim_kb + 2 <= plan->srows_kb
+                       ? uint32_t(plan->srows_lim_kb) * 1024u
+                       : a->srows_slots * 1024u - 2048u;
     a->rows_pipe = 0;
   }
   if (a->run_slots && tr > 32)

@@ -220,11 +220,11 @@ void apply_tuning(mdsx_plan* p) {
       p->rows_pipe = int(v);
     } else if (key == "rownt") {
       p->rows_nt = v ? 1 : 0;
-    } else if (key == "srows") {
-      p->srows = v ? 1 : 0;
+    } else if (key == "srows" && v >= 0 && v <= 2) {
+      p->srows = int(v);  // 1: through an LDS ring, 2: read from L2
     } else if (key == "srkb" && (v == 6 || v == 8 || v == 12)) {
       p->srows_kb = int(v);
-    } else if (key == "srlim" && v >= 0 && v <= 10) {
+    } else if (key == "srlim" && v >= 0 && v <= 32) {
       p->srows_lim_kb = int(v);
     } else if (key == "srtile" && v >= 4 && v <= 96) {
       p->srows_tile_kb = int(v);

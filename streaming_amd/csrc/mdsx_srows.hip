@@ -46,18 +46,34 @@
 namespace mdsx_kernels {
 namespace {
 
-constexpr int kSrWin = 31;  // samples per window at most (lane j: sample j, lane j + 1: its end)
+// Value records per column of a window (lane j: sample j, lane j + 1: its end): 32 with the ring
+// (windows of <= 31 samples), 64 when the samples are read from L2 (kL2, <= 63).
+__host__ __device__ __forceinline__ int sr_rec(bool l2) { return l2 ? 64 : 32; }
 
-// LDS: the workgroup's column table, then per wave: the ring (+ mirror), [ncols][32] value
-// records, [nvar][map_len] chunk maps, one UTF-8 word per column.
+// LDS: the workgroup's column table, then per wave: the ring (+ mirror) -- or (kL2) a 256-byte
+// scratch the line touches land in --, [ncols][sr_rec] value records, [nvar][map_len] chunk maps,
+// one UTF-8 word (two with kL2) per column.
 __host__ __device__ __forceinline__ uint32_t sr_cols_lds(int ncols) {
   return (uint32_t(ncols) * uint32_t(sizeof(DevCol)) + 15u) & ~15u;
 }
 __host__ __device__ __forceinline__ uint32_t sr_map_len(uint32_t lim) { return lim / 16u + 8u; }
-__host__ __device__ __forceinline__ uint32_t sr_wave_lds(int S, int ncols, int nvar,
-                                                         uint32_t lim) {
-  return uint32_t(S) * 1024u + kMirror + uint32_t(ncols) * 32u * 16u +
-         ((uint32_t(nvar) * sr_map_len(lim) + 15u) & ~15u) + ((uint32_t(ncols) * 4u + 15u) & ~15u);
+__host__ __device__ __forceinline__ uint32_t sr_wave_lds(int S, int ncols, int nvar, uint32_t lim,
+                                                         bool l2) {
+  return (l2 ? 256u : uint32_t(S) * 1024u + kMirror) + uint32_t(ncols) * uint32_t(sr_rec(l2)) * 16u +
+         ((uint32_t(nvar) * sr_map_len(lim) + 15u) & ~15u) + ((uint32_t(ncols) * 8u + 15u) & ~15u);
+}
+
+// 16 / 4 bytes at any byte address of global memory (gfx950 loads unaligned dwordx4 / dword:
+// scripts/microbench/unaligned_copy.hip, bit-exact at every offset).
+__device__ __forceinline__ uint4 ldu16(const uint8_t* p) {
+  u32x4 v;
+  __builtin_memcpy(&v, (const MDSX_G uint8_t*)p, 16);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint32_t ldu32(const uint8_t* p) {
+  uint32_t v;
+  __builtin_memcpy(&v, (const MDSX_G uint8_t*)p, 4);
+  return v;
 }
 
 struct SrRec {  // one value of a window: output byte (window-relative), bytes, stream position
@@ -91,8 +107,13 @@ __device__ __forceinline__ void store_small(uint64_t q, const uint4 v, uint32_t 
   }
 }
 
-template <int S, bool kNT, int W>
-__global__ __launch_bounds__(64 * W) void srows_decode_kernel(const DevArgs a) {
+// kL2: no ring -- the samples' bytes are read from global memory (their lines touched into L2
+// when the window is laid out, the reads unaligned 16-byte loads), so a wave's LDS is its tables
+// only and up to five waves per SIMD hold a tile each; windows of up to 63 samples, seg_lim bytes.
+template <int S, bool kNT, int W, bool kL2>
+__global__ __launch_bounds__(64 * W, kL2 ? 5 : 1) void srows_decode_kernel(const DevArgs a) {
+  constexpr int kRec = kL2 ? 64 : 32;
+  constexpr int kSrWin = kRec - 1;  // samples per window at most
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int t = threadIdx.x, lane = t & 63;
   const int wave = W == 1 ? 0 : __builtin_amdgcn_readfirstlane(t >> 6);
@@ -115,10 +136,10 @@ __global__ __launch_bounds__(64 * W) void srows_decode_kernel(const DevArgs a) {
   const int ncols = a.ncols, nvar = a.nvar;
   const uint32_t lim = a.seg_lim;
   const uint32_t map_len = sr_map_len(lim);
-  uint8_t* wl = smem + sr_cols_lds(ncols) + size_t(wave) * sr_wave_lds(S, ncols, nvar, lim);
+  uint8_t* wl = smem + sr_cols_lds(ncols) + size_t(wave) * sr_wave_lds(S, ncols, nvar, lim, kL2);
   const lds_u8* ring = (const lds_u8*)wl;
-  MDSX_L SrRec* rec = (MDSX_L SrRec*)(wl + S * 1024 + kMirror);  // [ncols][32]
-  MDSX_L uint8_t* map = (MDSX_L uint8_t*)(rec + ncols * 32);     // [nvar][map_len]
+  MDSX_L SrRec* rec = (MDSX_L SrRec*)(wl + (kL2 ? 256 : S * 1024 + kMirror));  // [ncols][kRec]
+  MDSX_L uint8_t* map = (MDSX_L uint8_t*)(rec + ncols * kRec);  // [nvar][map_len]
   MDSX_L uint32_t* bad = (MDSX_L uint32_t*)(map + ((uint32_t(nvar) * map_len + 15u) & ~15u));
   const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(
       static_cast<uint32_t>(reinterpret_cast<uintptr_t>((const MDSX_L uint8_t*)wl)));
@@ -133,18 +154,34 @@ __global__ __launch_bounds__(64 * W) void srows_decode_kernel(const DevArgs a) {
   uint32_t o3 = 192 + lane <= n ? offs[192 + lane] : 0u;
   uint32_t o4 = 256 + lane <= n ? offs[256 + lane] : 0u;
   // the tile's bytes: one range starting on a 128-byte line, its first S KiB in flight at once
+  // (kL2: positions are bytes of the shard file, read from global memory)
   Stream st;
   const uint64_t sbase = (batch + r.stream) & ~uint64_t(127);
-  st.base = reinterpret_cast<const uint4*>(sbase);
-  st.nq = uint32_t((batch + r.stream + r.bytes - sbase + 15) >> 4);
-  st.nslots = (st.nq + 63) >> 6;
-  st.issued = 0;
-  st.ops = 0;
-  st.op_at = 0;
-  st.mirrored = 0xffffffffu;
-  st.landed = 0;
-  pump<S, kNT>(st, ring_lds, 0, lane);
-  const uint32_t sp0 = uint32_t(batch + r.shard_off - sbase);  // stream position of file byte 0
+  const uint8_t* frame = a.batch + r.shard_off;
+  uint32_t sp0 = 0;
+  if constexpr (!kL2) {
+    st.base = reinterpret_cast<const uint4*>(sbase);
+    st.nq = uint32_t((batch + r.stream + r.bytes - sbase + 15) >> 4);
+    st.nslots = (st.nq + 63) >> 6;
+    st.issued = 0;
+    st.ops = 0;
+    st.op_at = 0;
+    st.mirrored = 0xffffffffu;
+    st.landed = 0;
+    pump<S, kNT>(st, ring_lds, 0, lane);
+    sp0 = uint32_t(batch + r.shard_off - sbase);  // stream position of file byte 0
+  }
+  // the source bytes: from the ring, or (kL2) from global memory at a shard-file position
+  auto rd16 = [&](uint32_t p) -> uint4 {
+    if constexpr (kL2) return ldu16(frame + p);
+    else return ring16<S>(ring, p);
+  };
+  auto rd32 = [&](uint32_t p) -> uint32_t {
+    if constexpr (kL2) return ldu32(frame + p);
+    else return ring_u32<S>(ring, p);
+  };
+  uint32_t sink = 0;  // (kL2) the line touches' words, kept live until the tile's end
+  uint32_t touch[4] = {0, 0, 0, 0};
 
   // column facts and cursors, lane-distributed (lane c: column c)
   int vi = -1;
@@ -168,8 +205,8 @@ __global__ __launch_bounds__(64 * W) void srows_decode_kernel(const DevArgs a) {
     }
     small = vi < 0 && rb <= uint32_t(kSmallMax);
     wide = !small && !skip;
-    bad[lane] = 0;
   }
+  for (int i = lane; i < 2 * ncols; i += 64) bad[i] = 0;
   const uint64_t wide_mask = __ballot(wide);
   const uint64_t small_mask = __ballot(small);
   const uint64_t utf8_mask = __ballot(utf8 && !skip);
@@ -190,7 +227,7 @@ __global__ __launch_bounds__(64 * W) void srows_decode_kernel(const DevArgs a) {
     const uint32_t vb = uint32_t(__shfl(int(sel5(o0, o1, o2, o3, o4, q0 + 1)), from));
     const uint32_t wo = lane + sh < 64 ? va : vb;
     const uint32_t ob = uint32_t(__builtin_amdgcn_readfirstlane(int(wo)));
-    const bool fit = lane <= kSrWin && j0 + lane <= n && wo - ob <= lim;
+    const bool fit = lane <= kSrWin && j0 + lane <= n && wo - ob <= lim;  // (kSrWin: uniform)
     const int m = __popcll(__ballot(fit)) - 1;  // samples of the window
     if (m < 1) {  // (every sample is at most seg_lim: TileRun bit 1; an exit every wave reaches)
       if (lane == 0) report_decode(a, MDSX_E_HIP, int(r.shard), int(r.r0) + j0, -1);
@@ -201,14 +238,29 @@ __global__ __launch_bounds__(64 * W) void srows_decode_kernel(const DevArgs a) {
     const uint32_t sp = b + sp0;  // stream position of the sample
     const uint32_t wlo = ob + sp0;
     const uint32_t whi = uint32_t(__builtin_amdgcn_readlane(int(wo), m)) + sp0;
-    ensure<S, kNT>(st, ring, ring_lds, wlo, whi - 1u, lane);  // the window's bytes landed
+    uint4 h4 = z4;
+    if constexpr (kL2) {
+      // the size heads first, then the window's 128-byte lines touched into L2 (one word each):
+      // the heads' wait leaves the touches in flight, and the chunk reads below hit L2
+      if (mine && nvar <= 4) h4 = ldu16(frame + b);
+      // (up to 4 x 8 KiB of lines, lim <= 32 KiB; each word folded into `sink` only after the
+      // window is written, so no wait for a touch is placed before that)
+      const uint64_t l0 = (reinterpret_cast<uint64_t>(frame) + wlo) & ~uint64_t(127);
+      const uint64_t l1 = reinterpret_cast<uint64_t>(frame) + whi;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint64_t q = l0 + 128ull * uint64_t(lane + 64 * i);
+        touch[i] = q < l1 ? *gp_at<const uint32_t>(q) : 0u;
+      }
+    } else {
+      ensure<S, kNT>(st, ring, ring_lds, wlo, whi - 1u, lane);  // the window's bytes landed
+      if (mine && nvar <= 4) h4 = ring16<S>(ring, sp);
+    }
 
     // ---- 2. column boundaries (mds/reader.py:111-125), value records
-    uint4 h4 = z4;
-    if (mine && nvar <= 4) h4 = ring16<S>(ring, sp);
     auto head = [&](int k) -> uint32_t {
       if (nvar <= 4) return k == 0 ? h4.x : k == 1 ? h4.y : k == 2 ? h4.z : h4.w;
-      return ring_u32<S>(ring, sp + 4u * uint32_t(k));
+      return rd32(sp + 4u * uint32_t(k));
     };
     bool ok = mine && hv <= e - b;
     uint64_t need = hv;
@@ -226,9 +278,9 @@ __global__ __launch_bounds__(64 * W) void srows_decode_kernel(const DevArgs a) {
         const uint32_t w = uint32_t(__builtin_amdgcn_readlane(int(rb), c));
         const uint32_t len = ok ? (v >= 0 ? head(v) : w) : 0u;
         if (mine) {
-          rec[c * 32 + lane].len = len;
-          rec[c * 32 + lane].src = sp + rel;
-          rec[c * 32 + lane].dst = v >= 0 ? 0u : uint32_t(lane) * w;
+          rec[c * kRec + lane].len = len;
+          rec[c * kRec + lane].src = sp + rel;
+          rec[c * kRec + lane].dst = v >= 0 ? 0u : uint32_t(lane) * w;
         }
         rel += len;
       }
@@ -242,7 +294,7 @@ __global__ __launch_bounds__(64 * W) void srows_decode_kernel(const DevArgs a) {
         if (lane == c) wtot = uint32_t(m) * w;
         continue;
       }
-      const uint32_t len = mine ? rec[c * 32 + lane].len : 0u;
+      const uint32_t len = mine ? rec[c * kRec + lane].len : 0u;
       const uint32_t incl = wave_incl_dpp(len);
       const uint32_t ex = incl - len;
       const uint32_t tot = uint32_t(__builtin_amdgcn_readlane(int(incl), 63));
@@ -250,7 +302,7 @@ __global__ __launch_bounds__(64 * W) void srows_decode_kernel(const DevArgs a) {
       const MDSX_L DevCol& col = cols[c];
       if (mine) {
         *gp(col.offsets + r.row0 + uint64_t(j0 + lane)) = int64_t(cc + ex);
-        rec[c * 32 + lane].dst = ex;
+        rec[c * kRec + lane].dst = ex;
         if (len) {
           // chunk k of the window's output begins at window byte 16 k - hd; this sample holds
           // the first byte of chunks [k0, k1)
@@ -267,8 +319,8 @@ __global__ __launch_bounds__(64 * W) void srows_decode_kernel(const DevArgs a) {
       const int c = __builtin_ctzll(mm);
       const uint32_t w = uint32_t(__builtin_amdgcn_readlane(int(rb), c));
       if (mine) {
-        const MDSX_L SrRec& q = rec[c * 32 + lane];
-        const uint4 v = q.len ? ring16<S>(ring, q.src) : z4;
+        const MDSX_L SrRec& q = rec[c * kRec + lane];
+        const uint4 v = q.len ? rd16(q.src) : z4;
         store_small(readlane64(data, c) + (r.row0 + uint64_t(j0 + lane)) * w, v, w);
       }
     }
@@ -290,7 +342,7 @@ __global__ __launch_bounds__(64 * W) void srows_decode_kernel(const DevArgs a) {
       const uint4 cy = readlane4(carry, c);
       const bool tail = ((uint32_t(hd) + T) & 15u) != 0;  // the last chunk is partly filled
       const MDSX_L uint8_t* mp = map + uint32_t(v >= 0 ? v : 0) * map_len;
-      const int base = c * 32;
+      const int base = c * kRec;
       uint4 last = z4;
       uint32_t last_lo = 0;
       for (uint32_t kb = 0; kb < K; kb += 64) {  // wave-uniform
@@ -306,7 +358,7 @@ __global__ __launch_bounds__(64 * W) void srows_decode_kernel(const DevArgs a) {
           const MDSX_L SrRec& qa = rec[base + rr];
           const int32_t dsA = int32_t(qa.dst), deA = dsA + int32_t(qa.len);
           const uint32_t pa = qa.src - uint32_t(dsA) + uint32_t(P0);  // stream pos. of byte 0
-          val = ring16<S>(ring, pa);
+          val = rd16(pa);
           const int32_t hiA = min(end, deA);
           bool simple = deA > pos;  // (a fixed column's failed sample: no bytes)
           uint32_t sB = 16;
@@ -316,7 +368,7 @@ __global__ __launch_bounds__(64 * W) void srows_decode_kernel(const DevArgs a) {
             const int32_t dsB = int32_t(qb.dst), deB = dsB + int32_t(qb.len);
             simple = dsB == hiA && deB >= end;
             if (simple) {
-              const uint4 vb4 = ring16<S>(ring, qb.src - uint32_t(dsB) + uint32_t(P0));
+              const uint4 vb4 = rd16(qb.src - uint32_t(dsB) + uint32_t(P0));
               sB = uint32_t(hiA - P0);
               const uint4 mk = byte_mask(0, sB);
               val = make_uint4((val.x & mk.x) | (vb4.x & ~mk.x), (val.y & mk.y) | (vb4.y & ~mk.y),
@@ -331,7 +383,7 @@ __global__ __launch_bounds__(64 * W) void srows_decode_kernel(const DevArgs a) {
                                   : val;
               uint32_t pw = 0;
               if (pos > dsA) {
-                pw = ring_u32<S>(ring, pa + uint32_t(pos - P0) - 4u);
+                pw = rd32(pa + uint32_t(pos - P0) - 4u);
                 const int32_t nv = pos - dsA;  // A's bytes before the chunk
                 if (nv < 4) pw &= ~((1u << (8 * (4 - nv))) - 1u);
               }
@@ -343,8 +395,8 @@ __global__ __launch_bounds__(64 * W) void srows_decode_kernel(const DevArgs a) {
                   if (sB < 16) er |= utf8_open_at(keep_bytes(X, sB, 16), 0, 16) ? 2u : 0u;
                   else er |= utf8_open_at(X, pw, 16) ? 1u : 0u;
                 }
-                if (er & 1u) atomicOr(&bad[c], 1u << rr);
-                if (er & 2u) atomicOr(&bad[c], 1u << (rr + 1));
+                if (er & 1u) atomicOr(&bad[2 * c + (rr >> 5)], 1u << (rr & 31));
+                if (er & 2u) atomicOr(&bad[2 * c + ((rr + 1) >> 5)], 1u << ((rr + 1) & 31));
               }
             }
           } else {
@@ -359,18 +411,18 @@ __global__ __launch_bounds__(64 * W) void srows_decode_kernel(const DevArgs a) {
               if (ds >= end) break;
               const int32_t lo = max(pos, ds), hi = min(end, de);
               const uint32_t p = qq.src - uint32_t(ds) + uint32_t(P0);
-              const uint4 pv = keep_bytes(ring16<S>(ring, p), uint32_t(lo - P0), uint32_t(hi - P0));
+              const uint4 pv = keep_bytes(rd16(p), uint32_t(lo - P0), uint32_t(hi - P0));
               val = make_uint4(val.x | pv.x, val.y | pv.y, val.z | pv.z, val.w | pv.w);
               if (chk) {
                 uint32_t pw = 0;
                 if (lo > ds) {
-                  pw = ring_u32<S>(ring, p + uint32_t(lo - P0) - 4u);
+                  pw = rd32(p + uint32_t(lo - P0) - 4u);
                   const int32_t nv = lo - ds;
                   if (nv < 4) pw &= ~((1u << (8 * (4 - nv))) - 1u);
                 }
                 if ((utf8_chunk_err2(pv, pw, 16) & 1u) ||
                     (hi == de && hi == P0 + 16 && utf8_open_at(pv, pw, 16)))
-                  atomicOr(&bad[c], 1u << q);
+                  atomicOr(&bad[2 * c + (q >> 5)], 1u << (q & 31));
               }
               pos = hi;
             }
@@ -407,11 +459,12 @@ __global__ __launch_bounds__(64 * W) void srows_decode_kernel(const DevArgs a) {
     // ---- 5. str flags of the window; the ring slots below the next window
     for (uint64_t mm = utf8_mask; mm; mm &= mm - 1) {
       const int c = __builtin_ctzll(mm);
-      const uint32_t word = bad[c];
-      if (mine) *gp(cols[c].flags + r.row0 + uint64_t(j0 + lane)) = uint8_t((word >> lane) & 1u);
+      const uint32_t word = bad[2 * c + (lane >> 5)];
+      if (mine) *gp(cols[c].flags + r.row0 + uint64_t(j0 + lane)) = uint8_t((word >> (lane & 31)) & 1u);
     }
-    if (lane < ncols) bad[lane] = 0;
-    pump<S, kNT>(st, ring_lds, whi >> 10, lane);
+    for (int i = lane; i < 2 * ncols; i += 64) bad[i] = 0;
+    if constexpr (!kL2) pump<S, kNT>(st, ring_lds, whi >> 10, lane);
+    else sink ^= touch[0] ^ touch[1] ^ touch[2] ^ touch[3];
     j0 += m;
   }
   // the partly filled last chunk of every wide column (its bytes [clo, cur & 15))
@@ -423,31 +476,49 @@ __global__ __launch_bounds__(64 * W) void srows_decode_kernel(const DevArgs a) {
     wave_edge_store(carry, c, C, C + uint32_t(__builtin_amdgcn_readlane(int(clo), c)), wend,
                     lane);
   }
+  if constexpr (kL2) asm volatile("" ::"v"(sink));  // (the touches' loads are not dead code)
 }
 
 }  // namespace
 
 int launch_srows_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
   constexpr int W = 2;
+  const bool l2 = plan->srows == 2;  // the samples read from L2, no ring
   const unsigned grid = (a.ntiles + W - 1) / W;
   const size_t lds = sr_cols_lds(a.ncols) + size_t(W) * sr_wave_lds(int(a.srows_slots), a.ncols,
-                                                                     a.nvar, a.seg_lim);
+                                                                     a.nvar, a.seg_lim, l2);
   if (lds > 160 * 1024)
     return mdsx::fail(MDSX_E_ARG, "mdsx: streaming row-parallel decode LDS exceeds 160 KiB");
-  if (a.seg_lim + 2048u > a.srows_slots * 1024u)
+  if (!l2 && a.seg_lim + 2048u > a.srows_slots * 1024u)
     return mdsx::fail(MDSX_E_ARG, "mdsx: streaming row-parallel window larger than its ring");
   const bool nt = plan->rows_nt != 0;
+  if (l2) {
+    const void* fn = nt ? reinterpret_cast<const void*>(srows_decode_kernel<0, true, W, true>)
+                        : reinterpret_cast<const void*>(srows_decode_kernel<0, false, W, true>);
+    if (lds > 64 * 1024) {
+      const int rc = hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   int(lds)), "hipFuncSetAttribute");
+      if (rc != MDSX_OK) return rc;
+    }
+    mdsx::set_last_kernel(nt ? "srows_decode_kernel<0, true, 2, true>"
+                             : "srows_decode_kernel<0, false, 2, true>");
+    if (nt)
+      hipLaunchKernelGGL((srows_decode_kernel<0, true, W, true>), dim3(grid), dim3(64 * W), lds, s, a);
+    else
+      hipLaunchKernelGGL((srows_decode_kernel<0, false, W, true>), dim3(grid), dim3(64 * W), lds, s, a);
+    return hip_check(hipGetLastError(), "srows_decode_kernel launch");
+  }
 #define MDSX_SR_CASE(S, NT)                                                                     \
   if (a.srows_slots == S && nt == NT) {                                                         \
     if (lds > 64 * 1024) {                                                                      \
       const int rc = hip_check(                                                                 \
-          hipFuncSetAttribute(reinterpret_cast<const void*>(srows_decode_kernel<S, NT, W>),    \
+          hipFuncSetAttribute(reinterpret_cast<const void*>(srows_decode_kernel<S, NT, W, false>), \
                               hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)),            \
           "hipFuncSetAttribute");                                                               \
       if (rc != MDSX_OK) return rc;                                                             \
     }                                                                                           \
-    mdsx::set_last_kernel("srows_decode_kernel<" #S ", " #NT ", 2>");                           \
-    hipLaunchKernelGGL((srows_decode_kernel<S, NT, W>), dim3(grid), dim3(64 * W), lds, s, a);   \
+    mdsx::set_last_kernel("srows_decode_kernel<" #S ", " #NT ", 2, false>");                    \
+    hipLaunchKernelGGL((srows_decode_kernel<S, NT, W, false>), dim3(grid), dim3(64 * W), lds, s, a); \
     return hip_check(hipGetLastError(), "srows_decode_kernel launch");                          \
   }
   MDSX_SR_CASE(6, true)

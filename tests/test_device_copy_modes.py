@@ -68,6 +68,9 @@ MODES = {
     # it lists; a 6 KiB ring (4 KiB windows) with small tiles and a 2 KiB fallback stage
     'srows': 'rows=-1,srows=1,rmin=1000000000',
     'srows_small': 'rows=2,srows=1,srkb=6,srtile=8,rmin=1000000000',
+    # ... its samples read from L2 (no ring); 2 KiB windows with a 2 KiB fallback stage
+    'srows_l2': 'rows=-1,srows=2,rmin=1000000000',
+    'srows_l2_small': 'rows=2,srows=2,srlim=2,srtile=8,rmin=1000000000',
     'gather': 'run=0,rows=0,gmin=1000000000',
     'group': 'run=0,rows=0,gmin=0,gmax=1000000000',
     'group_nt': 'run=0,rows=0,gmin=0,gmax=1000000000,strc=0',  # str rows streamed (non-temporal) too

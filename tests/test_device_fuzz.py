@@ -34,6 +34,7 @@ MODES = {
     'rows_small': 'rows=2,rmin=1000000000',  # row-parallel, 2 KiB stage (windows, huge rows)
     'rows_pipe': 'rows=4,rpipe=5,rmin=1000000000',  # ... two stages, next tile's DMA in flight
     'srows': 'rows=-1,srows=1,srkb=6,rmin=1000000000',  # streaming row-parallel + listed tiles
+    'srows_l2': 'rows=-1,srows=2,srlim=3,rmin=1000000000',  # ... read from L2, 3 KiB windows
     'register': 'run=0,rows=0',  # the register decode (+ gather / groups per column)
 }
 # the single pass (mdsx_decode_shards_single), fresh and re-run with known totals
