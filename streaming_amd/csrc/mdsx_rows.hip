@@ -494,8 +494,10 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
         if constexpr (kFlat) {
           if (ncols <= kEnds + 1) {  // uniform: the ends in scalar registers
 #pragma unroll
-            for (int j = 0; j < kEnds; ++j)
+            for (int j = 0; j < kEnds; ++j) {
+              if (j + 1 >= ncols) break;  // (uniform: a narrow schema compares ncols - 1 ends)
               if (kg >= ends[j]) c = j + 1, c0 = ends[j];
+            }
           } else {
             for (int j = 0; j + 1 < ncols; ++j) {
               const uint32_t e = s_ends[j];
