@@ -418,10 +418,16 @@ def step(leg, k, n, ev):
         leg.dec.run(ev)
 
 
+REWARM = 2  # untimed steps before each block: the other config's block left this one's buffers cold
+
+
 def timed_block(args, leg, nsteps, world, dev):
-    """``nsteps`` steps between barrier + synchronize on both sides; the same-run copy ceiling
-    right after them."""
+    """``nsteps`` steps between barrier + synchronize on both sides, after REWARM untimed ones
+    (interleaved with the other config's block and copy probe, a block's first launches ran 1-9 %
+    slower: profiles/r05/final); the same-run copy ceiling right after them."""
     from streaming_amd.distributed import max_over_ranks
+    for k in range(REWARM):
+        step(leg, k, REWARM, None)
     nev = 4 if leg.ahead else 3
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(nev)] for _ in range(nsteps)]
     span = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -506,6 +512,7 @@ def finish(args, leg, world, rank, tmpdir):
         'ms_per_step_blocks': {'median': float(np.median(spb)), 'min': float(np.min(spb)),
                                'max': float(np.max(spb)), 'blocks': len(spb)},
         'blocks': blocks,
+        'rewarm': REWARM,
         'config': {
             'workload': leg.desc,
             'workload_key': key,
@@ -516,6 +523,8 @@ def finish(args, leg, world, rank, tmpdir):
             'output_bytes_per_gpu': W,
             'parallelism': f'{world} GPU(s), global shard g -> rank g % {world}, no data-path '
                            f'collectives',
+            'blocks': (f'the K timed steps in {len(leg.blocks)} blocks interleaved with the other '
+                       f'config\'s, each after {REWARM} untimed steps'),
             'step': ('scan pass of step k+1 on a side stream beside the decode of step k '
                      '(ScanAheadDecoder); both passes of every timed step inside the timed region'
                      if leg.ahead else 'scan pass then decode, one stream'),
@@ -614,6 +623,7 @@ def main(argv=None):
             'per_rank': head['per_rank'],
             'ms_per_step_blocks': head['ms_per_step_blocks'],
             'blocks': head['blocks'],
+            'rewarm': head['rewarm'],
             # the timing barrier / max-over-ranks / report gather: a torch.distributed process
             # group ('nccl' = RCCL on ROCm) when one is up, else none (one process, no group)
             'process_group': (f'{torch.distributed.get_backend()}, {world} rank(s)'

@@ -102,7 +102,14 @@ def main(out):
             same = [c for c in configs(lines[0]) if c['roofline']['kernel'] == kernel]
             block = durs if len(same) == 1 else durs[idx * len(durs) // len(same):
                                                       (idx + 1) * len(durs) // len(same)]
-            timed = block[-steps:]
+            # the bench's blocks (bench.py timed_block): each block's timed launches follow its
+            # `rewarm` untimed ones; walked back from the config's last launch
+            sizes = [b['steps'] for b in cfg.get('blocks', [])] or [steps]
+            rewarm = int(cfg.get('rewarm', 0))
+            timed, pos = [], len(block)
+            for nb in reversed(sizes):
+                timed = block[max(pos - nb, 0):pos] + timed
+                pos -= nb + rewarm
             avg = sum(timed) / len(timed)
             algo = e['algorithmic_bytes_per_launch']
             e['trace_timed'] = {
