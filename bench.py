@@ -332,13 +332,15 @@ def committed_traffic(key, kernel):
 COPY_VARIANTS = (1, 3, 4, 5, 6)  # include/mdsx.h mdsx_copy_probe_variant shapes
 
 
-def copy_ceiling(batch, iters=10):
+def copy_ceiling(batch, iters=10, dst=None):
     """The same-run copy ceiling: a read+write streaming copy of the batch's shard bytes in each
-    probe shape (include/mdsx.h), interleaved launch by launch; the fastest shape's median (GB/s)."""
+    probe shape (include/mdsx.h), interleaved launch by launch; the fastest shape's median (GB/s).
+    ``dst``: the copy's destination (default: allocated here and freed)."""
     from streaming_amd import _native
     lib = _native.lib()
     src = batch.buffer
-    dst = torch.empty_like(src)
+    if dst is None:
+        dst = torch.empty_like(src)
     stream = torch.cuda.current_stream(src.device)
     ev = {v: [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(iters + 1)] for v in COPY_VARIANTS}
@@ -401,6 +403,12 @@ def prepare(args, config, world, rank, dev):
         verify(config, out, leg.synth.sources)
     for k in range(args.warmup):
         step(leg, k, args.warmup, None)
+    # the copy probe's destination, allocated (and the probe run once) before any timed block: a
+    # large allocation made between blocks slowed the next config's first block by 9-12 %
+    # (profiles/r05/final)
+    leg.copy_dst = torch.empty_like(batch.buffer) if args.copy_probe else None
+    if args.copy_probe:
+        copy_ceiling(batch, iters=1, dst=leg.copy_dst)
     torch.cuda.synchronize(dev)
     leg.R = batch.shard_bytes
     leg.W = output_bytes(plan, leg.dec.result())
@@ -452,7 +460,7 @@ def timed_block(args, leg, nsteps, world, dev):
         scan_ms = [e[0].elapsed_time(e[1]) for e in events]
     leg.decode_ms += dec_ms
     leg.scan_ms += scan_ms
-    copy = copy_ceiling(leg.synth.batch) if args.copy_probe else None
+    copy = copy_ceiling(leg.synth.batch, dst=leg.copy_dst) if args.copy_probe else None
     kern = float(np.mean(dec_ms))
     achieved = (leg.R + leg.W) / kern / 1e6
     leg.blocks.append({
@@ -559,7 +567,7 @@ def finish(args, leg, world, rank, tmpdir):
     # (the other ranks wait for it at the next barrier, outside any timed region)
     if rank == 0 and args.cpu_seconds > 0:
         result['cpu_baseline'] = cpu_baseline(args, config, leg.synth, tmpdir)
-    leg.dec = leg.synth = None
+    leg.dec = leg.synth = leg.copy_dst = None
     torch.cuda.empty_cache()
     return result
 
