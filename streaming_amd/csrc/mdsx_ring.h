@@ -85,13 +85,18 @@ struct Stream {
 };
 
 // Issue slots while they fit in the ring above slot `low`: the stream bytes still to be read
-// all lie in slots >= low (callers pass a non-decreasing low).
-template <int S, bool kNT>
+// all lie in slots >= low (callers pass a non-decreasing low). kEdge: the stream's first and
+// last slots -- the lines it shares with the neighbouring streams -- load with the default
+// cache policy (the others with kNT), so that the neighbour's read of a shared line can hit L2.
+template <int S, bool kNT, bool kEdge = false>
 __device__ __forceinline__ void pump(Stream& st, uint32_t ring_lds, uint32_t low, int lane) {
   while (st.issued < st.nslots && st.issued < low + S) {
     const uint32_t k = st.issued * 64u + uint32_t(lane);
     const uint32_t slot = st.issued % uint32_t(S);
-    glds16<kNT>(st.base + min(k, st.nq - 1), ring_lds + (slot << 10));
+    if (kEdge && (st.issued == 0 || st.issued + 1 == st.nslots))
+      glds16<false>(st.base + min(k, st.nq - 1), ring_lds + (slot << 10));
+    else
+      glds16<kNT>(st.base + min(k, st.nq - 1), ring_lds + (slot << 10));
     if (lane == int(slot)) st.op_at = st.ops;
     ++st.ops;
     ++st.issued;
@@ -100,10 +105,10 @@ __device__ __forceinline__ void pump(Stream& st, uint32_t ring_lds, uint32_t low
 
 // pump, then wait until stream bytes [lo, hi] (hi - lo < (S - 1) KiB) have landed; a slot at ring
 // position 0 that has landed is mirrored behind the ring for the reads that wrap.
-template <int S, bool kNT>
+template <int S, bool kNT, bool kEdge = false>
 __device__ __forceinline__ void ensure(Stream& st, const lds_u8* ring, uint32_t ring_lds,
                                        uint32_t lo, uint32_t hi, int lane) {
-  pump<S, kNT>(st, ring_lds, lo >> 10, lane);
+  pump<S, kNT, kEdge>(st, ring_lds, lo >> 10, lane);
   const uint32_t upto = min(hi >> 10, st.nslots - 1);
   if (upto < st.landed) return;  // waited for already
   st.landed = upto + 1;

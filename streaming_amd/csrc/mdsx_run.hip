@@ -103,12 +103,19 @@ __host__ __device__ __forceinline__ uint32_t seg_wave_lds(int S, int TR, int nva
 // has consumed after each step (not after the whole value), so the next sample's slots go in
 // flight while the value is still being written; 4 waits per 1 KiB step (not once per sample);
 // 8 (ablation, outputs incomplete) stores no partial edge chunk; 32 touches the run's lines
-// beyond the ring's first fill at the start (seg_decode_kernel).
+// beyond the ring's first fill at the start (seg_decode_kernel); 128: the chunks in the run's
+// first and last 128-byte line of the column (relative to base: outside [nlo, nhi)) -- lines
+// the neighbouring runs write too -- store with the default policy, the others with kNT, so
+// the two runs' pieces of a shared line can meet in L2 (and the stream's first and last ring
+// slots load so); 256 the stores alone, 512 the loads alone; 1024 (with 256): the policy chosen
+// per 64-chunk step (default when the step touches such a line), not per lane.
 template <int S, bool kNT, int kV = 0>
 __device__ __forceinline__ bool seg_copy(Stream& st, const lds_u8* ring, uint32_t ring_lds,
                                          uint64_t base, uint32_t cst, uint32_t d, uint32_t len,
                                          uint32_t p, bool utf8, bool zero, uint4& carry,
-                                         int lane) {
+                                         int lane, uint32_t nlo = 0, uint32_t nhi = 0) {
+  constexpr bool kE = (kV & (128 | 512)) != 0;
+  constexpr bool kES = (kV & (128 | 256)) != 0;
   uint32_t& ops = st.ops;
   const uint32_t head = d & 15u, dbeg = d - head, dend = d + len;
   const uint32_t nch = (dend - dbeg + 15u) >> 4;  // chunks touched
@@ -125,11 +132,24 @@ __device__ __forceinline__ bool seg_copy(Stream& st, const lds_u8* ring, uint32_
     const uint32_t kk = g + uint32_t(lane);
     const uint32_t gend = min(s0 + 16u * (g + 64u), p + len);  // this step's stream bytes end
     if constexpr ((kV & 4) != 0)
-      if (!zero) ensure<S, kNT>(st, ring, ring_lds, g ? s0 + 16u * g : p, gend - 1u, lane);
+      if (!zero) ensure<S, kNT, kE>(st, ring, ring_lds, g ? s0 + 16u * g : p, gend - 1u, lane);
     uint4 val = zero ? z4 : ring16<S>(ring, s0 + 16u * kk);
     if (g == 0 && head && lane == 0) val = splice_lo(carry, val, head);
     const bool skip0 = shared0 && g == 0;
-    if (kk < nfull && !(skip0 && lane == 0)) st16<kNT>(out + 16ull * kk, val);
+    if (kk < nfull && !(skip0 && lane == 0)) {
+      if constexpr (kES && (kV & 1024) != 0) {
+        if (dbeg + 16u * g >= nlo && dbeg + 16u * min(g + 64u, nfull) <= nhi)  // wave-uniform
+          st16<kNT>(out + 16ull * kk, val);
+        else
+          st16<false>(out + 16ull * kk, val);
+      } else if constexpr (kES) {
+        const uint32_t rk = dbeg + 16u * kk;
+        if (rk >= nlo && rk + 16u <= nhi) st16<kNT>(out + 16ull * kk, val);
+        else st16<false>(out + 16ull * kk, val);
+      } else {
+        st16<kNT>(out + 16ull * kk, val);
+      }
+    }
     if (min(nfull, g + 64u) > g + (skip0 ? 1u : 0u)) ++ops;  // that store was issued
     if ((kV & 8) == 0)
       if (skip0 && nfull > 0) wave_edge_store(val, 0, out, base + cst, out + 16, lane);
@@ -147,7 +167,7 @@ __device__ __forceinline__ bool seg_copy(Stream& st, const lds_u8* ring, uint32_
       prev_w = __builtin_amdgcn_readlane(vout.w, 63);
     }
     if (tail && nch - 1 - g < 64u) last = readlane4(val, int(nch - 1 - g));
-    if constexpr ((kV & 2) != 0) pump<S, kNT>(st, ring_lds, gend >> 10, lane);
+    if constexpr ((kV & 2) != 0) pump<S, kNT, kE>(st, ring_lds, gend >> 10, lane);
   }
   carry = last;
   return utf8 ? __any(bad) != 0 : false;
@@ -170,7 +190,7 @@ __device__ __forceinline__ uint64_t seg_clock() {
 }
 
 // The run's bytes: one range starting on a 128-byte line, its first S KiB in flight at once.
-template <int S, bool kNT>
+template <int S, bool kNT, bool kE = false>
 __device__ __forceinline__ uint64_t seg_stream_start(Stream& st, const TileRun& r, uint64_t batch,
                                                      uint32_t ring_lds, int lane) {
   const uint64_t sbase = (batch + r.stream) & ~uint64_t(127);
@@ -181,7 +201,7 @@ __device__ __forceinline__ uint64_t seg_stream_start(Stream& st, const TileRun& 
   st.op_at = 0;
   st.mirrored = 0xffffffffu;
   st.landed = 0;
-  pump<S, kNT>(st, ring_lds, 0, lane);
+  pump<S, kNT, kE>(st, ring_lds, 0, lane);
   return sbase;
 }
 
@@ -192,6 +212,8 @@ __device__ __forceinline__ uint64_t seg_stream_start(Stream& st, const TileRun& 
 template <int S, bool kNT, int W, bool kProf = false, int kV = 0>
 __global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr bool kE = (kV & (128 | 512)) != 0;  // boundary slots: default policy
+  constexpr bool kES = (kV & (128 | 256)) != 0;  // boundary lines' stores: default policy
   const uint64_t t_start = kProf ? seg_clock() : 0;
   uint64_t t_wait = 0, t_first = 0;
   const int t = threadIdx.x, lane = t & 63;
@@ -225,14 +247,14 @@ __global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) 
       ++st.ops;
     }
     r = a.tile_run[tile];
-    if (r.fast & 2) sbase = seg_stream_start<S, kNT>(st, r, batch, ring_lds, lane);
+    if (r.fast & 2) sbase = seg_stream_start<S, kNT, kE>(st, r, batch, ring_lds, lane);
     wait_vm_exact16(st.issued);  // the table's loads landed (issued before the ring's)
   } else {
     for (int c = t; c < a.ncols; c += 64 * W) s_cols[c] = a.cols[c];
     __syncthreads();
     if (tile >= a.ntiles) return;  // wave-uniform; no barrier below
     r = a.tile_run[tile];
-    if (r.fast & 2) sbase = seg_stream_start<S, kNT>(st, r, batch, ring_lds, lane);
+    if (r.fast & 2) sbase = seg_stream_start<S, kNT, kE>(st, r, batch, ring_lds, lane);
   }
   if constexpr ((kV & 32) != 0) {
     // the run's 128-byte lines beyond the ring's first fill, touched now (one 4-byte LDS-DMA
@@ -271,7 +293,7 @@ __global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) 
 
   // column facts and cursors, lane-distributed (lane c: column c)
   int vi = -1;
-  uint32_t rb = 0, meta = 0, cur = 0;
+  uint32_t rb = 0, meta = 0, cur = 0, nlo = 0, nhi = 0;
   uint64_t base = 0;
   bool small = false, wide = false;
   if (lane < ncols) {
@@ -295,6 +317,12 @@ __global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) 
     wide = !small && !skip;
     base = first & ~uint64_t(15);
     cur = uint32_t(first & 15);
+    if constexpr (kES) {  // the run's lines of the column no neighbouring run writes
+      const uint64_t end = first + (vi >= 0 ? uint64_t(a.tile_total[uint64_t(vi) * a.nscan + tile])
+                                            : uint64_t(n) * rb);
+      nlo = uint32_t(((first + 127) & ~uint64_t(127)) - base);
+      nhi = uint32_t(max(end & ~uint64_t(127), base) - base);
+    }
   }
   const uint32_t cst = cur;
   uint4 carry = make_uint4(0, 0, 0, 0);
@@ -312,13 +340,34 @@ __global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) 
     uint64_t t_w0 = 0;
     if constexpr (kProf) t_w0 = seg_clock();
     if constexpr ((kV & 4) != 0)  // the heads; every value's bytes are waited for step by step
-      ensure<S, kNT>(st, ring, ring_lds, sp, sp + min(size, hv) + 3u, lane);
+      ensure<S, kNT, kE>(st, ring, ring_lds, sp, sp + min(size, hv) + 3u, lane);
     else
-      ensure<S, kNT>(st, ring, ring_lds, sp, sp + size + 15u, lane);  // ALL of the sample's bytes
+      ensure<S, kNT, kE>(st, ring, ring_lds, sp, sp + size + 15u, lane);  // ALL of the sample's bytes
     if constexpr (kProf) {
       const uint64_t now = seg_clock();
       if (j == 0) t_first = now - t_start;
       else t_wait += now - t_w0;
+    }
+    if constexpr ((kV & 64) != 0) {
+      // (measurement only, outputs incomplete) column 0 alone -- a ragged column whose value
+      // comes first after the heads (config C's `b`) -- copied through the ring; no geometry, no
+      // other column, no str check (with bit 16: no per-run outputs either)
+      const int c0 = 0;
+      const uint32_t len0 = uint32_t(__builtin_amdgcn_readfirstlane(int(ring_u32<S>(ring, sp))));
+      const uint32_t l = ((wide_mask & 1ull) && hv + len0 <= size) ? len0 : 0u;  // else nothing
+      const uint32_t d = uint32_t(__builtin_amdgcn_readlane(int(cur), c0));
+      uint4 cy = (d & 15u) ? readlane4(carry, c0) : make_uint4(0, 0, 0, 0);
+      if (vi == 0 && lane == 0) obuf[j] = d;
+      seg_copy<S, kNT, 0>(st, ring, ring_lds, readlane64(base, c0),
+                          uint32_t(__builtin_amdgcn_readlane(int(cst), c0)), d, l, sp + hv, false,
+                          false, cy, lane);
+      if (lane == c0) {
+        cur = d + l;
+        carry = cy;
+      }
+      pump<S, kNT, kE>(st, ring_lds, (sp + size) >> 10, lane);
+      ++j;
+      continue;
     }
     // column geometry, lane c: size head (ragged) or row size (fixed), place by prefix sum
     uint32_t len = 0;
@@ -349,7 +398,7 @@ __global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) 
       if constexpr ((kV & 4) != 0) {
         if ((small_mask >> c) & 1ull) {
           const uint32_t w = uint32_t(__builtin_amdgcn_readlane(int(rb), c));
-          if (ok) ensure<S, kNT>(st, ring, ring_lds, p, p + w - 1u, lane);
+          if (ok) ensure<S, kNT, kE>(st, ring, ring_lds, p, p + w - 1u, lane);
           const uint4 v = ok ? ring16<S>(ring, p) : make_uint4(0, 0, 0, 0);
           if (lane == c) lds_put(sbuf + soff + uint32_t(j) * w, v, w);
           continue;
@@ -362,14 +411,16 @@ __global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) 
       const uint32_t cs = uint32_t(__builtin_amdgcn_readlane(int(cst), c));
       uint4 cy = (d & 15u) ? readlane4(carry, c) : make_uint4(0, 0, 0, 0);
       const bool utf8 = (mc >> 8) & 1u;
-      const bool bad = seg_copy<S, kNT, kV>(st, ring, ring_lds, readlane64(base, c), cs, d, l, p,
-                                            utf8, !ok, cy, lane);
+      const bool bad = seg_copy<S, kNT, kV>(
+          st, ring, ring_lds, readlane64(base, c), cs, d, l, p, utf8, !ok, cy, lane,
+          kES ? uint32_t(__builtin_amdgcn_readlane(int(nlo), c)) : 0u,
+          kES ? uint32_t(__builtin_amdgcn_readlane(int(nhi), c)) : 0u);
       if (lane == c) {
         cur = d + l;
         carry = cy;
       }
       if (bad && lane == 0) fbuf[(int(mc & 255u) - 1) * TR + j] = 1;
-      pump<S, kNT>(st, ring_lds, (p + l) >> 10, lane);  // the bytes before p + l are done
+      pump<S, kNT, kE>(st, ring_lds, (p + l) >> 10, lane);  // the bytes before p + l are done
     }
     ++j;
   }
@@ -463,7 +514,8 @@ int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
     return hip_check(hipGetLastError(), "seg_decode_kernel launch");                          \
   }
       MDSX_SEG_V(1) MDSX_SEG_V(2) MDSX_SEG_V(3) MDSX_SEG_V(4) MDSX_SEG_V(8) MDSX_SEG_V(16)
-      MDSX_SEG_V(7) MDSX_SEG_V(24) MDSX_SEG_V(32) MDSX_SEG_V(33)
+      MDSX_SEG_V(7) MDSX_SEG_V(24) MDSX_SEG_V(32) MDSX_SEG_V(33) MDSX_SEG_V(80) MDSX_SEG_V(128)
+      MDSX_SEG_V(256) MDSX_SEG_V(512) MDSX_SEG_V(1280)
 #undef MDSX_SEG_V
       return mdsx::fail(MDSX_E_ARG, "mdsx: seg variant out of range");
     }

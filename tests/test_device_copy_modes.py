@@ -41,6 +41,7 @@ MODES = {
     'seg8': 'run=8,seg=1,rmin=0',
     'seg7': 'run=7,seg=1,rmin=0',  # a 7 KiB ring (not a power of two: modulo addressing)
     'seg7_touch': 'run=7,seg=1,rmin=0,rnt=1,sv=32',  # ... the run's lines past the ring touched
+    'seg7_edge': 'run=7,seg=1,rmin=0,rnt=1,sv=128',  # ... shared boundary lines: default policy
     'run7': 'run=7,rmin=0',  # ... the general path through it
     'seg16': 'run=16,seg=1,rmin=0,rkb=1024',
     'seg8_nt': 'run=8,seg=1,rmin=0,rnt=1',

@@ -29,6 +29,7 @@ MODES = {
     'seg16': 'run=16,seg=1,rmin=0,rkb=64',
     'seg7': 'run=7,seg=1,rmin=0,rkb=12',  # a ring of 7 slots (modulo addressing)
     'seg7_v7': 'run=7,seg=1,rmin=0,rkb=12,sv=7',  # ... its early prologue, per-step release / waits
+    'seg7_edge': 'run=7,seg=1,rmin=0,rkb=12,sv=128',  # ... boundary lines, default policy
     'seg7_v3': 'run=7,seg=1,rmin=0,sv=3',  # ... early prologue and per-step release, 2-sample runs
     'seg_wg4': 'run=8,seg=1,rmin=0,swg=4',  # four waves per workgroup (the default is two)
     'rows_small': 'rows=2,rmin=1000000000',  # row-parallel, 2 KiB stage (windows, huge rows)
