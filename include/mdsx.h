@@ -331,8 +331,10 @@ int mdsx_copy_probe(const void* d_src, void* d_dst, uint64_t bytes, void* stream
  * flight, non-temporal); 1 one 4 KiB piece per wave, non-temporal loads and stores (the shape of
  * the config-B row copy; what mdsx_copy_probe runs); 2 as 1 with plain loads; 3 as 1 with 8 KiB
  * per wave; 4 as 1 with plain loads and stores; 5 as 1 and 6 as 3 with the workgroups dealt
- * to the 8 XCDs in contiguous ranges (the register decode's tile order). The bench reports the
- * fastest variant of its run as the same-run copy ceiling. */
+ * to the 8 XCDs in contiguous ranges (the register decode's tile order); 7 and 8 as 1 with
+ * unused LDS per workgroup so that only 2 / 3 workgroups (8 / 12 waves) share a CU -- fewer
+ * concurrent streams copy faster on MI355X (scripts/microbench/ring_copy3.hip). The bench
+ * reports the fastest variant of its run as the same-run copy ceiling. */
 int mdsx_copy_probe_variant(const void* d_src, void* d_dst, uint64_t bytes, int variant,
                             void* stream);
 /* Host hand-off copy: a 16-byte streaming kernel storing into PINNED host memory (a

@@ -121,7 +121,8 @@ def main():
     copy_dst = torch.empty_like(base_batch.buffer)
     times = {v: [] for v in args.variants}
     times['torch_copy'] = []
-    probes = [0, 1, 2, 3, 4] if os.environ.get('MDSX_PROBES') else []
+    pe = os.environ.get('MDSX_PROBES', '')  # '1': shapes 0-4; or a list of shapes, '1,5,7,8'
+    probes = [int(x) for x in pe.split(',')] if ',' in pe else [0, 1, 2, 3, 4] if pe else []
     times['mdsx_copy_probe'] = []
     for pv in probes:
         times[f'probe{pv}'] = []

@@ -598,11 +598,11 @@ __device__ __forceinline__ bool group_utf8_bad(const uint8_t* values, uint64_t o
 }
 
 // Fixed column of 1..16 bytes: one row per lane. dst is aligned to the largest power of two
-// dividing the row size (outputs are 256-byte aligned tensors).
-__device__ __forceinline__ void gather_small(const uint8_t* p, uint8_t* dst_, uint32_t size) {
+// dividing the row size (outputs are 256-byte aligned tensors). small_load: the row's bytes
+// (from any alignment) into the low bytes of a chunk; small_store: them to dst.
+__device__ __forceinline__ uint4 small_load(const uint8_t* p, uint32_t size) {
   const uint64_t a = reinterpret_cast<uint64_t>(p);
   const MDSX_G uint32_t* q = gp_at<const uint32_t>(a & ~uint64_t(3));
-  MDSX_G uint8_t* dst = gp(dst_);
   const uint32_t r = uint32_t(a & 3);
   const uint32_t nd = (size + 6) >> 2;  // dwords covering r + size bytes for any r <= 3
   const uint32_t w0 = q[0];
@@ -610,8 +610,12 @@ __device__ __forceinline__ void gather_small(const uint8_t* p, uint8_t* dst_, ui
   const uint32_t w2 = nd > 2 ? q[2] : 0u;
   const uint32_t w3 = nd > 3 ? q[3] : 0u;
   const uint32_t w4 = nd > 4 ? q[4] : 0u;
-  const uint4 o = make_uint4(alignbyte(w1, w0, r), alignbyte(w2, w1, r), alignbyte(w3, w2, r),
-                             alignbyte(w4, w3, r));
+  return make_uint4(alignbyte(w1, w0, r), alignbyte(w2, w1, r), alignbyte(w3, w2, r),
+                    alignbyte(w4, w3, r));
+}
+
+__device__ __forceinline__ void small_store(uint8_t* dst_, const uint4 o, uint32_t size) {
+  MDSX_G uint8_t* dst = gp(dst_);
   switch (size) {
     case 1: *dst = uint8_t(o.x); break;
     case 2: *(MDSX_G uint16_t*)dst = uint16_t(o.x); break;
@@ -629,6 +633,10 @@ __device__ __forceinline__ void gather_small(const uint8_t* p, uint8_t* dst_, ui
     default:
       for (uint32_t j = 0; j < size; ++j) dst[j] = uint8_t(byte_of(o, int(j)));
   }
+}
+
+__device__ __forceinline__ void gather_small(const uint8_t* p, uint8_t* dst, uint32_t size) {
+  small_store(dst, small_load(p, size), size);
 }
 
 }  // namespace mdsx_kernels

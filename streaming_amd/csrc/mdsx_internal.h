@@ -57,6 +57,10 @@ struct mdsx_plan {
   int xcd_order = 3;       // bits: decodes whose XCDs each take a contiguous range of tiles
                            // (profiles/r03/xcd_order/): 1 the lean path (+3 % on config C), 2 the
                            // register decode (+1.1 % on config B); not 4, the row-parallel (-1 %)
+  int rowwave = -1;        // all-fixed plans: one row per wave, this many waves per workgroup (0:
+                           // decode_kernel; -1: 1 for rows of >= 2 KiB, else 0; MDSX_TUNE rw)
+  int lds_pad_kb = 0;      // dynamic LDS added per workgroup of the register and streaming decodes
+                           // (KiB; MDSX_TUNE lpad): fewer workgroups per CU
   int seg_var = 0;         // lean path, measurement variants (MDSX_TUNE sv, bits; mdsx_run.hip)
   int seg_waves = 2;       // lean path: waves (runs) per workgroup (1, 2 or 4; 2: 18 waves per CU,
                            // +4 % on 3-5 KB samples, profiles/r03/seg_waves/)

@@ -923,6 +923,139 @@ __global__ __launch_bounds__(kBlock) void copy_probe_kernel(const uint4* __restr
   }
 }
 
+// ---- All-fixed plans, one row per wave (MDSX_TUNE rw = waves per workgroup) ----------------
+// decode_kernel reads a tile's offsets into LDS and meets them at a workgroup barrier before any
+// row's bytes are requested, so every row's copy waits for two dependent memory round trips. In
+// an all-fixed schema every sample has the same size, and the writer lays sample i at offsets[0]
+// + i x size (mds/writer.py:133-144: the header, the shard's config bytes, then the samples back
+// to back): this kernel requests the row's bytes from there once offsets[0] is known (one line
+// per shard, read by every wave of it), the row's offsets pair beside them, and stores only once
+// the pair confirms the address; a row whose pair says otherwise takes the checked path from its
+// offsets (decode_kernel's rules and reports: mds/reader.py:137-142 ranges, a row too short for
+// its columns). Reads of the predicted address stay inside the shard. One wave per row, kW waves per workgroup; the launch
+// sets the workgroups per CU (unused LDS): fewer, longer-lived streams copy faster on MI355X.
+template <bool kNT, int kW>
+__global__ __launch_bounds__(64 * kW) void rowwave_decode_kernel(const DevArgs a) {
+  constexpr int U = 4;  // 16-byte chunks per lane in flight: a column of up to 4 KiB in one step
+  const int lane = threadIdx.x & 63;
+  const uint32_t blk =
+      (a.xcd_order & kXcdRegister) ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint32_t w =
+      blk * kW + (kW == 1 ? 0u : uint32_t(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)));
+  const uint32_t TR = uint32_t(a.tile_rows);
+  const uint32_t tile = w / TR, r = w - tile * TR;
+  if (tile >= a.ntiles) return;  // wave-uniform; no barrier in this kernel
+  const TileView v = tile_view(a, tile);
+  if (!v.table_ok) {
+    if (r == 0 && lane == 0 && tile == v.d.tile0)
+      report_decode(a, MDSX_E_HEADER, v.shard_idx, -1, -1);
+    return;
+  }
+  if (r == 0 && lane == 0 && tile == v.d.tile0) {
+    // the shard header (mds/writer.py:133-144): u32 N, then N + 1 offsets
+    const uint32_t n = *reinterpret_cast<const uint32_t*>(v.shard);
+    if (n != v.d.samples || v.offs[0] < v.hdr_end || v.offs[v.d.samples] > v.d.bytes)
+      report_decode(a, MDSX_E_HEADER, v.shard_idx, -1, -1);
+  }
+  if (r >= v.nrows) return;
+  const uint32_t i = v.r0 + r;
+  const uint64_t row = v.d.row0 + i;
+  // the row size, lane c's column offset inside the sample, the first large column
+  const int ncols = a.ncols;
+  uint32_t size = 0, coff = 0, rb = 0, coff_l = 0, rb_l = 0;
+  int cl = -1;
+  for (int c = 0; c < ncols; ++c) {  // uniform
+    const uint32_t b = a.cols[c].row_bytes;
+    if (lane == c) coff = size, rb = b;
+    if (cl < 0 && b > uint32_t(kSmallMax)) cl = c, coff_l = size, rb_l = b;
+    size += b;
+  }
+  const bool small = lane < ncols && rb <= uint32_t(kSmallMax);
+  // the writer's layout: offsets[0] (after the header and the shard's config bytes) + i x size
+  const uint32_t o0 = __builtin_amdgcn_readfirstlane(v.offs[0]);  // (one line per shard: hot)
+  const uint64_t pred = uint64_t(o0) + uint64_t(i) * size;
+  const bool spec = o0 >= v.hdr_end && pred + size <= v.d.bytes;  // wave-uniform
+  const uint32_t ob = lane < 2 ? v.offs[i + uint32_t(lane)] : 0u;  // the row's offsets pair
+  // ---- requested together: the offsets pair, the small columns (lane c: column c) and the first
+  // large column's chunks (wave_copy's realigning layout), from the predicted address
+  uint4 o = make_uint4(0, 0, 0, 0);
+  if (spec && small) o = small_load(v.shard + pred + coff, rb);
+  uint8_t* ldst = cl >= 0 ? static_cast<uint8_t*>(a.cols[cl].data) + row * rb_l : nullptr;
+  const uint64_t d0 = reinterpret_cast<uint64_t>(ldst), dend = d0 + rb_l;
+  const uint64_t dbeg = d0 & ~uint64_t(15);
+  const uint32_t nch = uint32_t((((dend + 15) & ~uint64_t(15)) - dbeg) >> 4);
+  const bool one_step = spec && cl >= 0 && nch <= 64u * U;  // wave-uniform
+  const uint64_t sfirst = reinterpret_cast<uint64_t>(v.shard + pred + coff_l) - (d0 - dbeg);
+  const uint32_t sh = uint32_t(sfirst & 15);
+  const uint4* sal = reinterpret_cast<const uint4*>(sfirst & ~uint64_t(15));
+  const uint32_t nload = nch + (sh ? 1u : 0u);
+  uint4 lo[U];
+  uint4 tail = make_uint4(0, 0, 0, 0);
+  if (one_step) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t k = uint32_t(u) * 64u + uint32_t(lane);
+      lo[u] = k < nload ? ld16<kNT>(sal + k) : make_uint4(0, 0, 0, 0);
+    }
+    if (sh != 0 && lane == 63 && 64u * U < nload) tail = ld16<kNT>(sal + 64u * U);
+  }
+  const uint32_t b = uint32_t(__builtin_amdgcn_readlane(int(ob), 0));
+  const uint32_t e = uint32_t(__builtin_amdgcn_readlane(int(ob), 1));
+  if (spec && b == pred && e >= b && e - b >= size && e <= v.d.bytes) {  // the address holds
+    if (small) small_store(static_cast<uint8_t*>(a.cols[lane].data) + row * rb, o, rb);
+    int c = cl;
+    if (one_step) {  // the first large column from the registers
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t k0 = uint32_t(u) * 64u;
+        if (k0 >= nch) break;  // wave-uniform
+        const uint32_t k = k0 + uint32_t(lane);
+        uint4 out = lo[u];
+        if (sh != 0) {
+          uint4 hi = shfl_down1(lo[u]);
+          const uint4 nxt = (u + 1 < U) ? readlane0(lo[u + 1 < U ? u + 1 : u]) : tail;
+          if (lane == 63) hi = nxt;
+          out = funnel16(lo[u], hi, sh);
+        }
+        const uint64_t D = dbeg + 16ull * k;
+        if (k < nch && D >= d0 && D + 16 <= dend) st16<kNT>(D, out);
+        if (k0 == 0 && (dbeg < d0 || dbeg + 16 > dend)) wave_edge_store(out, 0, dbeg, d0, dend, lane);
+        if (nch > 1 && (dend & 15) != 0 && nch - 1 >= k0 && nch - 1 < k0 + 64)
+          wave_edge_store(out, int(nch - 1 - k0), dbeg + 16ull * (nch - 1), d0, dend, lane);
+      }
+      ++c;
+    }
+    for (uint32_t pos = 0; c >= 0 && c < ncols; ++c) {  // the other large columns (uniform)
+      pos = 0;
+      for (int j = 0; j < c; ++j) pos += a.cols[j].row_bytes;
+      const DevCol& col = a.cols[c];
+      if (col.row_bytes <= uint32_t(kSmallMax)) continue;
+      wave_copy<false, U, kNT>(v.shard + b + pos,
+                               static_cast<uint8_t*>(col.data) + row * col.row_bytes,
+                               col.row_bytes, lane);
+    }
+    return;
+  }
+  // ---- the checked path (decode_kernel's): the row's range and its columns from its offsets
+  uint32_t bb = 0, ee = 0;
+  int rc = sample_range(v, i, &bb, &ee);
+  if (rc == MDSX_OK && uint64_t(bb) + size > ee) rc = MDSX_E_BOUNDS;
+  if (rc != MDSX_OK) {
+    if (lane == 0) report_decode(a, rc, v.shard_idx, int(i), -1);
+    return;
+  }
+  if (small) gather_small(v.shard + bb + coff, static_cast<uint8_t*>(a.cols[lane].data) + row * rb, rb);
+  uint32_t pos = 0;
+  for (int c = 0; c < ncols; ++c) {  // uniform
+    const DevCol& col = a.cols[c];
+    if (col.row_bytes > uint32_t(kSmallMax))
+      wave_copy<false, U, kNT>(v.shard + bb + pos,
+                               static_cast<uint8_t*>(col.data) + row * col.row_bytes,
+                               col.row_bytes, lane);
+    pos += col.row_bytes;
+  }
+}
+
 // The same stream cut per wave: each wave copies its own contiguous kU x 1 KiB (64 lanes x 16 B,
 // kU loads per lane in flight, then kU stores) -- the access shape of the config-B decode's row
 // copy (one 4 KiB row per wave), which outruns the 256 KiB-per-workgroup loop above on MI355X.
@@ -1277,6 +1410,37 @@ static int launch_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s,
   }
   const size_t lds =
       size_t(a.tile_rows) * (12 * size_t(plan->nvar) + 4 * size_t(plan->ncols) + 1) + 16;
+  const size_t dlds = lds + size_t(plan->lds_pad_kb) * 1024;  // (+ unused pad: occupancy)
+  // All-fixed plans of rows >= 2 KiB: one row per wave (rowwave_decode_kernel), its copy issued
+  // before the row's offsets are known -- config B 6.24-6.25 vs 6.01 TB/s for decode_kernel, in
+  // one process (profiles/r05/rowwave/); shorter rows keep decode_kernel's row per lane.
+  uint64_t row_size = 0;
+  for (int c = 0; c < plan->ncols; ++c) row_size += plan->cols[c].row_bytes;
+  const int rw = plan->rowwave >= 0 ? plan->rowwave : (row_size >= 2048 ? 1 : 0);
+  if (plan->nvar == 0 && rw > 0) {
+    const size_t pad = size_t(plan->lds_pad_kb) * 1024;
+    const uint64_t waves = uint64_t(a.ntiles) * uint64_t(a.tile_rows);
+#define MDSX_ROWWAVE(NT, WV)                                                                   \
+  if (bool(plan->nontemporal) == NT && rw == WV) {                                             \
+    const void* fn = reinterpret_cast<const void*>(rowwave_decode_kernel<NT, WV>);              \
+    if (pad > 64 * 1024 &&                                                                     \
+        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(pad)) !=        \
+            hipSuccess)                                                                        \
+      return mdsx::fail(MDSX_E_HIP, "mdsx: rowwave_decode_kernel LDS attribute");             \
+    mdsx::set_last_kernel("rowwave_decode_kernel<" #NT ", " #WV ">");                         \
+    hipLaunchKernelGGL((rowwave_decode_kernel<NT, WV>), dim3(unsigned((waves + WV - 1) / WV)), \
+                       dim3(64 * WV), pad, s, a);                                              \
+    return hip_check(hipGetLastError(), "rowwave_decode_kernel launch");                       \
+  }
+    MDSX_ROWWAVE(true, 1)
+    MDSX_ROWWAVE(true, 2)
+    MDSX_ROWWAVE(true, 4)
+    MDSX_ROWWAVE(false, 1)
+    MDSX_ROWWAVE(false, 2)
+    MDSX_ROWWAVE(false, 4)
+#undef MDSX_ROWWAVE
+    return mdsx::fail(MDSX_E_ARG, "mdsx: rowwave: 1, 2 or 4 waves per workgroup");
+  }
   const bool nt = plan->nontemporal != 0, ragged = plan->nvar > 0;
   // Edge (partial 16-byte chunk) stores are only needed for ragged columns and for large fixed
   // columns whose row size is not a multiple of 16 (outputs are 256-byte aligned).
@@ -1288,7 +1452,11 @@ static int launch_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s,
 #define MDSX_DECODE(U, NT, RG, ED, SG)                                                           \
   do {                                                                                           \
     mdsx::set_last_kernel("decode_kernel<" #U ", " #NT ", " #RG ", " #ED ", " #SG ", 0>");       \
-    hipLaunchKernelGGL((decode_kernel<U, NT, RG, ED, SG>), dim3(a.ntiles), dim3(kBlock), lds, s, \
+    if (dlds > 64 * 1024 &&                                                                      \
+        hipFuncSetAttribute(reinterpret_cast<const void*>(decode_kernel<U, NT, RG, ED, SG>),     \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, int(dlds)) != hipSuccess)\
+      return mdsx::fail(MDSX_E_HIP, "mdsx: decode_kernel LDS attribute");                       \
+    hipLaunchKernelGGL((decode_kernel<U, NT, RG, ED, SG>), dim3(a.ntiles), dim3(kBlock), dlds, s, \
                        a);                                                                       \
   } while (0)
 #define MDSX_DECODE_U(U)                                                 \
@@ -1631,8 +1799,20 @@ int mdsx_copy_probe_variant(const void* d_src, void* d_dst, uint64_t bytes, int 
       hipLaunchKernelGGL((copy_wave_kernel<8, true, true, true>),
                          dim3(unsigned((n + per8 - 1) / per8)), dim3(kBlock), 0, s, src, dst, n);
       break;
+    case 7:
+    case 8: {
+      // as 1, with unused dynamic LDS so that only 2 (7) or 3 (8) workgroups -- 8 or 12 waves --
+      // share a CU: fewer concurrent streams, each with its bytes in flight
+      const int pad = variant == 7 ? 72 * 1024 : 50 * 1024;
+      const void* fn = reinterpret_cast<const void*>(copy_wave_kernel<4, true, true>);
+      if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, pad) != hipSuccess)
+        return mdsx::fail(MDSX_E_HIP, "mdsx_copy_probe_variant: LDS attribute");
+      hipLaunchKernelGGL((copy_wave_kernel<4, true, true>), dim3(unsigned((n + per4 - 1) / per4)),
+                         dim3(kBlock), size_t(pad), s, src, dst, n);
+      break;
+    }
     default:
-      return mdsx::fail(MDSX_E_ARG, "mdsx_copy_probe_variant: variant 0..6");
+      return mdsx::fail(MDSX_E_ARG, "mdsx_copy_probe_variant: variant 0..8");
   }
   return hip_check(hipGetLastError(), "copy probe launch");
 }

@@ -230,6 +230,10 @@ void apply_tuning(mdsx_plan* p) {
       p->srows_tile_kb = int(v);
     } else if (key == "swg" && (v == 1 || v == 2 || v == 4)) {
       p->seg_waves = int(v);
+    } else if (key == "rw" && (v == 0 || v == 1 || v == 2 || v == 4)) {
+      p->rowwave = int(v);
+    } else if (key == "lpad" && v >= 0 && v <= 150) {
+      p->lds_pad_kb = int(v);
     } else if (key == "sv" && v >= 0 && v <= 2047) {
       p->seg_var = int(v);
     } else if (key == "seg") {

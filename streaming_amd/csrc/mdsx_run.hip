@@ -477,7 +477,8 @@ int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
     const int W = plan->seg_waves;
     const size_t slds = seg_cols_lds(a.ncols) +
                         size_t(W) * seg_wave_lds(a.run_slots, a.tile_rows, a.nvar, a.seg_small) +
-                        ((plan->seg_var & 32) ? 256u : 0u);  // (the touch variant's scratch)
+                        ((plan->seg_var & 32) ? 256u : 0u) +  // (the touch variant's scratch)
+                        size_t(plan->lds_pad_kb) * 1024u;     // (+ unused pad: occupancy)
     if (slds > 160 * 1024)
       return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode LDS exceeds 160 KiB");
     const unsigned sgrid = (a.ntiles + unsigned(W) - 1) / unsigned(W);

@@ -37,6 +37,7 @@ MODES = {
     'srows': 'rows=-1,srows=1,srkb=6,rmin=1000000000',  # streaming row-parallel + listed tiles
     'srows_l2': 'rows=-1,srows=2,srlim=3,rmin=1000000000',  # ... read from L2, 3 KiB windows
     'register': 'run=0,rows=0',  # the register decode (+ gather / groups per column)
+    'rowwave': 'rw=1,lpad=12',  # all-fixed plans: one row per wave (others: as the default)
 }
 # the single pass (mdsx_decode_shards_single), fresh and re-run with known totals
 SINGLE_MODES = {
