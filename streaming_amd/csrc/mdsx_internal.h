@@ -59,6 +59,9 @@ struct mdsx_plan {
                            // register decode (+1.1 % on config B); not 4, the row-parallel (-1 %)
   int rowwave = -1;        // all-fixed plans: one row per wave, this many waves per workgroup (0:
                            // decode_kernel; -1: 1 for rows of >= 2 KiB, else 0; MDSX_TUNE rw)
+  int rowwave_occ = 6;     // ... registers bounded for this many waves per SIMD (MDSX_TUNE rwocc;
+                           // 0: the compiler's choice, 85 VGPRs = 5 waves)
+  int rowwave_rows = 1;    // ... rows per wave (MDSX_TUNE rwr: 1, 2, 4)
   int lds_pad_kb = 0;      // dynamic LDS added per workgroup of the register and streaming decodes
                            // (KiB; MDSX_TUNE lpad): fewer workgroups per CU
   int seg_var = 0;         // lean path, measurement variants (MDSX_TUNE sv, bits; mdsx_run.hip)

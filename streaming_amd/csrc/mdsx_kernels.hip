@@ -934,32 +934,51 @@ __global__ __launch_bounds__(kBlock) void copy_probe_kernel(const uint4* __restr
 // offsets (decode_kernel's rules and reports: mds/reader.py:137-142 ranges, a row too short for
 // its columns). Reads of the predicted address stay inside the shard. One wave per row, kW waves per workgroup; the launch
 // sets the workgroups per CU (unused LDS): fewer, longer-lived streams copy faster on MI355X.
-template <bool kNT, int kW>
-__global__ __launch_bounds__(64 * kW) void rowwave_decode_kernel(const DevArgs a) {
+// The large columns of one row, from column c on, from sample byte b of the shard (wave_copy).
+template <int U, bool kNT>
+__device__ __forceinline__ void rowwave_columns(const DevArgs& a, const TileView& v, uint32_t b,
+                                                uint64_t row, int c, int lane) {
+  uint32_t pos = 0;
+  for (int j = 0; j < c; ++j) pos += a.cols[j].row_bytes;
+  for (; c < a.ncols; ++c) {  // uniform
+    const DevCol& col = a.cols[c];
+    if (col.row_bytes > uint32_t(kSmallMax))
+      wave_copy<false, U, kNT>(v.shard + b + pos,
+                               static_cast<uint8_t*>(col.data) + row * col.row_bytes,
+                               col.row_bytes, lane);
+    pos += col.row_bytes;
+  }
+}
+
+// kR consecutive rows per wave (1, 2 or 4; the tile's rows a multiple), all of their bytes in
+// flight together. kOcc > 0: registers bounded for that many waves per SIMD.
+template <bool kNT, int kW, int kR = 1, int kOcc = 0>
+__global__ __launch_bounds__(64 * kW, kOcc > 0 ? kOcc : 1) void rowwave_decode_kernel(const DevArgs a) {
   constexpr int U = 4;  // 16-byte chunks per lane in flight: a column of up to 4 KiB in one step
   const int lane = threadIdx.x & 63;
   const uint32_t blk =
       (a.xcd_order & kXcdRegister) ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
   const uint32_t w =
       blk * kW + (kW == 1 ? 0u : uint32_t(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)));
-  const uint32_t TR = uint32_t(a.tile_rows);
-  const uint32_t tile = w / TR, r = w - tile * TR;
+  const uint32_t per = uint32_t(a.tile_rows) / kR;  // waves per tile
+  const uint32_t tile = w / per, rw0 = (w - tile * per) * kR;
   if (tile >= a.ntiles) return;  // wave-uniform; no barrier in this kernel
   const TileView v = tile_view(a, tile);
   if (!v.table_ok) {
-    if (r == 0 && lane == 0 && tile == v.d.tile0)
+    if (rw0 == 0 && lane == 0 && tile == v.d.tile0)
       report_decode(a, MDSX_E_HEADER, v.shard_idx, -1, -1);
     return;
   }
-  if (r == 0 && lane == 0 && tile == v.d.tile0) {
+  if (rw0 == 0 && lane == 0 && tile == v.d.tile0) {
     // the shard header (mds/writer.py:133-144): u32 N, then N + 1 offsets
     const uint32_t n = *reinterpret_cast<const uint32_t*>(v.shard);
     if (n != v.d.samples || v.offs[0] < v.hdr_end || v.offs[v.d.samples] > v.d.bytes)
       report_decode(a, MDSX_E_HEADER, v.shard_idx, -1, -1);
   }
-  if (r >= v.nrows) return;
-  const uint32_t i = v.r0 + r;
-  const uint64_t row = v.d.row0 + i;
+  if (rw0 >= v.nrows) return;
+  const uint32_t nr = min(uint32_t(kR), v.nrows - rw0);  // this wave's rows
+  const uint32_t i0 = v.r0 + rw0;
+  const uint64_t row0 = v.d.row0 + i0;
   // the row size, lane c's column offset inside the sample, the first large column
   const int ncols = a.ncols;
   uint32_t size = 0, coff = 0, rb = 0, coff_l = 0, rb_l = 0;
@@ -973,86 +992,93 @@ __global__ __launch_bounds__(64 * kW) void rowwave_decode_kernel(const DevArgs a
   const bool small = lane < ncols && rb <= uint32_t(kSmallMax);
   // the writer's layout: offsets[0] (after the header and the shard's config bytes) + i x size
   const uint32_t o0 = __builtin_amdgcn_readfirstlane(v.offs[0]);  // (one line per shard: hot)
-  const uint64_t pred = uint64_t(o0) + uint64_t(i) * size;
-  const bool spec = o0 >= v.hdr_end && pred + size <= v.d.bytes;  // wave-uniform
-  const uint32_t ob = lane < 2 ? v.offs[i + uint32_t(lane)] : 0u;  // the row's offsets pair
-  // ---- requested together: the offsets pair, the small columns (lane c: column c) and the first
-  // large column's chunks (wave_copy's realigning layout), from the predicted address
-  uint4 o = make_uint4(0, 0, 0, 0);
-  if (spec && small) o = small_load(v.shard + pred + coff, rb);
-  uint8_t* ldst = cl >= 0 ? static_cast<uint8_t*>(a.cols[cl].data) + row * rb_l : nullptr;
-  const uint64_t d0 = reinterpret_cast<uint64_t>(ldst), dend = d0 + rb_l;
-  const uint64_t dbeg = d0 & ~uint64_t(15);
-  const uint32_t nch = uint32_t((((dend + 15) & ~uint64_t(15)) - dbeg) >> 4);
-  const bool one_step = spec && cl >= 0 && nch <= 64u * U;  // wave-uniform
-  const uint64_t sfirst = reinterpret_cast<uint64_t>(v.shard + pred + coff_l) - (d0 - dbeg);
-  const uint32_t sh = uint32_t(sfirst & 15);
-  const uint4* sal = reinterpret_cast<const uint4*>(sfirst & ~uint64_t(15));
-  const uint32_t nload = nch + (sh ? 1u : 0u);
-  uint4 lo[U];
-  uint4 tail = make_uint4(0, 0, 0, 0);
-  if (one_step) {
+  const bool spec0 = o0 >= v.hdr_end;
+  // offsets[i0 .. i0 + nr], the rows' offsets pairs: every lane loads the same word and reads it
+  // back with readfirstlane (an active lane's copy: no cross-lane read of a lane that may be
+  // inactive where the register is reloaded)
+  uint32_t obv[kR + 1];
+#pragma unroll
+  for (int k = 0; k <= kR; ++k) obv[k] = k <= int(nr) ? v.offs[i0 + uint32_t(k)] : 0u;
+  // ---- requested together: the offsets, each row's small columns (lane c: column c) and first
+  // large column's chunks (wave_copy's realigning layout), from the predicted addresses
+  const uint64_t data_l = cl >= 0 ? reinterpret_cast<uint64_t>(a.cols[cl].data) : 0;
+  uint4 o[kR];
+  uint4 lo[kR][U];
+  uint4 tail[kR];
+  bool one[kR];
+#pragma unroll
+  for (int j = 0; j < kR; ++j) {
+    const uint64_t pred = uint64_t(o0) + uint64_t(i0 + j) * size;
+    const bool spec = j < int(nr) && spec0 && pred + size <= v.d.bytes;  // wave-uniform
+    o[j] = spec && small ? small_load(v.shard + pred + coff, rb) : make_uint4(0, 0, 0, 0);
+    const uint64_t d0 = data_l + (row0 + j) * rb_l, dend = d0 + rb_l;
+    const uint64_t dbeg = d0 & ~uint64_t(15);
+    const uint32_t nch = uint32_t((((dend + 15) & ~uint64_t(15)) - dbeg) >> 4);
+    one[j] = spec && cl >= 0 && nch <= 64u * U;
+    const uint64_t sfirst = reinterpret_cast<uint64_t>(v.shard + pred + coff_l) - (d0 - dbeg);
+    const uint32_t nload = nch + ((sfirst & 15) ? 1u : 0u);
+    const uint4* sal = reinterpret_cast<const uint4*>(sfirst & ~uint64_t(15));
+    tail[j] = make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t k = uint32_t(u) * 64u + uint32_t(lane);
-      lo[u] = k < nload ? ld16<kNT>(sal + k) : make_uint4(0, 0, 0, 0);
+      lo[j][u] = one[j] && k < nload ? ld16<kNT>(sal + k) : make_uint4(0, 0, 0, 0);
     }
-    if (sh != 0 && lane == 63 && 64u * U < nload) tail = ld16<kNT>(sal + 64u * U);
+    if (one[j] && (sfirst & 15) && lane == 63 && 64u * U < nload) tail[j] = ld16<kNT>(sal + 64u * U);
   }
-  const uint32_t b = uint32_t(__builtin_amdgcn_readlane(int(ob), 0));
-  const uint32_t e = uint32_t(__builtin_amdgcn_readlane(int(ob), 1));
-  if (spec && b == pred && e >= b && e - b >= size && e <= v.d.bytes) {  // the address holds
-    if (small) small_store(static_cast<uint8_t*>(a.cols[lane].data) + row * rb, o, rb);
-    int c = cl;
-    if (one_step) {  // the first large column from the registers
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t k0 = uint32_t(u) * 64u;
-        if (k0 >= nch) break;  // wave-uniform
-        const uint32_t k = k0 + uint32_t(lane);
-        uint4 out = lo[u];
-        if (sh != 0) {
-          uint4 hi = shfl_down1(lo[u]);
-          const uint4 nxt = (u + 1 < U) ? readlane0(lo[u + 1 < U ? u + 1 : u]) : tail;
-          if (lane == 63) hi = nxt;
-          out = funnel16(lo[u], hi, sh);
+  for (int j = 0; j < kR; ++j) {
+    if (j >= int(nr)) break;  // uniform
+    const uint32_t i = i0 + j;
+    const uint64_t row = row0 + j;
+    const uint64_t pred = uint64_t(o0) + uint64_t(i) * size;
+    const uint32_t b = __builtin_amdgcn_readfirstlane(obv[j]);
+    const uint32_t e = __builtin_amdgcn_readfirstlane(obv[j + 1]);
+    if (spec0 && pred + size <= v.d.bytes && b == pred && e >= b && e - b >= size &&
+        e <= v.d.bytes) {  // the predicted address holds
+      if (small) small_store(static_cast<uint8_t*>(a.cols[lane].data) + row * rb, o[j], rb);
+      int c = cl;
+      if (one[j]) {  // the first large column from the registers
+        const uint64_t d0 = data_l + row * rb_l, dend = d0 + rb_l;
+        const uint64_t dbeg = d0 & ~uint64_t(15);
+        const uint32_t nch = uint32_t((((dend + 15) & ~uint64_t(15)) - dbeg) >> 4);
+        const uint32_t sh = uint32_t((reinterpret_cast<uint64_t>(v.shard + pred + coff_l) -
+                                      (d0 - dbeg)) & 15);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t k0 = uint32_t(u) * 64u;
+          if (k0 >= nch) break;  // wave-uniform
+          const uint32_t k = k0 + uint32_t(lane);
+          uint4 out = lo[j][u];
+          if (sh != 0) {
+            uint4 hi = shfl_down1(lo[j][u]);
+            const uint4 nxt = (u + 1 < U) ? readlane0(lo[j][u + 1 < U ? u + 1 : u]) : tail[j];
+            if (lane == 63) hi = nxt;
+            out = funnel16(lo[j][u], hi, sh);
+          }
+          const uint64_t D = dbeg + 16ull * k;
+          if (k < nch && D >= d0 && D + 16 <= dend) st16<kNT>(D, out);
+          if (k0 == 0 && (dbeg < d0 || dbeg + 16 > dend))
+            wave_edge_store(out, 0, dbeg, d0, dend, lane);
+          if (nch > 1 && (dend & 15) != 0 && nch - 1 >= k0 && nch - 1 < k0 + 64)
+            wave_edge_store(out, int(nch - 1 - k0), dbeg + 16ull * (nch - 1), d0, dend, lane);
         }
-        const uint64_t D = dbeg + 16ull * k;
-        if (k < nch && D >= d0 && D + 16 <= dend) st16<kNT>(D, out);
-        if (k0 == 0 && (dbeg < d0 || dbeg + 16 > dend)) wave_edge_store(out, 0, dbeg, d0, dend, lane);
-        if (nch > 1 && (dend & 15) != 0 && nch - 1 >= k0 && nch - 1 < k0 + 64)
-          wave_edge_store(out, int(nch - 1 - k0), dbeg + 16ull * (nch - 1), d0, dend, lane);
+        ++c;
       }
-      ++c;
+      if (c >= 0) rowwave_columns<U, kNT>(a, v, b, row, c, lane);  // the other large columns
+      continue;
     }
-    for (uint32_t pos = 0; c >= 0 && c < ncols; ++c) {  // the other large columns (uniform)
-      pos = 0;
-      for (int j = 0; j < c; ++j) pos += a.cols[j].row_bytes;
-      const DevCol& col = a.cols[c];
-      if (col.row_bytes <= uint32_t(kSmallMax)) continue;
-      wave_copy<false, U, kNT>(v.shard + b + pos,
-                               static_cast<uint8_t*>(col.data) + row * col.row_bytes,
-                               col.row_bytes, lane);
+    // ---- the checked path (decode_kernel's): the row's range and columns from its offsets
+    uint32_t bb = 0, ee = 0;
+    int rc = sample_range(v, i, &bb, &ee);
+    if (rc == MDSX_OK && uint64_t(bb) + size > ee) rc = MDSX_E_BOUNDS;
+    if (rc != MDSX_OK) {
+      if (lane == 0) report_decode(a, rc, v.shard_idx, int(i), -1);
+      continue;
     }
-    return;
-  }
-  // ---- the checked path (decode_kernel's): the row's range and its columns from its offsets
-  uint32_t bb = 0, ee = 0;
-  int rc = sample_range(v, i, &bb, &ee);
-  if (rc == MDSX_OK && uint64_t(bb) + size > ee) rc = MDSX_E_BOUNDS;
-  if (rc != MDSX_OK) {
-    if (lane == 0) report_decode(a, rc, v.shard_idx, int(i), -1);
-    return;
-  }
-  if (small) gather_small(v.shard + bb + coff, static_cast<uint8_t*>(a.cols[lane].data) + row * rb, rb);
-  uint32_t pos = 0;
-  for (int c = 0; c < ncols; ++c) {  // uniform
-    const DevCol& col = a.cols[c];
-    if (col.row_bytes > uint32_t(kSmallMax))
-      wave_copy<false, U, kNT>(v.shard + bb + pos,
-                               static_cast<uint8_t*>(col.data) + row * col.row_bytes,
-                               col.row_bytes, lane);
-    pos += col.row_bytes;
+    if (small)
+      gather_small(v.shard + bb + coff, static_cast<uint8_t*>(a.cols[lane].data) + row * rb, rb);
+    rowwave_columns<U, kNT>(a, v, bb, row, 0, lane);
   }
 }
 
@@ -1412,34 +1438,59 @@ static int launch_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s,
       size_t(a.tile_rows) * (12 * size_t(plan->nvar) + 4 * size_t(plan->ncols) + 1) + 16;
   const size_t dlds = lds + size_t(plan->lds_pad_kb) * 1024;  // (+ unused pad: occupancy)
   // All-fixed plans of rows >= 2 KiB: one row per wave (rowwave_decode_kernel), its copy issued
-  // before the row's offsets are known -- config B 6.24-6.25 vs 6.01 TB/s for decode_kernel, in
-  // one process (profiles/r05/rowwave/); shorter rows keep decode_kernel's row per lane.
+  // before the row's offsets are known, registers bounded for 6 waves per SIMD -- config B, in
+  // one process on each of three boxes: 6.22-6.23 / 6.66 vs 5.96 / 6.51 TB/s for decode_kernel
+  // (5 waves per SIMD: 6.15 / 6.43; profiles/r05/rowwave/); shorter rows keep decode_kernel's
+  // row per lane.
   uint64_t row_size = 0;
   for (int c = 0; c < plan->ncols; ++c) row_size += plan->cols[c].row_bytes;
   const int rw = plan->rowwave >= 0 ? plan->rowwave : (row_size >= 2048 ? 1 : 0);
   if (plan->nvar == 0 && rw > 0) {
     const size_t pad = size_t(plan->lds_pad_kb) * 1024;
-    const uint64_t waves = uint64_t(a.ntiles) * uint64_t(a.tile_rows);
-#define MDSX_ROWWAVE(NT, WV)                                                                   \
-  if (bool(plan->nontemporal) == NT && rw == WV) {                                             \
-    const void* fn = reinterpret_cast<const void*>(rowwave_decode_kernel<NT, WV>);              \
+    const int rr = plan->rowwave_rows;  // rows per wave
+    // registers bounded for rowwave_occ waves per SIMD: built for the default shape (one row per
+    // one-wave workgroup, non-temporal); other shapes take the compiler's bound
+    const int occ = plan->nontemporal && rw == 1 && rr == 1 ? plan->rowwave_occ : 0;
+    if (a.tile_rows % rr != 0)
+      return mdsx::fail(MDSX_E_ARG, "mdsx: rowwave: tile rows not a multiple of rows per wave");
+#define MDSX_ROWWAVE(NT, WV, R)                                                                \
+  if (bool(plan->nontemporal) == NT && rw == WV && rr == R && occ == 0) {                      \
+    const void* fn = reinterpret_cast<const void*>(rowwave_decode_kernel<NT, WV, R>);           \
     if (pad > 64 * 1024 &&                                                                     \
         hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(pad)) !=        \
             hipSuccess)                                                                        \
       return mdsx::fail(MDSX_E_HIP, "mdsx: rowwave_decode_kernel LDS attribute");             \
-    mdsx::set_last_kernel("rowwave_decode_kernel<" #NT ", " #WV ">");                         \
-    hipLaunchKernelGGL((rowwave_decode_kernel<NT, WV>), dim3(unsigned((waves + WV - 1) / WV)), \
+    mdsx::set_last_kernel(R == 1 ? "rowwave_decode_kernel<" #NT ", " #WV ">"                  \
+                                 : "rowwave_decode_kernel<" #NT ", " #WV ", " #R ">");         \
+    const uint64_t waves = uint64_t(a.ntiles) * uint64_t(a.tile_rows / R);                     \
+    hipLaunchKernelGGL((rowwave_decode_kernel<NT, WV, R>), dim3(unsigned((waves + WV - 1) / WV)), \
                        dim3(64 * WV), pad, s, a);                                              \
     return hip_check(hipGetLastError(), "rowwave_decode_kernel launch");                       \
   }
-    MDSX_ROWWAVE(true, 1)
-    MDSX_ROWWAVE(true, 2)
-    MDSX_ROWWAVE(true, 4)
-    MDSX_ROWWAVE(false, 1)
-    MDSX_ROWWAVE(false, 2)
-    MDSX_ROWWAVE(false, 4)
+    MDSX_ROWWAVE(true, 1, 1)
+    MDSX_ROWWAVE(true, 2, 1)
+    MDSX_ROWWAVE(true, 4, 1)
+    MDSX_ROWWAVE(false, 1, 1)
+    MDSX_ROWWAVE(false, 2, 1)
+    MDSX_ROWWAVE(false, 4, 1)
+    MDSX_ROWWAVE(true, 1, 2)
+    MDSX_ROWWAVE(true, 1, 4)
+    MDSX_ROWWAVE(true, 2, 2)
+#define MDSX_ROWWAVE_OCC(OCC)                                                                   \
+  if (occ == OCC) {                                                                            \
+    mdsx::set_last_kernel("rowwave_decode_kernel<true, 1, 1, " #OCC ">");                      \
+    const uint64_t waves = uint64_t(a.ntiles) * uint64_t(a.tile_rows);                         \
+    hipLaunchKernelGGL((rowwave_decode_kernel<true, 1, 1, OCC>), dim3(unsigned(waves)), dim3(64), \
+                       pad, s, a);                                                             \
+    return hip_check(hipGetLastError(), "rowwave_decode_kernel launch");                       \
+  }
+    MDSX_ROWWAVE_OCC(6)
+    MDSX_ROWWAVE_OCC(7)
+    MDSX_ROWWAVE_OCC(8)
+#undef MDSX_ROWWAVE_OCC
 #undef MDSX_ROWWAVE
-    return mdsx::fail(MDSX_E_ARG, "mdsx: rowwave: 1, 2 or 4 waves per workgroup");
+    return mdsx::fail(MDSX_E_ARG, "mdsx: rowwave: 1, 2 or 4 waves per workgroup (rows per wave "
+                                 "2 / 4: 1 wave, nt; 2 / 2 waves, nt)");
   }
   const bool nt = plan->nontemporal != 0, ragged = plan->nvar > 0;
   // Edge (partial 16-byte chunk) stores are only needed for ragged columns and for large fixed

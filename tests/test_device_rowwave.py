@@ -18,11 +18,16 @@ pytestmark = pytest.mark.gpu
 
 MODES = {
     'rw0': 'rw=0',  # decode_kernel (rows of >= 2 KiB take the row-per-wave kernel by default)
-    'rw1': 'rw=1',
-    'rw1_pad': 'rw=1,lpad=12',  # 12 waves per CU
-    'rw2': 'rw=2,lpad=24',
-    'rw4': 'rw=4',
-    'rw1_temporal': 'rw=1,nt=0',
+    'rw1': 'rw=1',  # registers bounded for 6 waves per SIMD (the default)
+    'rw1_occ0': 'rw=1,rwocc=0',  # ... the compiler's choice (5)
+    'rw1_occ8': 'rw=1,rwocc=8',  # ... 8 (spills)
+    'rw1_rows2': 'rw=1,rwr=2,rwocc=0',  # two rows per wave
+    'rw1_rows4': 'rw=1,rwr=4,rwocc=0',
+    'rw1_pad': 'rw=1,rwocc=0,lpad=12',  # 12 waves per CU
+    'rw2': 'rw=2,rwocc=0,lpad=24',
+    'rw2_rows2': 'rw=2,rwr=2,rwocc=0',
+    'rw4': 'rw=4,rwocc=0',
+    'rw1_temporal': 'rw=1,rwocc=0,nt=0',
 }
 FIXED_SETS = [n for n in gu.ALL_SETS
               if all(s is not None for s in gu.index(n)['shards'][0]['column_sizes'])]
