@@ -276,7 +276,7 @@ __device__ __forceinline__ uint32_t draw_ticket(const DevArgs& a, uint32_t* s_ti
 // The LDS-staged decode of ragged plans (mdsx_stage.hip). Pass 1: the ragged bytes of every tile
 // (then scan_totals_kernel, one entry per tile: a.scan_per == 1). Pass 2: every column of every
 // row from each tile's shard bytes staged once in LDS. Return MDSX_OK or a launch error.
-int launch_stage_totals(const DevArgs& a, hipStream_t s);
+int launch_stage_totals(const DevArgs& a, bool nt, hipStream_t s);
 int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s);
 int launch_rows_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s);
 // The streaming row-parallel decode (mdsx_srows.hip): every tile the scan pass marked (TileRun

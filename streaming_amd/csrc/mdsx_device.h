@@ -147,14 +147,15 @@ typedef unsigned int u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 struct Heads {
   uint32_t w[8];
   uint32_t sh;
+  template <bool kNT = false>
   __device__ __forceinline__ void load(const uint8_t* p, int n) {
     const uint64_t a = reinterpret_cast<uint64_t>(p);
     const MDSX_G u32x4a4* q = gp_at<const u32x4a4>(a & ~uint64_t(3));
     sh = uint32_t(a & 3);
-    const u32x4a4 x = q[0];
+    const u32x4a4 x = kNT ? __builtin_nontemporal_load(q) : q[0];
     w[0] = x.x, w[1] = x.y, w[2] = x.z, w[3] = x.w;
     if (4 * n + int(sh) > 16) {
-      const u32x4a4 y = q[1];
+      const u32x4a4 y = kNT ? __builtin_nontemporal_load(q + 1) : q[1];
       w[4] = y.x, w[5] = y.y, w[6] = y.z, w[7] = y.w;
     } else {
       w[4] = w[5] = w[6] = w[7] = 0;

@@ -1387,7 +1387,9 @@ uint64_t mdsx_workspace_bytes(const mdsx_plan* plan, const mdsx_batch* batch) {
 static int scan_pass(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
   int rc = MDSX_OK;
   if (a.ntiles > 0 && (a.run_slots || a.rows_bytes)) {
-    rc = launch_stage_totals(a, s);
+    // heads non-temporal for the row-parallel decode's short samples (plan->scan_nt -1: auto)
+    const bool nt = plan->scan_nt >= 0 ? plan->scan_nt != 0 : a.run_slots == 0;
+    rc = launch_stage_totals(a, nt, s);
     if (rc != MDSX_OK) return rc;
   } else if (a.ntiles > 0) {
     hipLaunchKernelGGL(scan_tiles_kernel, dim3(a.nscan), dim3(kBlock), 0, s, a);

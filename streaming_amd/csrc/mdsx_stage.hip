@@ -28,7 +28,10 @@ namespace mdsx_kernels {
 
 // The totals pass: the ragged bytes of every tile (one thread per row; 256 / TR tiles
 // per workgroup), with the staged kernel's row rule: a row whose range, heads or columns do not
-// fit counts zero.
+// fit counts zero. kNT: the size heads loaded non-temporal (each costs a whole 128-byte line
+// either way; measured 10 % faster at a 254-byte stride, 9 % slower at 4.3 KB:
+// profiles/r05/scan_heads/).
+template <bool kNT>
 __global__ __launch_bounds__(kBlock) void stage_totals_kernel(const DevArgs a) {
   __shared__ int64_t s_part[kBlock / 64][MDSX_MAX_COLUMNS];
   __shared__ uint32_t s_bad[kBlock / 64], s_big[kBlock / 64];
@@ -47,7 +50,7 @@ __global__ __launch_bounds__(kBlock) void stage_totals_kernel(const DevArgs a) {
   }
   const bool few = a.nvar <= kHeadRegs;
   Heads h;
-  if (ok && few) h.load(v.shard + b, a.nvar);
+  if (ok && few) h.template load<kNT>(v.shard + b, a.nvar);
   auto head = [&](int vi) -> uint32_t {
     return few ? h.get(vi) : load_u32_any(v.shard + b + 4u * uint32_t(vi));
   };
@@ -178,9 +181,12 @@ __global__ __launch_bounds__(kBlock) void stage_huge_kernel(const DevArgs a) {
 
 }  // namespace
 
-int launch_stage_totals(const DevArgs& a, hipStream_t s) {
+int launch_stage_totals(const DevArgs& a, bool nt, hipStream_t s) {
   const unsigned grid = unsigned((uint64_t(a.ntiles) * a.tile_rows + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(stage_totals_kernel, dim3(grid), dim3(kBlock), 0, s, a);
+  if (nt)
+    hipLaunchKernelGGL(stage_totals_kernel<true>, dim3(grid), dim3(kBlock), 0, s, a);
+  else
+    hipLaunchKernelGGL(stage_totals_kernel<false>, dim3(grid), dim3(kBlock), 0, s, a);
   return hip_check(hipGetLastError(), "stage_totals_kernel launch");
 }
 
