@@ -78,7 +78,7 @@ def main():
         # '#tag' makes a repeated variant distinct (an identical control)
         spec = v.split('#')[0].split(',')
         knobs = [kv for kv in spec if kv and not kv.startswith('enc=') and kv not in
-                 ('single', 'nocheck', 'ahead')]
+                 ('single', 'nocheck', 'ahead', 'ahead_hi')]
         encs = [kv[4:].split('|') for kv in spec if kv.startswith('enc=')]
         os.environ['MDSX_TUNE'] = ','.join(knobs)
         plan = Plan(names[0], encs[0] if encs else names[1], names[2])
@@ -92,10 +92,11 @@ def main():
             else:
                 dec.outputs, dec._fixed_raw = shared
         decs[v] = dec
-        if 'ahead' in spec:  # the next step's scan on a side stream (ScanAheadDecoder)
+        if 'ahead' in spec or 'ahead_hi' in spec:  # the next step's scan on a side stream
             dec.run()
             dec.check()
-            sad = ScanAheadDecoder(plan, dec.batch, capacities=dec.capacities)
+            sad = ScanAheadDecoder(plan, dec.batch, capacities=dec.capacities,
+                                   priority=-1 if 'ahead_hi' in spec else 0)
             sad.outputs_owner = dec  # (keeps the sizing decoder's buffers alive)
             decs[v] = sad
         if 'nocheck' in spec:  # measurement-only variants (e.g. parts skipped)

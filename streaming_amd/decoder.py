@@ -840,10 +840,14 @@ class ScanAheadDecoder:
     ``run(ahead)`` is one step over the decoder's own batch: the decode of the batch scanned
     before and, with ``ahead``, the scan for the next step beside it (the first call scans its
     own batch first).
+
+    ``priority``: the side stream's priority (torch.cuda.Stream; lower is higher -- a scan whose
+    workgroups are dispatched before the queued decode's as CUs free up).
     """
 
     def __init__(self, plan: Plan, batch: DeviceBatch,
-                 capacities: Optional[dict[str, int]] = None, slots: int = 2) -> None:
+                 capacities: Optional[dict[str, int]] = None, slots: int = 2,
+                 priority: int = 0) -> None:
         if slots < 2:
             raise ValueError('ScanAheadDecoder: at least 2 slots (one scanned while one decodes)')
         self.plan = plan
@@ -851,7 +855,7 @@ class ScanAheadDecoder:
         self.device = batch.device
         self._caps = dict(capacities) if capacities else None
         self._slots = [self._new_slot(batch) for _ in range(slots)]
-        self._side = torch.cuda.Stream(self.device)
+        self._side = torch.cuda.Stream(self.device, priority=priority)
         self._free = list(range(slots))
         self._pending: list[tuple[int, torch.cuda.Event, Optional[torch.cuda.Event]]] = []
         self._last: Optional[int] = None
