@@ -329,7 +329,7 @@ def committed_traffic(key, kernel):
     return None, None
 
 
-COPY_VARIANTS = (1, 3, 4, 5, 6, 7, 8)  # include/mdsx.h mdsx_copy_probe_variant shapes
+COPY_VARIANTS = (1, 3, 4, 5, 6, 7, 8, 9, 10)  # include/mdsx.h mdsx_copy_probe_variant shapes
 
 
 def copy_ceiling(batch, iters=10, dst=None):

@@ -333,7 +333,8 @@ int mdsx_copy_probe(const void* d_src, void* d_dst, uint64_t bytes, void* stream
  * per wave; 4 as 1 with plain loads and stores; 5 as 1 and 6 as 3 with the workgroups dealt
  * to the 8 XCDs in contiguous ranges (the register decode's tile order); 7 and 8 as 1 with
  * unused LDS per workgroup so that only 2 / 3 workgroups (8 / 12 waves) share a CU -- fewer
- * concurrent streams copy faster on MI355X (scripts/microbench/ring_copy3.hip). The bench
+ * concurrent streams copy faster on MI355X (scripts/microbench/ring_copy3.hip); 9 as 5 with one
+ * wave per workgroup, 10 as 9 with unused LDS so that 12 workgroups share a CU. The bench
  * reports the fastest variant of its run as the same-run copy ceiling. */
 int mdsx_copy_probe_variant(const void* d_src, void* d_dst, uint64_t bytes, int variant,
                             void* stream);

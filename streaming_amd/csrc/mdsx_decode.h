@@ -84,6 +84,7 @@ struct DevArgs {
   uint32_t xcd_order;    // kXcd* bits: decodes whose workgroups take XCD-contiguous tile ranges
   uint32_t rows_pipe;    // row-parallel decode: tiles per workgroup through two stages (0: one)
   uint32_t srows_slots;  // streaming row-parallel decode: KiB of its per-wave ring (0: off)
+  uint32_t rw_k;         // (measurement only, rowwave kX bit 2: offsets[0] taken as hdr_end + rw_k)
   uint32_t* tile_list;   // [ntiles] tiles the streaming row-parallel decode leaves to the
                          // row-parallel kernel (count at kSrowsCountOffset)
   uint32_t gather_block0[MDSX_MAX_COLUMNS + 1];  // first gather workgroup of each ragged column

@@ -62,6 +62,8 @@ struct mdsx_plan {
   int rowwave_occ = 6;     // ... registers bounded for this many waves per SIMD (MDSX_TUNE rwocc;
                            // 0: the compiler's choice, 85 VGPRs = 5 waves)
   int rowwave_rows = 1;    // ... rows per wave (MDSX_TUNE rwr: 1, 2, 4)
+  int rowwave_x = 0;       // (measurement only) rowwave kX variants (MDSX_TUNE rwx, rwk)
+  int rowwave_k = 0;
   int scan_nt = -1;        // the scan pass's head loads non-temporal (MDSX_TUNE snt; -1: for the
                            // row-parallel decode's batches)
   int lds_pad_kb = 0;      // dynamic LDS added per workgroup of the register and streaming decodes

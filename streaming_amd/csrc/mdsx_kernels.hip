@@ -807,6 +807,7 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
     return mdsx::fail(MDSX_E_ARG, "mdsx: batch tile_rows must be a power of two in [1, 256]");
   a->stage_debug = uint32_t(plan->stage_debug);
   a->xcd_order = uint32_t(plan->xcd_order);
+  a->rw_k = uint32_t(plan->rowwave_k);
   a->run_slots = use_run_decode(plan, b->bytes, b->rows) ? uint32_t(plan->run_slots) : 0u;
   if (a->run_slots && plan->seg) {
     // lean path: a sample must fit the ring with a slot to spare (seg_decode_kernel)
@@ -951,8 +952,11 @@ __device__ __forceinline__ void rowwave_columns(const DevArgs& a, const TileView
 }
 
 // kR consecutive rows per wave (1, 2 or 4; the tile's rows a multiple), all of their bytes in
-// flight together. kOcc > 0: registers bounded for that many waves per SIMD.
-template <bool kNT, int kW, int kR = 1, int kOcc = 0>
+// flight together. kOcc > 0: registers bounded for that many waves per SIMD. kX (measurement
+// only, MDSX_TUNE rwx; correct only on the writer's layout with rw_k config bytes): bit 1 no
+// offsets pair (every row taken as predicted), bit 2 offsets[0] not loaded (hdr_end + rw_k),
+// bit 4 (outputs incomplete) no small column loaded or stored.
+template <bool kNT, int kW, int kR = 1, int kOcc = 0, int kX = 0>
 __global__ __launch_bounds__(64 * kW, kOcc > 0 ? kOcc : 1) void rowwave_decode_kernel(const DevArgs a) {
   constexpr int U = 4;  // 16-byte chunks per lane in flight: a column of up to 4 KiB in one step
   const int lane = threadIdx.x & 63;
@@ -989,16 +993,18 @@ __global__ __launch_bounds__(64 * kW, kOcc > 0 ? kOcc : 1) void rowwave_decode_k
     if (cl < 0 && b > uint32_t(kSmallMax)) cl = c, coff_l = size, rb_l = b;
     size += b;
   }
-  const bool small = lane < ncols && rb <= uint32_t(kSmallMax);
+  const bool small = !(kX & 4) && lane < ncols && rb <= uint32_t(kSmallMax);
   // the writer's layout: offsets[0] (after the header and the shard's config bytes) + i x size
-  const uint32_t o0 = __builtin_amdgcn_readfirstlane(v.offs[0]);  // (one line per shard: hot)
+  const uint32_t o0 = (kX & 2) ? uint32_t(v.hdr_end) + a.rw_k
+                              : __builtin_amdgcn_readfirstlane(v.offs[0]);  // (one line per shard)
   const bool spec0 = o0 >= v.hdr_end;
   // offsets[i0 .. i0 + nr], the rows' offsets pairs: every lane loads the same word and reads it
   // back with readfirstlane (an active lane's copy: no cross-lane read of a lane that may be
   // inactive where the register is reloaded)
   uint32_t obv[kR + 1];
 #pragma unroll
-  for (int k = 0; k <= kR; ++k) obv[k] = k <= int(nr) ? v.offs[i0 + uint32_t(k)] : 0u;
+  for (int k = 0; k <= kR; ++k)
+    obv[k] = (kX & 1) ? o0 + (i0 + uint32_t(k)) * size : k <= int(nr) ? v.offs[i0 + uint32_t(k)] : 0u;
   // ---- requested together: the offsets, each row's small columns (lane c: column c) and first
   // large column's chunks (wave_copy's realigning layout), from the predicted addresses
   const uint64_t data_l = cl >= 0 ? reinterpret_cast<uint64_t>(a.cols[cl].data) : 0;
@@ -1087,11 +1093,13 @@ __global__ __launch_bounds__(64 * kW, kOcc > 0 ? kOcc : 1) void rowwave_decode_k
 // copy (one 4 KiB row per wave), which outruns the 256 KiB-per-workgroup loop above on MI355X.
 // kXcd: workgroups dealt to the 8 XCDs in contiguous ranges (xcd_block), the tile order of the
 // register decode (config B) -- the line two neighbouring workgroups share meets in one L2.
-template <int kU, bool kNTLoad, bool kNTStore, bool kXcd = false>
-__global__ __launch_bounds__(kBlock) void copy_wave_kernel(const uint4* __restrict__ src,
-                                                           uint4* __restrict__ dst, uint64_t n) {
+// kWaves: waves per workgroup.
+template <int kU, bool kNTLoad, bool kNTStore, bool kXcd = false, int kWaves = kBlock / 64>
+__global__ __launch_bounds__(64 * kWaves) void copy_wave_kernel(const uint4* __restrict__ src,
+                                                                uint4* __restrict__ dst,
+                                                                uint64_t n) {
   const uint32_t blk = kXcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-  const uint64_t w = uint64_t(blk) * (kBlock / 64) + (threadIdx.x >> 6);
+  const uint64_t w = uint64_t(blk) * kWaves + (threadIdx.x >> 6);
   const uint64_t b0 = w * (64 * kU) + (threadIdx.x & 63);
   uint4 v[kU];
 #pragma unroll
@@ -1486,6 +1494,23 @@ static int launch_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s,
                        pad, s, a);                                                             \
     return hip_check(hipGetLastError(), "rowwave_decode_kernel launch");                       \
   }
+    if (plan->rowwave_x) {  // measurement variants
+#define MDSX_ROWWAVE_X(X)                                                                       \
+  if (occ == 6 && plan->rowwave_x == X) {                                                      \
+    mdsx::set_last_kernel("rowwave_decode_kernel<true, 1, 1, 6, " #X ">");                     \
+    hipLaunchKernelGGL((rowwave_decode_kernel<true, 1, 1, 6, X>),                               \
+                       dim3(unsigned(uint64_t(a.ntiles) * uint64_t(a.tile_rows))), dim3(64), pad, \
+                       s, a);                                                                  \
+    return hip_check(hipGetLastError(), "rowwave_decode_kernel launch");                       \
+  }
+      MDSX_ROWWAVE_X(1)
+      MDSX_ROWWAVE_X(2)
+      MDSX_ROWWAVE_X(3)
+      MDSX_ROWWAVE_X(4)
+      MDSX_ROWWAVE_X(7)
+#undef MDSX_ROWWAVE_X
+      return mdsx::fail(MDSX_E_ARG, "mdsx: rowwave measurement variants: rw=1, rwocc=6 only");
+    }
     MDSX_ROWWAVE_OCC(6)
     MDSX_ROWWAVE_OCC(7)
     MDSX_ROWWAVE_OCC(8)
@@ -1864,8 +1889,20 @@ int mdsx_copy_probe_variant(const void* d_src, void* d_dst, uint64_t bytes, int 
                          dim3(kBlock), size_t(pad), s, src, dst, n);
       break;
     }
+    case 9:
+    case 10: {
+      // one wave per workgroup, XCD-contiguous (the row-per-wave decode's shape); 10: unused LDS
+      // so that 12 workgroups share a CU (a pure copy's best occupancy on MI355X,
+      // scripts/microbench/ring_copy4.hip)
+      const int pad = variant == 10 ? 13 * 1024 : 0;
+      const uint64_t per1 = 64 * 4;
+      hipLaunchKernelGGL((copy_wave_kernel<4, true, true, true, 1>),
+                         dim3(unsigned((n + per1 - 1) / per1)), dim3(64), size_t(pad), s, src, dst,
+                         n);
+      break;
+    }
     default:
-      return mdsx::fail(MDSX_E_ARG, "mdsx_copy_probe_variant: variant 0..8");
+      return mdsx::fail(MDSX_E_ARG, "mdsx_copy_probe_variant: variant 0..10");
   }
   return hip_check(hipGetLastError(), "copy probe launch");
 }

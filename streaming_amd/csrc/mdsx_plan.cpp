@@ -232,6 +232,10 @@ void apply_tuning(mdsx_plan* p) {
       p->seg_waves = int(v);
     } else if (key == "rw" && (v == 0 || v == 1 || v == 2 || v == 4)) {
       p->rowwave = int(v);
+    } else if (key == "rwx" && v >= 0 && v <= 7) {
+      p->rowwave_x = int(v);
+    } else if (key == "rwk" && v >= 0 && v <= 65536) {
+      p->rowwave_k = int(v);
     } else if (key == "snt" && v >= -1 && v <= 1) {
       p->scan_nt = int(v);
     } else if (key == "rwocc" && (v == 0 || v == 6 || v == 7 || v == 8)) {
