@@ -1488,6 +1488,10 @@ static int launch_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s,
     MDSX_ROWWAVE(true, 2, 2)
 #define MDSX_ROWWAVE_OCC(OCC)                                                                   \
   if (occ == OCC) {                                                                            \
+    if (pad > 64 * 1024 &&                                                                     \
+        hipFuncSetAttribute(reinterpret_cast<const void*>(rowwave_decode_kernel<true, 1, 1, OCC>), \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, int(pad)) != hipSuccess) \
+      return mdsx::fail(MDSX_E_HIP, "mdsx: rowwave_decode_kernel LDS attribute");             \
     mdsx::set_last_kernel("rowwave_decode_kernel<true, 1, 1, " #OCC ">");                      \
     const uint64_t waves = uint64_t(a.ntiles) * uint64_t(a.tile_rows);                         \
     hipLaunchKernelGGL((rowwave_decode_kernel<true, 1, 1, OCC>), dim3(unsigned(waves)), dim3(64), \
@@ -1497,6 +1501,10 @@ static int launch_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s,
     if (plan->rowwave_x) {  // measurement variants
 #define MDSX_ROWWAVE_X(X)                                                                       \
   if (occ == 6 && plan->rowwave_x == X) {                                                      \
+    if (pad > 64 * 1024 &&                                                                     \
+        hipFuncSetAttribute(reinterpret_cast<const void*>(rowwave_decode_kernel<true, 1, 1, 6, X>), \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, int(pad)) != hipSuccess) \
+      return mdsx::fail(MDSX_E_HIP, "mdsx: rowwave_decode_kernel LDS attribute");             \
     mdsx::set_last_kernel("rowwave_decode_kernel<true, 1, 1, 6, " #X ">");                     \
     hipLaunchKernelGGL((rowwave_decode_kernel<true, 1, 1, 6, X>),                               \
                        dim3(unsigned(uint64_t(a.ntiles) * uint64_t(a.tile_rows))), dim3(64), pad, \

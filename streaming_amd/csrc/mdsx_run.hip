@@ -354,7 +354,9 @@ __global__ __launch_bounds__(64 * W, 4) void seg_decode_kernel(const DevArgs a) 
       // other column, no str check (with bit 16: no per-run outputs either)
       const int c0 = 0;
       const uint32_t len0 = uint32_t(__builtin_amdgcn_readfirstlane(int(ring_u32<S>(ring, sp))));
-      const uint32_t l = ((wide_mask & 1ull) && hv + len0 <= size) ? len0 : 0u;  // else nothing
+      // (column 0 must be a ragged column whose head comes first, and writable; else nothing)
+      const bool col0 = __builtin_amdgcn_readfirstlane(vi) == 0 && (wide_mask & 1ull);
+      const uint32_t l = (col0 && hv + len0 <= size) ? len0 : 0u;
       const uint32_t d = uint32_t(__builtin_amdgcn_readlane(int(cur), c0));
       uint4 cy = (d & 15u) ? readlane4(carry, c0) : make_uint4(0, 0, 0, 0);
       if (vi == 0 && lane == 0) obuf[j] = d;
