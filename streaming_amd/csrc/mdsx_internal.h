@@ -58,7 +58,7 @@ struct mdsx_plan {
                            // (profiles/r03/xcd_order/): 1 the lean path (+3 % on config C), 2 the
                            // register decode (+1.1 % on config B); not 4, the row-parallel (-1 %)
   int rowwave = -1;        // all-fixed plans: one row per wave, this many waves per workgroup (0:
-                           // decode_kernel; -1: 1 for rows of >= 2 KiB, else 0; MDSX_TUNE rw)
+                           // decode_kernel; -1: 1 for rows of >= 3 KiB, else 0; MDSX_TUNE rw)
   int rowwave_occ = 6;     // ... registers bounded for this many waves per SIMD (MDSX_TUNE rwocc;
                            // 0: the compiler's choice, 85 VGPRs = 5 waves)
   int rowwave_rows = 1;    // ... rows per wave (MDSX_TUNE rwr: 1, 2, 4)

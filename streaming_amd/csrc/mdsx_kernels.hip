@@ -1447,14 +1447,15 @@ static int launch_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s,
   const size_t lds =
       size_t(a.tile_rows) * (12 * size_t(plan->nvar) + 4 * size_t(plan->ncols) + 1) + 16;
   const size_t dlds = lds + size_t(plan->lds_pad_kb) * 1024;  // (+ unused pad: occupancy)
-  // All-fixed plans of rows >= 2 KiB: one row per wave (rowwave_decode_kernel), its copy issued
+  // All-fixed plans of rows >= 3 KiB: one row per wave (rowwave_decode_kernel), its copy issued
   // before the row's offsets are known, registers bounded for 6 waves per SIMD -- config B, in
   // one process on each of three boxes: 6.22-6.23 / 6.66 vs 5.96 / 6.51 TB/s for decode_kernel
-  // (5 waves per SIMD: 6.15 / 6.43; profiles/r05/rowwave/); shorter rows keep decode_kernel's
-  // row per lane.
+  // (5 waves per SIMD: 6.15 / 6.43; profiles/r05/rowwave/). By row size (fixed_rows.json):
+  // ahead from 3 KiB rows (+2 % at 3 KiB, +7 % at 8 KiB), behind below (-5 % at 2.5 KiB, -12 %
+  // at 2 KiB, -63 % at 256 B: decode_kernel's row per lane and four rows per workgroup win).
   uint64_t row_size = 0;
   for (int c = 0; c < plan->ncols; ++c) row_size += plan->cols[c].row_bytes;
-  const int rw = plan->rowwave >= 0 ? plan->rowwave : (row_size >= 2048 ? 1 : 0);
+  const int rw = plan->rowwave >= 0 ? plan->rowwave : (row_size >= 3072 ? 1 : 0);
   if (plan->nvar == 0 && rw > 0) {
     const size_t pad = size_t(plan->lds_pad_kb) * 1024;
     const int rr = plan->rowwave_rows;  // rows per wave

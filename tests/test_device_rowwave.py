@@ -17,7 +17,7 @@ from tests.test_device_decode import _device_digests
 pytestmark = pytest.mark.gpu
 
 MODES = {
-    'rw0': 'rw=0',  # decode_kernel (rows of >= 2 KiB take the row-per-wave kernel by default)
+    'rw0': 'rw=0',  # decode_kernel (rows of >= 3 KiB take the row-per-wave kernel by default)
     'rw1': 'rw=1',  # registers bounded for 6 waves per SIMD (the default)
     'rw1_occ0': 'rw=1,rwocc=0',  # ... the compiler's choice (5)
     'rw1_occ8': 'rw=1,rwocc=8',  # ... 8 (spills)
