@@ -121,6 +121,7 @@ def main():
     W = output_bytes(decs[args.variants[0]].plan, decs[args.variants[0]].result())
     copy_dst = torch.empty_like(base_batch.buffer)
     times = {v: [] for v in args.variants}
+    dtimes = {v: [] for v in args.variants}  # the decode launch alone (after the scan pass)
     times['torch_copy'] = []
     pe = os.environ.get('MDSX_PROBES', '')  # '1': shapes 0-4; or a list of shapes, '1,5,7,8'
     probes = [int(x) for x in pe.split(',')] if ',' in pe else [0, 1, 2, 3, 4] if pe else []
@@ -151,6 +152,7 @@ def main():
                 dec.run(e)
             torch.cuda.synchronize()
             times[v].extend(e[0].elapsed_time(e[2]) for e in evs)  # scan (if any) + decode
+            dtimes[v].extend(e[1].elapsed_time(e[2]) for e in evs)
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         for _ in range(args.iters):
@@ -218,6 +220,9 @@ def main():
         nbytes = 2 * base_batch.buffer.numel() if v in ('torch_copy', 'mdsx_copy_probe') or \
             v.startswith('probe') else R + W
         res[v] = {'median_ms': ms, 'min_ms': float(np.min(ts)), 'GBps': nbytes / ms / 1e6}
+        if dtimes.get(v):
+            dms = float(np.median(dtimes[v]))
+            res[v].update(decode_ms=dms, decode_GBps=nbytes / dms / 1e6)
     print(json.dumps({'config': args.config, 'blob': args.blob, 'chars': args.chars, 'R': R,
                       'W': W, 'rows': base_batch.total_rows, 'results': res,
                       'phase_cycles_per_tile': phases}, indent=1))

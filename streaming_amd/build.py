@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SOURCES = [
     os.path.join(HERE, 'csrc', name)
-    for name in ('mdsx_kernels.hip', 'mdsx_stage.hip', 'mdsx_run.hip', 'mdsx_rows.hip', 'mdsx_srows.hip',
+    for name in ('mdsx_kernels.hip', 'mdsx_stage.hip', 'mdsx_run.hip', 'mdsx_rows.hip', 'mdsx_swave.hip',
                  'mdsx_encode.hip', 'mdsx_hash.hip', 'mdsx_plan.cpp')
 ]
 HEADERS = [os.path.join(HERE, 'csrc', name)
@@ -79,14 +79,27 @@ def _compile_device(src: str, obj: str, verbose: bool) -> None:
     subprocess.run(cmd, check=True)
 
 
-def _check_cross_lane_reads(obj: str) -> None:
-    """Refuse a build whose row-parallel decode reads a register across lanes where the exec mask
-    may be partial (streaming_amd/isa_check.py)."""
+# Kernels whose cross-lane reads the ISA check covers, per source: the row-parallel decode, the
+# one-row-per-wave decode of all-fixed plans and the one-sample-per-wave decode of ragged plans
+# (each reads registers of a lane chosen at run time: v_readlane with an SGPR lane).
+ISA_CHECKED = {
+    'mdsx_rows.hip': ('rows_decode_kernel',),
+    'mdsx_kernels.hip': ('rowwave_decode_kernel',),
+    'mdsx_swave.hip': ('swave_decode_kernel',),
+}
+
+
+def _check_cross_lane_reads(obj: str, want: tuple = ('rows_decode_kernel',)) -> None:
+    """Refuse a build whose listed kernels read a register across lanes where the exec mask may
+    be partial (streaming_amd/isa_check.py)."""
     from streaming_amd import isa_check
     rocm = os.environ.get('ROCM_PATH', '/opt/rocm')
     text = subprocess.run([os.path.join(rocm, 'lib', 'llvm', 'bin', 'llvm-objdump'), '-d', obj],
                           capture_output=True, text=True, check=True).stdout
-    bad = isa_check.check(text)
+    bad = [hit for w in want for hit in isa_check.check(text, w)]
+    missing = [w for w in want if not any(w in name for name, _ in isa_check.kernels(text))]
+    if missing:
+        raise RuntimeError(f'mdsx build: no kernel named {missing} in {obj} for the ISA check')
     if bad:
         raise RuntimeError('mdsx build: cross-lane reads under a possibly partial exec mask in ' +
                            '; '.join(f'{name} (at {", ".join(hex(a) for a in addrs)})'
@@ -106,14 +119,16 @@ def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(objdir, exist_ok=True)
     objs = [os.path.join(objdir, os.path.basename(s) + '.o') for s in SOURCES]
     from concurrent.futures import ThreadPoolExecutor
-    rows_dev = os.path.join(objdir, 'mdsx_rows.device.o')
-    with ThreadPoolExecutor(max_workers=max(1, min(len(SOURCES) + 1, os.cpu_count() or 1))) as pool:
+    devs = {src: os.path.join(objdir, src.replace('.hip', '.device.o')) for src in ISA_CHECKED}
+    with ThreadPoolExecutor(max_workers=max(1, min(len(SOURCES) + len(devs),
+                                                   os.cpu_count() or 1))) as pool:
         jobs = [pool.submit(_compile, s, o, verbose) for s, o in zip(SOURCES, objs)]
-        jobs.append(pool.submit(_compile_device, os.path.join(HERE, 'csrc', 'mdsx_rows.hip'),
-                                rows_dev, verbose))
+        jobs += [pool.submit(_compile_device, os.path.join(HERE, 'csrc', src), obj, verbose)
+                 for src, obj in devs.items()]
         for f in jobs:
             f.result()
-    _check_cross_lane_reads(rows_dev)
+    for src, obj in devs.items():
+        _check_cross_lane_reads(obj, ISA_CHECKED[src])
     tmp = OUTPUT + '.tmp'
     cmd = [hipcc(), f'--offload-arch={ARCH}', '-shared', '-fPIC', '-o', tmp, *objs]
     if verbose:

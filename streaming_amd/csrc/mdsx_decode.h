@@ -83,10 +83,8 @@ struct DevArgs {
   uint32_t seg_small;    // lean path: bytes per row of the fixed columns of <= 16 bytes
   uint32_t xcd_order;    // kXcd* bits: decodes whose workgroups take XCD-contiguous tile ranges
   uint32_t rows_pipe;    // row-parallel decode: tiles per workgroup through two stages (0: one)
-  uint32_t srows_slots;  // streaming row-parallel decode: KiB of its per-wave ring (0: off)
   uint32_t rw_k;         // (measurement only, rowwave kX bit 2: offsets[0] taken as hdr_end + rw_k)
-  uint32_t* tile_list;   // [ntiles] tiles the streaming row-parallel decode leaves to the
-                         // row-parallel kernel (count at kSrowsCountOffset)
+  uint32_t swave;        // ragged plans of long samples: one sample per wave (mdsx_swave.hip)
   uint32_t gather_block0[MDSX_MAX_COLUMNS + 1];  // first gather workgroup of each ragged column
   DevCol cols[MDSX_MAX_COLUMNS];
 };
@@ -177,8 +175,6 @@ __device__ __forceinline__ int64_t block_exclusive_scan(int64_t x, int64_t* s_ws
 // Byte offset, inside the workspace's 256-byte status block, of the staged decode's count of
 // huge rows (listed in the src_abs region; mdsx_stage.hip).
 constexpr uint64_t kHugeCountOffset = 192;
-// ... and of the count of tiles the streaming row-parallel decode lists (a.tile_list).
-constexpr uint64_t kSrowsCountOffset = 196;
 // Bit (-code) set for every kind of error a decode kernel reported (the status record keeps only
 // the first): the gather pass runs when every error is a per-sample one (empty sample, range),
 // which leaves its row zero-length and every offset consistent.
@@ -280,11 +276,11 @@ __device__ __forceinline__ uint32_t draw_ticket(const DevArgs& a, uint32_t* s_ti
 int launch_stage_totals(const DevArgs& a, bool nt, hipStream_t s);
 int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s);
 int launch_rows_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s);
-// The streaming row-parallel decode (mdsx_srows.hip): every tile the scan pass marked (TileRun
-// bit 1), the others listed in a.tile_list for launch_rows_decode's list launch.
-int launch_srows_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s);
 // The samples listed (tile << 32 | row in tile, a.src_abs; count at kHugeCountOffset) as larger
 // than an LDS stage: one workgroup each, straight from HBM (mdsx_stage.hip).
 int launch_huge_rows(const DevArgs& a, bool nt, hipStream_t s);
+// One sample per one-wave workgroup, the sample in registers (mdsx_swave.hip), after the register
+// decode's scan pass (scan-block-local offsets in the offsets outputs, block bases in tile_prefix).
+int launch_swave_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s);
 
 }  // namespace mdsx_kernels

@@ -81,12 +81,12 @@ struct mdsx_plan {
                            // else 4)
   int rows_pipe = 0;       // row-parallel decode: tiles per workgroup, the next tile's DMA in
                            // flight while one is written (two stages; 0: one tile, one stage)
-  int srows = 0;           // row-parallel batches: the streaming row-parallel decode first
-                           // (mdsx_srows.hip; the row-parallel kernel takes the tiles it lists);
-                           // 1: the samples through a per-wave LDS ring, 2: read from L2
-  int srows_kb = 8;        // its per-wave ring in KiB (6, 8 or 12)
-  int srows_lim_kb = 0;    // its windows: at most this many KiB (0: ring - 2)
-  int srows_tile_kb = 40;  // its tiles: about this many KiB of samples (<= 256 rows)
+  int swave = 0;           // ragged batches of the streaming decode's sample sizes: one sample per
+                           // one-wave workgroup, in registers, instead (mdsx_swave.hip)
+  int swave_kb = 6;        // ... KiB of a sample held in registers (4, 6 or 8; larger samples are
+                           // copied straight from HBM)
+  int swave_occ = 0;       // ... waves per SIMD its registers are bounded for (0: the compiler's)
+  int swave_tile = 64;     // ... rows per tile (the scan pass's unit: 256 / this tiles per block)
   int gather_chunks = 2;  // 16-byte chunks per lane in the ragged gather (tile = 4 KiB x this)
   int gather_min = 256;   // ragged columns averaging fewer bytes per row use the gather kernel
   int group_max = 1024;   // ... fewer than this (and >= gather_min): four rows per wave
@@ -101,6 +101,11 @@ struct mdsx_plan {
 // decode leads, 2.85 vs 2.26).
 inline bool use_run_decode(const mdsx_plan* p, uint64_t bytes, uint64_t rows) {
   return p->nvar > 0 && p->run_slots > 0 && rows > 0 && bytes / rows >= uint64_t(p->run_min);
+}
+
+// Whether such a batch decodes one sample per wave instead (mdsx_swave.hip).
+inline bool use_swave_decode(const mdsx_plan* p, uint64_t bytes, uint64_t rows) {
+  return p->swave != 0 && use_run_decode(p, bytes, rows);
 }
 
 // Whether a ragged batch of shorter samples decodes through the row-parallel decode
@@ -128,12 +133,10 @@ inline uint64_t rows_auto_stage(uint64_t per_row, uint64_t tr, uint64_t slack = 
 // stage -- rows_kb, or by default 20 KiB for samples under 512 bytes (per-sample work dominates:
 // five workgroups per CU) and 40 KiB above (three workgroups of larger tiles; measured)
 // -- with the workgroup's LDS within the CU's 160 KiB.
-// target_kb > 0 (the streaming row-parallel decode's tiles): that many KiB of samples instead.
-inline int rows_tile_rows(const mdsx_plan* p, uint64_t per_row, int target_kb = 0) {
+inline int rows_tile_rows(const mdsx_plan* p, uint64_t per_row) {
   if (per_row == 0) per_row = 1;
-  const uint64_t target = target_kb > 0  ? uint64_t(target_kb) * 1024
-                          : p->rows_kb > 0 ? uint64_t(p->rows_kb) * 1024
-                                           : (per_row < 512 ? 20 : 40) * 1024ull;
+  const uint64_t target = p->rows_kb > 0 ? uint64_t(p->rows_kb) * 1024
+                                         : (per_row < 512 ? 20 : 40) * 1024ull;
   int tr = 1;
   while (tr < 256) {
     const uint64_t t2 = uint64_t(tr) * 2;

@@ -745,7 +745,7 @@ __global__ __launch_bounds__(kBlock) void gather_ragged_kernel(const DevArgs a) 
 
 // ---------------------------------------------------------------------------------------------
 struct Layout {
-  uint64_t tile_total, tile_prefix, chunk_sum, tile_run, src_abs, row_map, tile_list, map_len,
+  uint64_t tile_total, tile_prefix, chunk_sum, tile_run, src_abs, row_map, map_len,
       total;
 };
 
@@ -765,8 +765,7 @@ Layout workspace_layout(const mdsx_plan* plan, const mdsx_batch* b) {
   L.tile_run = L.chunk_sum + round256(nv * (b->ntiles / kScanChunk + 1) * 8);
   L.src_abs = L.tile_run + round256(nv ? uint64_t(b->ntiles) * sizeof(TileRun) : 0);
   L.row_map = L.src_abs + round256(nv * b->rows * 8);
-  L.tile_list = L.row_map + round256(nv * L.map_len * 4);
-  L.total = L.tile_list + round256(nv ? uint64_t(b->ntiles) * 4 : 0);
+  L.total = L.row_map + round256(nv * L.map_len * 4);
   return L;
 }
 
@@ -795,7 +794,6 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   a->tile_run = reinterpret_cast<TileRun*>(ws + L.tile_run);
   a->src_abs = reinterpret_cast<uint64_t*>(ws + L.src_abs);
   a->row_map = reinterpret_cast<uint32_t*>(ws + L.row_map);
-  a->tile_list = reinterpret_cast<uint32_t*>(ws + L.tile_list);
   a->lookback = reinterpret_cast<uint64_t*>(ws + L.tile_total);  // single pass: no tile totals
   a->ticket = reinterpret_cast<uint32_t*>(ws + kTicketOffset);
   a->map_len = L.map_len;
@@ -808,7 +806,9 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   a->stage_debug = uint32_t(plan->stage_debug);
   a->xcd_order = uint32_t(plan->xcd_order);
   a->rw_k = uint32_t(plan->rowwave_k);
-  a->run_slots = use_run_decode(plan, b->bytes, b->rows) ? uint32_t(plan->run_slots) : 0u;
+  a->swave = use_swave_decode(plan, b->bytes, b->rows) ? 1u : 0u;
+  a->run_slots = use_run_decode(plan, b->bytes, b->rows) && !a->swave ? uint32_t(plan->run_slots)
+                                                                      : 0u;
   if (a->run_slots && plan->seg) {
     // lean path: a sample must fit the ring with a slot to spare (seg_decode_kernel)
     a->seg_lim = a->run_slots * 1024u - 1024u - 32u;
@@ -824,18 +824,6 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   if (a->rows_bytes && rows_lds_bytes_est(plan, a->rows_bytes, uint64_t(tr)) > 160 * 1024)
     a->rows_bytes = 0;
   a->rows_pipe = a->rows_bytes ? uint32_t(plan->rows_pipe) : 0u;
-  // the streaming row-parallel decode: windows of at most (ring - 2) KiB; tiles with a larger
-  // sample (TileRun bit 1 clear, stage_totals_kernel) go to the row-parallel kernel
-  if (a->rows_bytes && plan->srows && !a->run_slots) {
-    a->srows_slots = uint32_t(plan->srows_kb);
-    if (plan->srows == 2)  // read from L2: windows of <= srows_lim_kb (default 16) KiB
-      a->seg_lim = uint32_t(plan->srows_lim_kb > 0 ? std::min(plan->srows_lim_kb, 32) : 16) * 1024u;
-    else
-      a->seg_lim = plan->srows_lim_kb > 0 && plan->srows_lim_kb + 2 <= plan->srows_kb
-                       ? uint32_t(plan->srows_lim_kb) * 1024u
-                       : a->srows_slots * 1024u - 2048u;
-    a->rows_pipe = 0;
-  }
   if (a->run_slots && tr > 32)
     return mdsx::fail(MDSX_E_ARG, "mdsx: streaming decode tiles hold at most 32 rows");
   // the staged and streaming decodes scan one total per tile; the register-copy decode one per
@@ -1437,6 +1425,10 @@ int mdsx_scan_shards(const mdsx_plan* plan, const mdsx_batch* batch, const mdsx_
 static int launch_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s, bool single,
                          const uint64_t* mode_bytes) {
   int rc = MDSX_OK;
+  if (a.swave) {  // one sample per wave: the register decode's scan pass, then the decode
+    if (single && (rc = scan_pass(plan, a, s)) != MDSX_OK) return rc;
+    return launch_swave_decode(plan, a, s);
+  }
   if (plan->nvar > 0 && (a.run_slots > 0 || a.rows_bytes > 0)) {
     // the streaming and row-parallel decodes have no single-pass form: their scan pass, then
     // the decode (a look-back across the ~1000 tiles in flight measured slower than the pass:

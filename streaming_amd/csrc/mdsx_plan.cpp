@@ -220,14 +220,6 @@ void apply_tuning(mdsx_plan* p) {
       p->rows_pipe = int(v);
     } else if (key == "rownt") {
       p->rows_nt = v ? 1 : 0;
-    } else if (key == "srows" && v >= 0 && v <= 2) {
-      p->srows = int(v);  // 1: through an LDS ring, 2: read from L2
-    } else if (key == "srkb" && (v == 6 || v == 8 || v == 12)) {
-      p->srows_kb = int(v);
-    } else if (key == "srlim" && v >= 0 && v <= 32) {
-      p->srows_lim_kb = int(v);
-    } else if (key == "srtile" && v >= 4 && v <= 96) {
-      p->srows_tile_kb = int(v);
     } else if (key == "swg" && (v == 1 || v == 2 || v == 4)) {
       p->seg_waves = int(v);
     } else if (key == "rw" && (v == 0 || v == 1 || v == 2 || v == 4)) {
@@ -251,6 +243,15 @@ void apply_tuning(mdsx_plan* p) {
     } else if (key == "xcd" || key == "xcdb" || key == "xcdr") {
       const int bit = key == "xcd" ? 1 : key == "xcdb" ? 2 : 4;  // kXcdSeg / Register / Rows
       p->xcd_order = v ? (p->xcd_order | bit) : (p->xcd_order & ~bit);
+    } else if (key == "swave") {
+      p->swave = v ? 1 : 0;
+    } else if (key == "swkb" && (v == 4 || v == 6 || v == 8)) {
+      p->swave_kb = int(v);
+    } else if (key == "swocc" && (v == 0 || v == 4 || v == 5 || v == 6)) {
+      p->swave_occ = int(v);
+    } else if (key == "swtile" && (v == 1 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32 ||
+                                   v == 64 || v == 128 || v == 256)) {
+      p->swave_tile = int(v);
     } else if (key == "rkb" && v >= 1 && v <= 4096) {
       p->run_kb = int(v);
     }
@@ -386,6 +387,7 @@ int mdsx_plan_tile_rows(const mdsx_plan* plan) { return plan ? plan->tile_rows :
 
 int mdsx_plan_tile_rows_for(const mdsx_plan* plan, uint64_t shard_bytes, uint64_t rows) {
   if (!plan) return MDSX_E_ARG;
+  if (use_swave_decode(plan, shard_bytes, rows)) return plan->swave_tile;
   if (use_run_decode(plan, shard_bytes, rows)) {
     // streaming decode: about run_kb KiB of samples per tile (one wave's run), 1..32 rows
     const uint64_t per_row = std::max<uint64_t>(1, shard_bytes / rows);
@@ -394,7 +396,7 @@ int mdsx_plan_tile_rows_for(const mdsx_plan* plan, uint64_t shard_bytes, uint64_
     return tr;
   }
   if (use_rows_decode(plan, shard_bytes, rows))
-    return rows_tile_rows(plan, shard_bytes / rows, plan->srows ? plan->srows_tile_kb : 0);
+    return rows_tile_rows(plan, shard_bytes / rows);
   return plan->tile_rows;
 }
 

@@ -143,10 +143,8 @@ struct RowsTab {
 // workgroups fit a CU where their LDS does).
 // kFlat: the write loop over all columns' chunks at once (else one loop per column; measurement
 // control, MDSX_TUNE sdbg bit 256).
-// kList: the workgroups take the tiles the streaming row-parallel decode listed (a.tile_list,
-// mdsx_srows.hip), each in turn, instead of one tile per workgroup.
 template <bool kNT, bool kPipe, bool kProf = false, bool kFence = false, int kOcc = 4,
-          bool kFlat = true, bool kList = false>
+          bool kFlat = true>
 __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const DevArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   __shared__ int64_t s_wsum[kRowsBlock / 64];
@@ -197,13 +195,8 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
   }
 
   uint32_t count = kPipe ? last - first : 1u;  // (1: the loop folds away)
-  if constexpr (kList) {
-    const uint32_t listed = *reinterpret_cast<const uint32_t*>(
-        reinterpret_cast<const uint8_t*>(a.status) + kSrowsCountOffset);
-    count = blockIdx.x < listed ? (listed - blockIdx.x + gridDim.x - 1) / gridDim.x : 0u;
-  }
   for (uint32_t it = 0; it < count; ++it) {  // block-uniform
-  const uint32_t tile = kList ? a.tile_list[blockIdx.x + it * gridDim.x] : first + it;
+  const uint32_t tile = first + it;
   const uint32_t sbuf = kPipe ? it & 1u : 0u;
   const lds_u8* stage = (const lds_u8*)(smem + kStageFront + sbuf * stage_stride);
   const uint32_t stage_lds = lds0 + sbuf * stage_stride;
@@ -248,7 +241,7 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
   } else {
     const TileView v = tile_view(a, tile);
     if (!v.table_ok) {  // block-uniform; reported by the scan pass
-      if constexpr (!kPipe && !kList) return;
+      if constexpr (!kPipe) return;
       pre = false;  // (nothing was prefetched for the next tile either)
       continue;
     }
@@ -623,7 +616,7 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
     if constexpr (prof) prof_mark(a, tile, 6, ts);
     ga = gb;
   }
-  if constexpr (kPipe || kList) rows_barrier<kFence>();  // this tile's readers of the tables and its stage are done
+  if constexpr (kPipe) rows_barrier<kFence>();  // this tile's readers of the tables and its stage are done
   }  // tile
 }
 
@@ -631,12 +624,9 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
 
 uint32_t rows_tile_rows_limit() { return kRowsBlock; }
 
-static int launch_rows_listed(const mdsx_plan* plan, const DevArgs& a, hipStream_t s);
-
 int launch_rows_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
   if (a.tile_rows > kRowsBlock)
     return mdsx::fail(MDSX_E_ARG, "mdsx: row-parallel decode tiles hold at most 256 rows");
-  if (a.srows_slots) return launch_rows_listed(plan, a, s);
   // the huge-row list (samples larger than the stage) starts empty
   int rc = hip_check(hipMemsetAsync(reinterpret_cast<uint8_t*>(a.status) + kHugeCountOffset, 0,
                                     4, s),
@@ -727,40 +717,6 @@ int launch_rows_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
 #undef MDSX_ROWS_CASE
   rc = hip_check(hipGetLastError(), "rows_decode_kernel launch");
   if (rc != MDSX_OK) return rc;
-  return launch_huge_rows(a, nt, s);
-}
-
-// The streaming row-parallel decode, then this kernel over the tiles it listed (a few workgroups
-// taking them in turn; usually none), then the huge rows.
-static int launch_rows_listed(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
-  int rc = hip_check(hipMemsetAsync(reinterpret_cast<uint8_t*>(a.status) + kHugeCountOffset, 0,
-                                    8, s),  // the huge-row and listed-tile counts
-                     "hipMemsetAsync");
-  if (rc != MDSX_OK) return rc;
-  rc = launch_srows_decode(plan, a, s);
-  if (rc != MDSX_OK) return rc;
-  const std::string name = mdsx::last_kernel_name();
-  const size_t lds = rows_lds_bytes(a.rows_bytes, a.tile_rows, a.ncols, a.nvar, 1);
-  if (lds > 160 * 1024)
-    return mdsx::fail(MDSX_E_ARG, "mdsx: row-parallel decode stage and tables exceed 160 KiB of LDS");
-  const bool nt = plan->rows_nt != 0;
-  const unsigned grid = std::min<unsigned>(a.ntiles, 512);
-  const void* fn = nt ? reinterpret_cast<const void*>(rows_decode_kernel<true, false, false, false, 4, true, true>)
-                      : reinterpret_cast<const void*>(rows_decode_kernel<false, false, false, false, 4, true, true>);
-  if (lds > 64 * 1024) {
-    rc = hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)),
-                   "hipFuncSetAttribute");
-    if (rc != MDSX_OK) return rc;
-  }
-  if (nt)
-    hipLaunchKernelGGL((rows_decode_kernel<true, false, false, false, 4, true, true>), dim3(grid),
-                       dim3(kRowsBlock), lds, s, a);
-  else
-    hipLaunchKernelGGL((rows_decode_kernel<false, false, false, false, 4, true, true>), dim3(grid),
-                       dim3(kRowsBlock), lds, s, a);
-  rc = hip_check(hipGetLastError(), "rows_decode_kernel launch");
-  if (rc != MDSX_OK) return rc;
-  mdsx::set_last_kernel(name);  // the decode the batch's bytes go through
   return launch_huge_rows(a, nt, s);
 }
 

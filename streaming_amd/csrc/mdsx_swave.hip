@@ -1,0 +1,315 @@
+// Ragged plans of long samples, one sample per one-wave workgroup, the sample in registers
+// (gfx950): swave_decode_kernel.
+//
+// The reference decodes one sample per call: MDSReader.get_sample_data reads the sample's byte
+// range (streaming/base/format/mds/reader.py:128-149), decode_sample splits it at the u32 size
+// heads of the variable columns (mds/reader.py:103-126) and each column's decoder returns its
+// value (encodings.py:62-81: bytes / str; 84-94: int; 270-397: ndarray and scalars).
+//
+// Here a wave takes one sample -- the same unit -- with nothing staged ahead of it:
+//   * pass 1 is the register decode's scan (scan_tiles_kernel + the chunk scans): each row's
+//     ragged bytes, scanned into scan-block-local offsets (left in the offsets outputs) and
+//     scan-block bases (tile_prefix). So every wave knows where its sample's ragged values go
+//     before it has read a byte of the sample;
+//   * the wave requests, together: its offsets pair (mds/reader.py:137-142), the output positions
+//     of its ragged columns, then its size heads (lane v: head v) and the whole sample as aligned
+//     16-byte chunks held in registers (lane k: chunk k of every 1 KiB step; up to U KiB);
+//   * lane-parallel geometry: lane c takes column c's length (its head, or the fixed size), a
+//     wave prefix sum places it in the sample, one ballot checks the boundaries
+//     (mds/reader.py:111-125);
+//   * each wide column (ragged, or fixed > 16 B) is written destination-major: lane k owns 16-byte
+//     output chunk k. The first wide column sits right behind the heads (and any fixed columns
+//     before it), so its chunks are the loaded chunks shifted by at most one lane (DPP
+//     wave_shl / wave_shr) and realigned with the neighbour lane's chunk (v_alignbyte funnel): no
+//     LDS. Columns further in (config C's `n` and `s`), and fixed columns of <= 16 B, are read
+//     from a copy of just their chunks in the wave's LDS (one unaligned ds_read_b128 per output
+//     chunk);
+//   * str values are checked for strict UTF-8 (bytes.decode('utf-8'), encodings.py:80-81) on the
+//     same registers; the partial 16-byte chunks at a value's two ends are stored one byte per
+//     lane (their other bytes are the neighbouring samples' values).
+// Samples larger than U KiB are listed for stage_huge_kernel (mdsx_stage.hip), which copies each
+// column straight from HBM in a second launch. A sample failing the
+// file checks is reported (MDSX_E_BOUNDS / MDSX_E_EMPTY) and leaves zero-length ragged values and
+// its fixed rows unwritten, the register decode's rule (the scan pass counted it zero).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+
+#include "mdsx_decode.h"
+#include "mdsx_device.h"
+#include "mdsx_internal.h"
+#include "mdsx_ring.h"
+
+namespace mdsx_kernels {
+namespace {
+
+constexpr uint32_t kSwPad = 16;  // LDS bytes before the wave's chunk copy (reads from S >= -15)
+constexpr int kDppWaveShr1 = 0x138;  // lane i <- lane i - 1 across the wave (lane 0: 0)
+
+__device__ __forceinline__ uint4 lds16(const lds_u8* p) {
+  const u32x4 v = *(const MDSX_L u32x4*)p;  // any byte address (gfx950 reads LDS unaligned)
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// Lane k: loaded chunk q + 64 G + k (q in {-1, 0, 1}, wave-uniform; chunks outside: zeros). G
+// is a constant once the caller's loop is unrolled.
+template <int U>
+__device__ __forceinline__ uint4 near_chunk(const uint4 (&L)[U], int G, int q, int lane) {
+  if (q == 0) return L[G];
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  if (q > 0) {
+    uint4 x = dpp_mov4<kDppWaveShl1>(L[G]);
+    const uint4 n = G + 1 < U ? readlane0(L[G + 1 < U ? G + 1 : G]) : z;
+    if (lane == 63) x = n;
+    return x;
+  }
+  uint4 x = dpp_mov4<kDppWaveShr1>(L[G]);
+  const uint4 p = G > 0 ? readlane4(L[G > 0 ? G - 1 : 0], 63) : z;
+  if (lane == 0) x = p;
+  return x;
+}
+
+// One wide column of the sample: output bytes [d0, d0 + len) from stream byte S + h of the
+// loaded chunks (S = the stream byte of output chunk 0's byte 0, h = d0 & 15; S >= -15). near:
+// S in [-16, 32) -- chunks from the registers; else from the wave's LDS copy (buf: stream byte 0).
+// Returns (utf8) whether the value is not well-formed UTF-8 (wave-uniform).
+template <bool kNT, int U>
+__device__ __forceinline__ bool sw_copy(const uint4 (&L)[U], const lds_u8* buf, uint64_t d0,
+                                        uint32_t len, int32_t S, bool near, bool utf8, int lane) {
+  const uint64_t dend = d0 + len;
+  const uint64_t dbeg = d0 & ~uint64_t(15);
+  const uint32_t nch = uint32_t((((dend + 15) & ~uint64_t(15)) - dbeg) >> 4);
+  const int q = S >> 4;  // arithmetic: -1 for S in [-16, 0)
+  const uint32_t sh = uint32_t(S) & 15u;
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  bool bad = false;
+  uint32_t prev_w = 0;
+#pragma unroll
+  for (int g = 0; g < U; ++g) {
+    if (64u * uint32_t(g) >= nch) break;  // wave-uniform
+    const uint32_t k = 64u * uint32_t(g) + uint32_t(lane);
+    uint4 out;
+    if (near) {
+      const uint4 lo = near_chunk<U>(L, g, q, lane);
+      out = lo;
+      if (sh != 0) {
+        // the neighbour chunk: lane k + 1's, lane 63 the next step's lane 0
+        uint4 hi = dpp_mov4<kDppWaveShl1>(lo);
+        const uint4 n63 = q < 0 ? readlane4(L[g], 63)
+                                : (g + 1 < U ? readlane4(L[g + 1 < U ? g + 1 : g], q) : z);
+        if (lane == 63) hi = n63;
+        out = funnel16(lo, hi, sh);
+      }
+    } else {
+      out = k < nch ? lds16(buf + (S + int32_t(16u * k))) : z;
+    }
+    const uint64_t D = dbeg + 16ull * k;
+    if (k < nch && D >= d0 && D + 16 <= dend) st16<kNT>(D, out);
+    if (g == 0 && (dbeg < d0 || dbeg + 16 > dend)) wave_edge_store(out, 0, dbeg, d0, dend, lane);
+    if (nch > 1 && (dend & 15) != 0 && nch - 1 >= 64u * uint32_t(g) &&
+        nch - 1 < 64u * uint32_t(g) + 64u)
+      wave_edge_store(out, int(nch - 1 - 64u * uint32_t(g)), dbeg + 16ull * (nch - 1), d0, dend,
+                      lane);
+    if (utf8) {
+      const uint4 vout = keep_range(out, D, d0, dend);  // this value's bytes only
+      const uint32_t any8 = (vout.x | vout.y | vout.z | vout.w) & 0x80808080u;
+      if (__any(any8 != 0) || hi_c0(prev_w)) {  // a byte >= 0x80 (or a sequence open before)
+        uint32_t pw = uint32_t(__shfl_up(int(vout.w), 1));
+        if (lane == 0) pw = prev_w;
+        if (k < nch) bad |= utf8_chunk_bad(vout, pw, k == nch - 1);
+      }
+      prev_w = uint32_t(__builtin_amdgcn_readlane(int(vout.w), 63));
+    }
+  }
+  return utf8 ? __any(bad) != 0 : false;
+}
+
+// kOcc: registers bounded for that many waves per SIMD (0: the compiler's choice).
+template <bool kNT, int U, int kOcc>
+__global__ __launch_bounds__(64, kOcc > 0 ? kOcc : 1) void swave_decode_kernel(const DevArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const lds_u8* const buf = (const lds_u8*)smem + kSwPad;
+  const int lane = threadIdx.x;
+  // XCD-contiguous samples: the offsets line and the partial output chunks two neighbouring
+  // samples share meet in one L2
+  const uint32_t blk = (a.xcd_order & kXcdSeg) ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint32_t lg = uint32_t(__builtin_ctz(uint32_t(a.tile_rows)));
+  const uint32_t tile = blk >> lg, t = blk & uint32_t(a.tile_rows - 1);
+  if (tile >= a.ntiles) return;  // wave-uniform; no barrier in this kernel
+  const TileView v = tile_view(a, tile);
+  const bool first = t == 0 && tile == v.d.tile0;
+  if (!v.table_ok) {
+    if (first && lane == 0) report_decode(a, MDSX_E_HEADER, int(v.shard_idx), -1, -1);
+    return;
+  }
+  if (t >= v.nrows) return;
+  const uint32_t i = v.r0 + t;
+  const uint64_t row = v.d.row0 + i;
+  const int ncols = a.ncols, nvar = a.nvar;
+  const uint32_t hv = 4u * uint32_t(nvar);
+  // ---- requested first: the offsets pair and the ragged outputs' positions (lane c: column c;
+  // the scan pass left the scan-block-local offset in offsets[row])
+  const uint32_t b = __builtin_amdgcn_readfirstlane(v.offs[i]);
+  const uint32_t e = __builtin_amdgcn_readfirstlane(v.offs[i + 1]);
+  int vi = -1;
+  uint32_t rb = 0;
+  bool str = false;
+  uint64_t data = 0, cap = 0;
+  int64_t* offp = nullptr;
+  uint8_t* flp = nullptr;
+  for (int c = 0; c < ncols; ++c) {  // uniform
+    const DevCol& col = a.cols[c];
+    const int cv = col.var_index;
+    const uint32_t crb = col.row_bytes;
+    const bool cs = col.kind == MDSX_KIND_STR && col.flags != nullptr;
+    const uint64_t cdata = reinterpret_cast<uint64_t>(col.data);
+    int64_t* const coffs = col.offsets;
+    uint8_t* const cflags = col.flags;
+    const uint64_t ccap = col.capacity;
+    if (lane == c) {
+      vi = cv, rb = crb, str = cs, data = cdata, offp = coffs,
+      flp = cflags, cap = ccap;
+    }
+  }
+  int64_t off = 0;
+  if (vi >= 0) off = a.tile_prefix[uint64_t(vi) * a.nscan + tile / a.scan_per] + offp[row];
+  // ---- the sample (mds/reader.py:137-148): its heads, then all of its bytes
+  int rc = !(v.hdr_end <= b && b <= e && e <= v.d.bytes) ? MDSX_E_BOUNDS
+           : b == e                                       ? MDSX_E_EMPTY
+           : e - b < hv                                   ? MDSX_E_BOUNDS
+                                                          : MDSX_OK;
+  const uint32_t size = rc == MDSX_OK ? e - b : 0u;
+  const uint64_t s0 = reinterpret_cast<uint64_t>(v.shard) + b;
+  const uint32_t sa = uint32_t(s0 & 15);
+  const uint4* const sal = reinterpret_cast<const uint4*>(s0 - sa);
+  const uint32_t nload = (sa + size + 15u) >> 4;
+  const bool inreg = rc == MDSX_OK && nload <= 64u * U;  // wave-uniform
+  uint32_t hd = 0;
+  if (rc == MDSX_OK && lane < nvar)
+    hd = load_u32_any(reinterpret_cast<const uint8_t*>(s0) + 4u * uint32_t(lane));
+  uint4 L[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t k = 64u * uint32_t(u) + uint32_t(lane);
+    L[u] = inreg && k < nload ? ld16<kNT>(sal + k) : make_uint4(0, 0, 0, 0);
+  }
+  // ---- geometry (mds/reader.py:111-125): lane c's length, its place by a wave prefix sum
+  const uint32_t hl = uint32_t(__shfl(int(hd), vi > 0 ? vi : 0));
+  const uint32_t len = lane < ncols ? (vi >= 0 ? hl : rb) : 0u;
+  const bool over = lane < ncols && len > size;
+  const uint32_t lc = over ? 0u : len;
+  const uint32_t incl = wave_incl_u32(lc, lane, ncols);
+  const uint32_t total = uint32_t(__builtin_amdgcn_readlane(int(incl), ncols - 1));
+  if (rc == MDSX_OK && (__any(over) || total > size - hv)) rc = MDSX_E_BOUNDS;
+  if (rc != MDSX_OK && lane == 0) report_decode(a, rc, int(v.shard_idx), int(i), -1);
+  const bool ok = rc == MDSX_OK;  // wave-uniform
+  const uint32_t rel = hv + incl - lc;  // the column's first byte inside the sample
+  bool skip = false;
+  if (ok && vi >= 0 && uint64_t(off) + len > cap) {
+    report_decode(a, MDSX_E_CAPACITY, int(v.shard_idx), int(i), lane);
+    skip = true;  // the sample writes nothing of the column
+  }
+  const bool is_small = lane < ncols && vi < 0 && rb <= uint32_t(kSmallMax);
+  const uint64_t D = vi >= 0 ? data + uint64_t(off) : data + row * rb;
+  const bool small = ok && is_small;
+  const bool wide = ok && lane < ncols && !is_small && !skip && len > 0;
+  const uint64_t wide_mask = __ballot(wide);
+  uint64_t badm = 0;  // bit c: column c's str value is not well-formed UTF-8
+  if (ok && inreg) {
+    // output chunk 0 of the column starts at stream byte S (relative to the aligned sample start)
+    const int32_t S = int32_t(sa + rel) - int32_t(D & 15);
+    const bool near = S >= -16 && S < 32;
+    const bool via_lds = small || (wide && !near);
+    if (__ballot(via_lds)) {
+      // the chunks those columns' bytes lie in, copied to the wave's LDS
+      const uint32_t lo = via_lds ? (sa + rel) >> 4 : 0xffffffffu;
+      const uint32_t hi = via_lds ? (sa + rel + (small ? rb : len) + 15u) >> 4 : 0u;
+      uint32_t jlo = lo, jhi = hi;
+      for (int o = 32; o > 0; o >>= 1) {
+        jlo = min(jlo, uint32_t(__shfl_xor(int(jlo), o)));
+        jhi = max(jhi, uint32_t(__shfl_xor(int(jhi), o)));
+      }
+      jlo = __builtin_amdgcn_readfirstlane(jlo);
+      jhi = __builtin_amdgcn_readfirstlane(jhi);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (64u * uint32_t(u) >= jhi || 64u * uint32_t(u) + 64u <= jlo) continue;  // uniform
+        const uint32_t k = 64u * uint32_t(u) + uint32_t(lane);
+        if (k >= jlo && k < jhi)
+          *(MDSX_L u32x4*)(smem + kSwPad + 16u * k) = u32x4{L[u].x, L[u].y, L[u].z, L[u].w};
+      }
+      if (small) small_store(reinterpret_cast<uint8_t*>(D), lds16(buf + (sa + rel)), rb);
+    }
+    const uint64_t str_mask = __ballot(str), near_mask = __ballot(near);
+    for (uint64_t m = wide_mask; m; m &= m - 1) {  // wave-uniform, in column order
+      const int c = __builtin_ctzll(m);
+      const bool bad = sw_copy<kNT, U>(L, buf, readlane64(D, c),
+                                       uint32_t(__builtin_amdgcn_readlane(int(len), c)),
+                                       __builtin_amdgcn_readlane(S, c), (near_mask >> c) & 1ull,
+                                       (str_mask >> c) & 1ull, lane);
+      if (bad) badm |= 1ull << c;
+    }
+  } else if (ok && lane == 0) {
+    // a sample past the register window: listed for stage_huge_kernel (every column straight
+    // from HBM, after this launch; it reads the final offsets written below)
+    uint32_t* count = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(a.status) +
+                                                  kHugeCountOffset);
+    a.src_abs[atomicAdd(count, 1u)] = (uint64_t(tile) << 32) | t;
+  }
+  // ---- the row's ragged offsets and str flags
+  if (vi >= 0) {
+    *gp(offp + row) = off;
+    if (flp) *gp(flp + row) = uint8_t((badm >> lane) & 1ull);
+  }
+  // the shard header (mds/writer.py:133-144): u32 N, then N + 1 offsets
+  if (first && lane == 0) {
+    const uint32_t n = *reinterpret_cast<const uint32_t*>(v.shard);
+    if (n != v.d.samples || v.offs[0] < v.hdr_end || v.offs[v.d.samples] > v.d.bytes)
+      report_decode(a, MDSX_E_HEADER, int(v.shard_idx), -1, -1);
+  }
+}
+
+}  // namespace
+
+int launch_swave_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
+  const uint64_t waves = uint64_t(a.ntiles) * uint64_t(a.tile_rows);
+  if (waves == 0) return MDSX_OK;
+  if (waves > 0xffffffffull) return mdsx::fail(MDSX_E_ARG, "mdsx: swave: too many samples");
+  // the list of samples past the register window starts empty
+  const int zc = hip_check(hipMemsetAsync(reinterpret_cast<uint8_t*>(a.status) + kHugeCountOffset,
+                                          0, 4, s),
+                           "hipMemsetAsync");
+  if (zc != MDSX_OK) return zc;
+  const int U = plan->swave_kb, occ = plan->swave_occ;
+  const bool nt = plan->run_nt != 0;
+  const size_t lds = size_t(U) * 1024 + 2 * kSwPad + size_t(plan->lds_pad_kb) * 1024;
+#define MDSX_SWAVE(NT, UU, OCC)                                                                  \
+  if (nt == NT && U == UU && occ == OCC) {                                                       \
+    const void* fn = reinterpret_cast<const void*>(swave_decode_kernel<NT, UU, OCC>);            \
+    if (lds > 64 * 1024 &&                                                                       \
+        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)) !=         \
+            hipSuccess)                                                                          \
+      return mdsx::fail(MDSX_E_HIP, "mdsx: swave_decode_kernel LDS attribute");                 \
+    mdsx::set_last_kernel("swave_decode_kernel<" #NT ", " #UU ", " #OCC ">");                    \
+    hipLaunchKernelGGL((swave_decode_kernel<NT, UU, OCC>), dim3(unsigned(waves)), dim3(64), lds, \
+                       s, a);                                                                    \
+    const int rc = hip_check(hipGetLastError(), "swave_decode_kernel launch");                   \
+    return rc != MDSX_OK ? rc : launch_huge_rows(a, NT, s);                                      \
+  }
+  MDSX_SWAVE(true, 6, 0)
+  MDSX_SWAVE(true, 6, 4)
+  MDSX_SWAVE(true, 6, 5)
+  MDSX_SWAVE(true, 6, 6)
+  MDSX_SWAVE(true, 4, 0)
+  MDSX_SWAVE(true, 4, 6)
+  MDSX_SWAVE(true, 8, 0)
+  MDSX_SWAVE(true, 8, 4)
+  MDSX_SWAVE(false, 6, 0)
+#undef MDSX_SWAVE
+  return mdsx::fail(MDSX_E_ARG,
+                    "mdsx: swave: (nt, KiB, occupancy) of (1, 6, 0/4/5/6), (1, 4, 0/6), (1, 8, 0/4), "
+                    "(0, 6, 0)");
+}
+
+}  // namespace mdsx_kernels

@@ -54,6 +54,15 @@ MODES = {
     'seg7_v1': 'run=7,seg=1,rmin=0,sv=1',
     'seg7_v3': 'run=7,seg=1,rmin=0,sv=3',
     'seg7_v7': 'run=7,seg=1,rmin=0,sv=7',
+    # one sample per one-wave workgroup, the sample in registers (mdsx_swave.hip), for every
+    # sample size: the default 6 KiB window (larger samples straight from HBM), 4 KiB, a 1-row
+    # tile, launch order, temporal loads / stores, registers bounded for 4 / 6 waves per SIMD
+    'swave': 'swave=1,rmin=0',
+    'swave4': 'swave=1,rmin=0,swkb=4,swtile=1',
+    'swave_xcd0': 'swave=1,rmin=0,xcd=0,swtile=256',
+    'swave_temporal': 'swave=1,rmin=0,rnt=0',
+    'swave_occ4': 'swave=1,rmin=0,swocc=4',
+    'swave_occ6': 'swave=1,rmin=0,swocc=6',
     'rows': 'rows=32,rmin=1000000000',  # the row-parallel decode (mdsx_rows.hip) for every size
     'rows_auto': 'rows=-1,rmin=1000000000',  # ... its tiles and stage sized per batch
     'rows_small': 'rows=2,rmin=1000000000',  # a 2 KiB stage: windows and HBM-direct samples
@@ -65,13 +74,7 @@ MODES = {
     'rows_pipe_one': 'rows=8,rpipe=1,rmin=1000000000',  # one tile per workgroup, two stages
     'rows_occ6': 'rows=-1,rocc=6,rmin=1000000000',  # registers bounded for six waves per SIMD
     'rows_occ8': 'rows=12,rocc=8,rmin=1000000000',  # ... eight, smaller tiles
-    # the streaming row-parallel decode (mdsx_srows.hip), the row-parallel kernel over the tiles
     # it lists; a 6 KiB ring (4 KiB windows) with small tiles and a 2 KiB fallback stage
-    'srows': 'rows=-1,srows=1,rmin=1000000000',
-    'srows_small': 'rows=2,srows=1,srkb=6,srtile=8,rmin=1000000000',
-    # ... its samples read from L2 (no ring); 2 KiB windows with a 2 KiB fallback stage
-    'srows_l2': 'rows=-1,srows=2,rmin=1000000000',
-    'srows_l2_small': 'rows=2,srows=2,srlim=2,srtile=8,rmin=1000000000',
     'gather': 'run=0,rows=0,gmin=1000000000',
     'group': 'run=0,rows=0,gmin=0,gmax=1000000000',
     'group_nt': 'run=0,rows=0,gmin=0,gmax=1000000000,strc=0',  # str rows streamed (non-temporal) too

@@ -32,10 +32,10 @@ MODES = {
     'seg7_edge': 'run=7,seg=1,rmin=0,rkb=12,sv=128',  # ... boundary lines, default policy
     'seg7_v3': 'run=7,seg=1,rmin=0,sv=3',  # ... early prologue and per-step release, 2-sample runs
     'seg_wg4': 'run=8,seg=1,rmin=0,swg=4',  # four waves per workgroup (the default is two)
+    'swave': 'swave=1,rmin=0',  # one sample per wave, in registers (larger ones from HBM)
+    'swave4': 'swave=1,rmin=0,swkb=4,swtile=2',
     'rows_small': 'rows=2,rmin=1000000000',  # row-parallel, 2 KiB stage (windows, huge rows)
     'rows_pipe': 'rows=4,rpipe=5,rmin=1000000000',  # ... two stages, next tile's DMA in flight
-    'srows': 'rows=-1,srows=1,srkb=6,rmin=1000000000',  # streaming row-parallel + listed tiles
-    'srows_l2': 'rows=-1,srows=2,srlim=3,rmin=1000000000',  # ... read from L2, 3 KiB windows
     'register': 'run=0,rows=0',  # the register decode (+ gather / groups per column)
     'rowwave': 'rw=1,lpad=12',  # all-fixed plans: one row per wave (others: as the default)
 }
@@ -44,8 +44,8 @@ SINGLE_MODES = {
     'single': '',  # streaming / row-parallel batches: scan pass + decode, no host round trip
     'single_rows_small': 'rows=2,rmin=1000000000',  # ... row-parallel in windows, huge rows
     'single_rows_pipe': 'rows=4,rpipe=5,rmin=1000000000',  # ... two stages per workgroup
-    'single_srows': 'rows=-1,srows=1,rmin=1000000000',  # ... the streaming row-parallel decode
     'single_register': 'run=0,rows=0',  # the register decode's single-pass form (look-back)
+    'single_swave': 'swave=1,rmin=0',  # scan pass + one sample per wave
 }
 
 

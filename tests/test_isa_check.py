@@ -154,3 +154,31 @@ def test_built_row_decode_passes():
                           text=True, check=True).stdout
     assert 'rows_decode_kernel' in text
     assert isa_check.check(text) == []
+
+
+def test_checked_kernels_by_name():
+    """The build checks the one-row-per-wave and one-sample-per-wave decodes too:
+    the same flow refuses their variable-lane reads under a partial exec mask."""
+    lines = ['v_cmp_gt_u32_e32 vcc, s36, v0', 's_and_saveexec_b64 s[2:3], vcc',
+             'v_readlane_b32 s1, v7, s2', 's_or_b64 exec, exec, s[2:3]',
+             'v_readlane_b32 s3, v7, s2', 's_endpgm']
+    for kernel in ('rowwave_decode_kernel', 'swave_decode_kernel'):
+        name = NAME.replace('rows_decode_kernel', kernel)
+        bad = isa_check.check(asm(lines, name=name), kernel)
+        assert [a for _, addrs in bad for a in addrs] == [0x1008], kernel
+
+
+def test_built_checked_kernels_pass():
+    from streaming_amd import build
+    import subprocess
+    for src, want in build.ISA_CHECKED.items():
+        obj = os.path.join(os.path.dirname(isa_check.__file__), 'build',
+                           src.replace('.hip', '.device.o'))
+        if not os.path.exists(obj):
+            import pytest
+            pytest.skip('library not built here')
+        text = subprocess.run(['/opt/rocm/lib/llvm/bin/llvm-objdump', '-d', obj],
+                              capture_output=True, text=True, check=True).stdout
+        for w in want:
+            assert w in text, (src, w)
+            assert isa_check.check(text, w) == [], (src, w)

@@ -108,9 +108,9 @@ def test_workspace_bytes():
     r = lambda x: (x + 255) // 256 * 256
     # status block, per-tile totals and prefixes, chunk sums of their scan, the streaming
     # decode's 48-byte run records, per-row addresses (also the staged decode's huge-row list),
-    # row map, the streaming row-parallel decode's tile list
+    # row map
     want = 256 + 2 * r(2 * 100 * 8) + r(2 * (100 // 4096 + 1) * 8) + r(100 * 48) + \
-        r(2 * 6400 * 8) + r(2 * ((1 << 20) // 4096 + 8) * 4) + r(100 * 4)
+        r(2 * 6400 * 8) + r(2 * ((1 << 20) // 4096 + 8) * 4)
     assert lib.mdsx_workspace_bytes(plan.handle, ctypes.byref(b)) == want
     fixed = Plan(['id', 'x'], ['int32', 'ndarray:float32:1024'], [4, 4096])
     assert lib.mdsx_workspace_bytes(fixed.handle, ctypes.byref(b)) == 256
@@ -141,6 +141,11 @@ def test_tile_rows_for_sizes_ragged_tiles_to_the_decode(monkeypatch):
     assert wide.tile_rows_for(1 << 26, 1 << 20) == 64  # 64 columns: the tables bound the tile
     monkeypatch.setenv('MDSX_TUNE', 'rows=18')
     assert Plan(['b'], ['bytes'], [None]).tile_rows_for(1 << 26, (1 << 26) // 100) == 128
+    monkeypatch.setenv('MDSX_TUNE', 'swave=1')  # one sample per wave: the scan pass's tiles
+    assert Plan(['b'], ['bytes'], [None]).tile_rows_for(1 << 26, 15_700) == 64
+    assert Plan(['b'], ['bytes'], [None]).tile_rows_for(1 << 26, (1 << 26) // 100) == 128
+    monkeypatch.setenv('MDSX_TUNE', 'swave=1,swtile=256')
+    assert Plan(['b'], ['bytes'], [None]).tile_rows_for(1 << 26, 15_700) == 256
     monkeypatch.setenv('MDSX_TUNE', 'run=4,rkb=256')
     assert Plan(['b'], ['bytes'], [None]).tile_rows_for(1 << 26, 15_700) == 32
     monkeypatch.setenv('MDSX_TUNE', 'run=0,rows=0')  # the register decode: the plan's tiles
