@@ -83,6 +83,11 @@ def parse_args(argv=None):
                     help='set up the process group even for one rank (nccl = RCCL on the GPU): '
                          'runs the barrier / max-over-ranks / gather collectives of the N > 1 '
                          'path on a one-GPU box')
+    ap.add_argument('--fresh-steps', type=int, default=6,
+                    help='ragged configs: also time this many steps over two distinct resident '
+                    'batches taken in turn, each with a decoder of its own (its sizing included: '
+                    'the totals read back and the outputs allocated; and the single-pass form, '
+                    'outputs at their upper bound); 0 disables')
     ap.add_argument('--dry-run', action='store_true',
                     help='no GPU: exercise the launcher, process group (gloo) and shard '
                     'ownership only (CPU test hook)')
@@ -478,6 +483,40 @@ def timed_block(args, leg, nsteps, world, dev):
     })
 
 
+def rank_record(rank, leg_rows, shards, shard_ids, elapsed_s, K, blocks, R, W, decode_ms):
+    """What one rank reports for the line's ``per_rank`` list: its step time, its decode kernel's
+    time and fraction of the HBM peak, its step fraction and its own same-run copy ceiling (so an
+    N-GPU line tells a slow rank from a slow box)."""
+    kern_ms = float(np.mean(decode_ms)) if len(decode_ms) else None
+    step_ms = (sum(b['step_ms_events'] * b['steps'] for b in blocks) / K) if blocks else None
+    copies = [b['copy_ceiling_GBps'] for b in blocks if b.get('copy_ceiling_GBps')]
+    achieved = (R + W) / kern_ms / 1e6 if kern_ms else None
+    copy = float(np.median(copies)) if copies else None
+    return {
+        'rank': rank, 'ms_per_step': elapsed_s / K * 1e3, 'rows': leg_rows, 'shards': shards,
+        'shard_ids': shard_ids,
+        'kernel_ms': kern_ms,
+        'frac': achieved / HBM_PEAK_GBS if achieved else None,
+        'step_frac': (R + W) / step_ms / 1e6 / HBM_PEAK_GBS if step_ms else None,
+        'copy_ceiling_GBps': copy,
+        'frac_of_same_run_copy': achieved / copy if achieved and copy else None,
+    }
+
+
+def aggregate_ranks(per_rank):
+    """min / median / max over the ranks of each per-rank figure, and the slowest rank."""
+    out = {}
+    for k in ('ms_per_step', 'kernel_ms', 'frac', 'step_frac', 'copy_ceiling_GBps',
+              'frac_of_same_run_copy'):
+        xs = [p[k] for p in per_rank if p.get(k) is not None]
+        if xs:
+            out[k] = {'min': float(np.min(xs)), 'median': float(np.median(xs)),
+                      'max': float(np.max(xs))}
+    out['slowest_rank'] = max(per_rank, key=lambda p: p['ms_per_step'])['rank']
+    out['ranks'] = len(per_rank)
+    return out
+
+
 def block_sizes(k, n=BLOCKS):
     """K steps split into at most n blocks (sizes differ by at most one)."""
     n = max(1, min(n, k))
@@ -495,9 +534,9 @@ def finish(args, leg, world, rank, tmpdir):
     K = sum(b['steps'] for b in leg.blocks)
     elapsed = sum(b['elapsed_s'] for b in leg.blocks)
     rows = batch.total_rows
-    per_rank = gather_objects(world, {
-        'rank': rank, 'ms_per_step': elapsed / K * 1e3, 'rows': rows, 'shards': len(leg.mine),
-        'shard_ids': f'{leg.mine[0]}..{leg.mine[-1]} step {world}' if leg.mine else ''})
+    per_rank = gather_objects(world, rank_record(
+        rank, rows, len(leg.mine), f'{leg.mine[0]}..{leg.mine[-1]} step {world}' if leg.mine else '',
+        elapsed, K, leg.blocks, leg.R, leg.W, leg.decode_ms))
     all_rows = sum(p['rows'] for p in per_rank)
     R, W = leg.R, leg.W
     kern_s = float(np.mean(leg.decode_ms)) / 1e3
@@ -538,6 +577,9 @@ def finish(args, leg, world, rank, tmpdir):
                      if leg.ahead else 'scan pass then decode, one stream'),
         },
         'per_rank': per_rank,
+        'per_rank_summary': aggregate_ranks(per_rank),
+        'fresh_batch_ms_per_step': leg.fresh['fresh_batch_ms_per_step'] if leg.fresh else None,
+        'fresh_batch': leg.fresh,
         'roofline': {
             'bound': 'hbm',
             'kernel': leg.kernel,
@@ -572,6 +614,57 @@ def finish(args, leg, world, rank, tmpdir):
     return result
 
 
+def fresh_batches(args, leg, world, dev):
+    """Steps over TWO distinct resident batches of the config taken in turn (this rank's shards and
+    as many other shards of the same workload, from their own seeds), each step with a decoder of
+    its own, as a loader handed a new batch every step runs it: the two-pass decode pays the
+    batch's sizing inside the step (scan pass, its totals read back to the host, the ragged outputs
+    allocated, then the decode), the single-pass one allocates its ragged outputs at their upper
+    bound and reads nothing back (``BatchDecoder(single=True)``). The headline's steps re-decode one
+    batch whose outputs were sized once. Returns the ``fresh_batch`` object."""
+    from streaming_amd.decoder import BatchDecoder, output_bytes
+    from streaming_amd.distributed import max_over_ranks
+    plan = leg.synth.plan
+    synth2, _ = build_workload(leg.config, [g + leg.total_shards for g in leg.mine])
+    pairs = [(leg.synth.batch, leg.synth.sources), (synth2.batch, synth2.sources)]
+    rw = []
+    for b, src in pairs:  # each batch decoded and checked once
+        d = BatchDecoder(plan, b)
+        out = d.run()
+        d.check()
+        verify(leg.config, out, src)
+        rw.append(b.shard_bytes + output_bytes(plan, out))
+        del d, out
+    res = {'steps': args.fresh_steps,
+           'batches': (f'2 distinct resident batches of {leg.synth.batch.nshards} shards, '
+                       f'taken in turn; a new decoder per step (outputs from torch\'s caching '
+                       f'allocator)'),
+           'algorithmic_bytes_per_step': float(np.mean(rw))}
+    for mode, single in (('two_pass', False), ('single_pass', True)):
+        for k in range(2):  # warm: the allocator's pool holds both batches' outputs
+            BatchDecoder(plan, pairs[k][0], single=single).run()
+        barrier(world)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for k in range(args.fresh_steps):
+            d = BatchDecoder(plan, pairs[k % 2][0], single=single)
+            out = d.run()
+        torch.cuda.synchronize(dev)
+        barrier(world)
+        elapsed = max_over_ranks(time.perf_counter() - t0, device=dev)
+        d.check()
+        if not args.no_verify:
+            verify(leg.config, out, pairs[(args.fresh_steps - 1) % 2][1])
+        del d, out
+        ms = elapsed / args.fresh_steps * 1e3
+        res[mode] = {'ms_per_step': ms, 'step_frac': float(np.mean(rw)) / ms / 1e6 / HBM_PEAK_GBS,
+                     'samples_per_s': leg.synth.batch.total_rows * world / (ms / 1e3)}
+    res['fresh_batch_ms_per_step'] = res['two_pass']['ms_per_step']
+    del synth2, pairs
+    torch.cuda.empty_cache()
+    return res
+
+
 def measure_all(args, configs, world, rank, dev, tmpdir):
     """Every config prepared, then BLOCKS timed blocks per config, interleaved (B1 C1 B2 C2 B3
     C3): each config's K steps are timed in blocks that fall on the same GPU phases."""
@@ -579,6 +672,9 @@ def measure_all(args, configs, world, rank, dev, tmpdir):
     for n in block_sizes(args.steps):
         for c in configs:
             timed_block(args, legs[c], n, world, dev)
+    for c in configs:  # after every timed block of every config
+        legs[c].fresh = fresh_batches(args, legs[c], world, dev) if (
+            args.fresh_steps > 0 and legs[c].synth.plan.num_var > 0 and not legs[c].ahead) else None
     return {c: finish(args, legs[c], world, rank, tmpdir) for c in configs}
 
 
@@ -588,9 +684,16 @@ def dry_run(args, world, rank):
     for config in ('B', 'C') if args.config == 'BC' else (args.config, ):
         mine, total = shard_plan(args, config, rank, world)
         lines[config] = gather_objects(world, {'rank': rank, 'shards': mine, 'total': total})
+    # the N-GPU line's per-rank report, from made-up timings (rank r: 1 + r/10 ms per step)
+    ms = 1.0 + rank / 10
+    blocks = [{'steps': 2, 'step_ms_events': ms, 'copy_ceiling_GBps': 6000.0 + rank}]
+    rec = rank_record(rank, 1000, len(mine), '', ms * 2e-3, 2, blocks, 4e9, 4e9, [ms * 0.9] * 2)
+    per_rank = gather_objects(world, rec)
     barrier(world)
     if rank == 0:
-        print(json.dumps({'dry_run': True, 'n_gpus': world, 'ownership': lines}), flush=True)
+        print(json.dumps({'dry_run': True, 'n_gpus': world, 'ownership': lines,
+                          'per_rank': per_rank, 'per_rank_summary': aggregate_ranks(per_rank)}),
+              flush=True)
     if _dist_on():
         torch.distributed.destroy_process_group()
 
@@ -629,6 +732,7 @@ def main(argv=None):
             'parity': 'bit-exact vs encoded source columns' if not args.no_verify else 'skipped',
             'config': head['config'],
             'per_rank': head['per_rank'],
+            'per_rank_summary': head['per_rank_summary'],
             'ms_per_step_blocks': head['ms_per_step_blocks'],
             'blocks': head['blocks'],
             'rewarm': head['rewarm'],

@@ -200,6 +200,20 @@ int mdsx_decode_shards_single(const mdsx_plan* plan, const mdsx_batch* batch,
                               void* d_workspace, uint64_t workspace_bytes, int64_t* d_totals,
                               void* stream);
 
+/* One sample, exactly as MDSReader.decode_sample slices it (mds/reader.py:103-126): the per-sample
+ * path for samples the whole-shard decodes report (a head larger than the sample, a sample shorter
+ * than its fixed columns), where the reference clips each column's slice instead of raising.
+ *   d_data   : device, the n bytes get_sample_data returned (mds/reader.py:128-149), with 64
+ *              readable bytes before and after them
+ *   d_values : device uint8[>= n]: every column's clipped slice, packed in column order
+ *   d_meta   : device int64[2 ncols + 1]: per column (offset in d_values, clipped length), then a
+ *              status: 0, or 1 + c when column c's u32 size head is cut short (the reference's
+ *              ValueError from np.frombuffer; the per-column entries are then not written)
+ * The caller applies each column's decoder to its slice (a short int / scalar / static ndarray
+ * raises there, as numpy does in the reference). */
+int mdsx_decode_sample(const mdsx_plan* plan, const uint8_t* d_data, uint32_t n, uint8_t* d_values,
+                       int64_t* d_meta, void* stream);
+
 /* ---- batch gather by sample id ---------------------------------------------
  * out[k] = column[idx[k]] over already-decoded columns: the device side of the reference's
  * per-sample iteration over a worker's sample ids (StreamingDataset.__iter__ ->

@@ -102,23 +102,33 @@ def load_index(dirname: str, split: Optional[str] = None) -> dict[str, Any]:
 
 
 class OracleMDSReader:
-    """Per-sample reader over one shard, same algorithm as the reference MDSReader."""
+    """Per-sample reader over one shard, same algorithm as the reference MDSReader.
 
-    def __init__(self, dirname: str, split: Optional[str], info: dict[str, Any]) -> None:
-        self.filename = os.path.join(dirname, split or '', info['raw_data']['basename'])
+    ``data``: the shard file's bytes, read from memory instead of the file (the same reads:
+    ``fp.read(n)`` from ``begin`` is ``data[begin:begin + n]``)."""
+
+    def __init__(self, dirname: str, split: Optional[str], info: dict[str, Any],
+                 data: Optional[bytes] = None) -> None:
+        self.filename = os.path.join(dirname or '', split or '', info['raw_data']['basename'])
         self.column_names = info['column_names']
         self.column_encodings = info['column_encodings']
         self.column_sizes = info['column_sizes']
         self.samples = info['samples']
+        self.data = data
 
     def get_sample_data(self, idx: int) -> bytes:
         offset = (1 + idx) * 4
-        with open(self.filename, 'rb', 0) as fp:
-            fp.seek(offset)
-            pair = fp.read(8)
-            begin, end = np.frombuffer(pair, np.uint32)
-            fp.seek(begin)
-            data = fp.read(end - begin)
+        if self.data is not None:
+            begin, end = np.frombuffer(self.data[offset:offset + 8], np.uint32)
+            n = int(end - begin)  # (numpy uint32: wraps where end < begin, as the reference's)
+            data = self.data[int(begin):int(begin) + n]
+        else:
+            with open(self.filename, 'rb', 0) as fp:
+                fp.seek(offset)
+                pair = fp.read(8)
+                begin, end = np.frombuffer(pair, np.uint32)
+                fp.seek(begin)
+                data = fp.read(end - begin)
         if not data:
             raise IndexError(f'Relative sample index {idx} is not present.')
         return data
@@ -212,13 +222,15 @@ def utf8_is_valid(data: bytes) -> bool:
         return False
 
 
-def decode_shard_columns(dirname: str, split: Optional[str], info: dict[str, Any]) -> dict[str, Any]:
+def decode_shard_columns(dirname: str, split: Optional[str], info: dict[str, Any],
+                         data: Optional[bytes] = None) -> dict[str, Any]:
     """Every sample of a shard through the per-sample reader, in the device output format.
 
     Returns ``{name: ('fixed', rows_bytes[N, size]) | ('ragged', values, offsets, flags)}``
     where ``flags`` is a uint8 array for ``str`` columns (1 = decode raises) else None.
+    ``data``: the shard file's bytes (read from memory, OracleMDSReader).
     """
-    r = OracleMDSReader(dirname, split, info)
+    r = OracleMDSReader(dirname, split, info, data=data)
     n = r.samples
     parts = [r.split_sample(r.get_sample_data(i)) for i in range(n)]
     out: dict[str, Any] = {}

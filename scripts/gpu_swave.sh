@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/${TAG:-swave}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 600 python3 -u -m pytest tests/test_device_copy_modes.py tests/test_device_fuzz.py -m gpu -x -q --timeout 300 --timeout-method thread -k "${PYTEST_K:-swave}" > "$OUT/pytest_gpu.log" 2>&1 || { tail -60 "$OUT/pytest_gpu.log"; exit 1; }
+timeout -k 10 600 python3 -u -m pytest tests/test_device_copy_modes.py tests/test_device_fuzz.py tests/test_malformed.py -m gpu -x -q --timeout 300 --timeout-method thread -k "${PYTEST_K:-swave or malformed or reference_outcomes or decode_sample}" > "$OUT/pytest_gpu.log" 2>&1 || { tail -60 "$OUT/pytest_gpu.log"; exit 1; }
 tail -2 "$OUT/pytest_gpu.log"
 export MDSX_PROBES=5,10
 VARS=${VARS:-"swave=0 swave=1 swave=1,swocc=4 swave=1,swocc=6 swave=1,swkb=8 swave=1,swtile=256 swave=0#ctl"}

@@ -178,7 +178,21 @@ def main():
     phases = {}
     for v, dec in decs.items():  # sdbg bit 16: the staged decode's cycles per phase, per tile
         dbg = [int(kv[5:], 0) for kv in v.split('#')[0].split(',') if kv.startswith('sdbg=')]
-        if dbg and dbg[0] & 64 and 'run=' in v:  # the lean streaming decode's wave stamps
+        swx = [int(kv[4:], 0) for kv in v.split('#')[0].split(',') if kv.startswith('swx=')]
+        if swx and swx[0] & 8:  # one sample per wave: per-wave stamps (mdsx_swave.hip kX 8)
+            dec.run()
+            torch.cuda.synchronize()
+            ntile = int(dec.batch.tile_shard.numel())
+            rows = dec.batch.total_rows
+            off = src_abs_offset(dec.plan.num_var, ntile, int(dec.batch.buffer.numel()))
+            raw = dec.workspace[off:off + 16 * rows].cpu().view(torch.int32).view(rows, 4)
+            raw = raw.double()
+            names = ['offsets_pair_in', 'loads_landed', 'stores_issued', 'wave_end']
+            phases[v] = dict(zip(names, [round(x) for x in raw.mean(dim=0).tolist()]))
+            phases[v]['median'] = [round(x) for x in raw.median(dim=0).values.tolist()]
+            phases[v]['p90'] = [round(x) for x in raw.quantile(0.9, dim=0).tolist()]
+            phases[v]['waves'] = rows
+        elif dbg and dbg[0] & 64 and 'run=' in v:  # the lean streaming decode's wave stamps
             dec.run()
             torch.cuda.synchronize()
             ntile = int(dec.batch.tile_shard.numel())

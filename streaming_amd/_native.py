@@ -59,6 +59,7 @@ EXPORTED_SYMBOLS = (
     'mdsx_scan_shards',
     'mdsx_decode_shards',
     'mdsx_decode_shards_single',
+    'mdsx_decode_sample',
     'mdsx_copy_probe',
     'mdsx_copy_probe_variant',
     'mdsx_copy_to_host',
@@ -179,6 +180,8 @@ def _declare(handle: ctypes.CDLL) -> None:
     handle.mdsx_decode_shards_single.argtypes = [
         vp, pb, ctypes.POINTER(ColumnOut), ctypes.POINTER(c_u64), vp, c_u64, vp, vp
     ]
+    handle.mdsx_decode_sample.restype = c_int
+    handle.mdsx_decode_sample.argtypes = [vp, vp, c_u32, vp, vp, vp]
     handle.mdsx_copy_probe.restype = c_int
     handle.mdsx_copy_probe.argtypes = [vp, vp, c_u64, vp]
     handle.mdsx_copy_probe_variant.restype = c_int

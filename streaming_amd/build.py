@@ -16,7 +16,7 @@ ROOT = os.path.dirname(HERE)
 SOURCES = [
     os.path.join(HERE, 'csrc', name)
     for name in ('mdsx_kernels.hip', 'mdsx_stage.hip', 'mdsx_run.hip', 'mdsx_rows.hip', 'mdsx_swave.hip',
-                 'mdsx_encode.hip', 'mdsx_hash.hip', 'mdsx_plan.cpp')
+                 'mdsx_sample.hip', 'mdsx_encode.hip', 'mdsx_hash.hip', 'mdsx_plan.cpp')
 ]
 HEADERS = [os.path.join(HERE, 'csrc', name)
            for name in ('mdsx_internal.h', 'mdsx_device.h', 'mdsx_decode.h', 'mdsx_ring.h',

@@ -86,7 +86,8 @@ struct mdsx_plan {
   int swave_kb = 6;        // ... KiB of a sample held in registers (4, 6 or 8; larger samples are
                            // copied straight from HBM)
   int swave_occ = 0;       // ... waves per SIMD its registers are bounded for (0: the compiler's)
-  int swave_tile = 64;     // ... rows per tile (the scan pass's unit: 256 / this tiles per block)
+  int swave_tile = 64;
+  int swave_x = 0;         // ... measurement variants (MDSX_TUNE swx, bits; mdsx_swave.hip)     // ... rows per tile (the scan pass's unit: 256 / this tiles per block)
   int gather_chunks = 2;  // 16-byte chunks per lane in the ragged gather (tile = 4 KiB x this)
   int gather_min = 256;   // ragged columns averaging fewer bytes per row use the gather kernel
   int group_max = 1024;   // ... fewer than this (and >= gather_min): four rows per wave

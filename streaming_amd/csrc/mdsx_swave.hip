@@ -74,7 +74,7 @@ __device__ __forceinline__ uint4 near_chunk(const uint4 (&L)[U], int G, int q, i
 // loaded chunks (S = the stream byte of output chunk 0's byte 0, h = d0 & 15; S >= -15). near:
 // S in [-16, 32) -- chunks from the registers; else from the wave's LDS copy (buf: stream byte 0).
 // Returns (utf8) whether the value is not well-formed UTF-8 (wave-uniform).
-template <bool kNT, int U>
+template <bool kNT, int U, int kX = 0>
 __device__ __forceinline__ bool sw_copy(const uint4 (&L)[U], const lds_u8* buf, uint64_t d0,
                                         uint32_t len, int32_t S, bool near, bool utf8, int lane) {
   const uint64_t dend = d0 + len;
@@ -106,12 +106,13 @@ __device__ __forceinline__ bool sw_copy(const uint4 (&L)[U], const lds_u8* buf, 
     }
     const uint64_t D = dbeg + 16ull * k;
     if (k < nch && D >= d0 && D + 16 <= dend) st16<kNT>(D, out);
-    if (g == 0 && (dbeg < d0 || dbeg + 16 > dend)) wave_edge_store(out, 0, dbeg, d0, dend, lane);
-    if (nch > 1 && (dend & 15) != 0 && nch - 1 >= 64u * uint32_t(g) &&
+    if ((kX & 2) == 0 && g == 0 && (dbeg < d0 || dbeg + 16 > dend))
+      wave_edge_store(out, 0, dbeg, d0, dend, lane);
+    if ((kX & 2) == 0 && nch > 1 && (dend & 15) != 0 && nch - 1 >= 64u * uint32_t(g) &&
         nch - 1 < 64u * uint32_t(g) + 64u)
       wave_edge_store(out, int(nch - 1 - 64u * uint32_t(g)), dbeg + 16ull * (nch - 1), d0, dend,
                       lane);
-    if (utf8) {
+    if ((kX & 1) == 0 && utf8) {
       const uint4 vout = keep_range(out, D, d0, dend);  // this value's bytes only
       const uint32_t any8 = (vout.x | vout.y | vout.z | vout.w) & 0x80808080u;
       if (__any(any8 != 0) || hi_c0(prev_w)) {  // a byte >= 0x80 (or a sequence open before)
@@ -125,10 +126,22 @@ __device__ __forceinline__ bool sw_copy(const uint4 (&L)[U], const lds_u8* buf, 
   return utf8 ? __any(bad) != 0 : false;
 }
 
+__device__ __forceinline__ uint64_t sw_clock() {
+  uint64_t c;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(c)::"memory");
+  return c;
+}
+
 // kOcc: registers bounded for that many waves per SIMD (0: the compiler's choice).
-template <bool kNT, int U, int kOcc>
+// kX (measurement only, MDSX_TUNE swx; bits 1-4 leave outputs incomplete): 1 no UTF-8 check, 2 no
+// partial edge chunk stored, 4 only the register-path columns written (none through LDS), 8
+// shader-clock stamps per sample into src_abs (u32 x 4 per row, cycles from the wave's start: its
+// offsets pair in, its loads landed -- an added vmcnt(0) wait --, its stores issued, its end).
+template <bool kNT, int U, int kOcc, int kX = 0>
 __global__ __launch_bounds__(64, kOcc > 0 ? kOcc : 1) void swave_decode_kernel(const DevArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint64_t t_start = (kX & 8) ? sw_clock() : 0;
+  uint32_t t_pair = 0, t_loads = 0;
   const lds_u8* const buf = (const lds_u8*)smem + kSwPad;
   const int lane = threadIdx.x;
   // XCD-contiguous samples: the offsets line and the partial output chunks two neighbouring
@@ -180,6 +193,7 @@ __global__ __launch_bounds__(64, kOcc > 0 ? kOcc : 1) void swave_decode_kernel(c
            : e - b < hv                                   ? MDSX_E_BOUNDS
                                                           : MDSX_OK;
   const uint32_t size = rc == MDSX_OK ? e - b : 0u;
+  if constexpr ((kX & 8) != 0) t_pair = uint32_t(sw_clock() - t_start);
   const uint64_t s0 = reinterpret_cast<uint64_t>(v.shard) + b;
   const uint32_t sa = uint32_t(s0 & 15);
   const uint4* const sal = reinterpret_cast<const uint4*>(s0 - sa);
@@ -193,6 +207,10 @@ __global__ __launch_bounds__(64, kOcc > 0 ? kOcc : 1) void swave_decode_kernel(c
   for (int u = 0; u < U; ++u) {
     const uint32_t k = 64u * uint32_t(u) + uint32_t(lane);
     L[u] = inreg && k < nload ? ld16<kNT>(sal + k) : make_uint4(0, 0, 0, 0);
+  }
+  if constexpr ((kX & 8) != 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    t_loads = uint32_t(sw_clock() - t_start);
   }
   // ---- geometry (mds/reader.py:111-125): lane c's length, its place by a wave prefix sum
   const uint32_t hl = uint32_t(__shfl(int(hd), vi > 0 ? vi : 0));
@@ -220,7 +238,7 @@ __global__ __launch_bounds__(64, kOcc > 0 ? kOcc : 1) void swave_decode_kernel(c
     // output chunk 0 of the column starts at stream byte S (relative to the aligned sample start)
     const int32_t S = int32_t(sa + rel) - int32_t(D & 15);
     const bool near = S >= -16 && S < 32;
-    const bool via_lds = small || (wide && !near);
+    const bool via_lds = (kX & 4) ? false : small || (wide && !near);
     if (__ballot(via_lds)) {
       // the chunks those columns' bytes lie in, copied to the wave's LDS
       const uint32_t lo = via_lds ? (sa + rel) >> 4 : 0xffffffffu;
@@ -242,9 +260,9 @@ __global__ __launch_bounds__(64, kOcc > 0 ? kOcc : 1) void swave_decode_kernel(c
       if (small) small_store(reinterpret_cast<uint8_t*>(D), lds16(buf + (sa + rel)), rb);
     }
     const uint64_t str_mask = __ballot(str), near_mask = __ballot(near);
-    for (uint64_t m = wide_mask; m; m &= m - 1) {  // wave-uniform, in column order
-      const int c = __builtin_ctzll(m);
-      const bool bad = sw_copy<kNT, U>(L, buf, readlane64(D, c),
+    for (uint64_t m = (kX & 4) ? wide_mask & near_mask : wide_mask; m; m &= m - 1) {
+      const int c = __builtin_ctzll(m);  // wave-uniform, in column order
+      const bool bad = sw_copy<kNT, U, kX>(L, buf, readlane64(D, c),
                                        uint32_t(__builtin_amdgcn_readlane(int(len), c)),
                                        __builtin_amdgcn_readlane(S, c), (near_mask >> c) & 1ull,
                                        (str_mask >> c) & 1ull, lane);
@@ -257,10 +275,18 @@ __global__ __launch_bounds__(64, kOcc > 0 ? kOcc : 1) void swave_decode_kernel(c
                                                   kHugeCountOffset);
     a.src_abs[atomicAdd(count, 1u)] = (uint64_t(tile) << 32) | t;
   }
+  const uint32_t t_copied = (kX & 8) ? uint32_t(sw_clock() - t_start) : 0u;
   // ---- the row's ragged offsets and str flags
   if (vi >= 0) {
     *gp(offp + row) = off;
     if (flp) *gp(flp + row) = uint8_t((badm >> lane) & 1ull);
+  }
+  if constexpr ((kX & 8) != 0) {
+    if (lane < 4) {
+      const uint32_t st = lane == 0 ? t_pair : lane == 1 ? t_loads : lane == 2 ? t_copied
+                                                                          : uint32_t(sw_clock() - t_start);
+      *gp(reinterpret_cast<uint32_t*>(a.src_abs) + 4ull * row + lane) = st;
+    }
   }
   // the shard header (mds/writer.py:133-144): u32 N, then N + 1 offsets
   if (first && lane == 0) {
@@ -296,6 +322,24 @@ int launch_swave_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) 
                        s, a);                                                                    \
     const int rc = hip_check(hipGetLastError(), "swave_decode_kernel launch");                   \
     return rc != MDSX_OK ? rc : launch_huge_rows(a, NT, s);                                      \
+  }
+  if (plan->swave_x) {  // measurement variants (nt, 6 KiB, the compiler's occupancy)
+    if (!nt || U != 6 || occ != 0)
+      return mdsx::fail(MDSX_E_ARG, "mdsx: swave variants: rnt=1, swkb=6, swocc=0 only");
+    if ((plan->swave_x & 8) && a.nvar < 2)
+      return mdsx::fail(MDSX_E_ARG, "mdsx: swave stamps need two ragged columns (src_abs space)");
+#define MDSX_SWAVE_X(X)                                                                          \
+  if (plan->swave_x == X) {                                                                      \
+    mdsx::set_last_kernel("swave_decode_kernel<true, 6, 0, " #X ">");                            \
+    hipLaunchKernelGGL((swave_decode_kernel<true, 6, 0, X>), dim3(unsigned(waves)), dim3(64),     \
+                       lds, s, a);                                                               \
+    const int rc = hip_check(hipGetLastError(), "swave_decode_kernel launch");                   \
+    return rc != MDSX_OK ? rc : launch_huge_rows(a, true, s);                                    \
+  }
+    MDSX_SWAVE_X(1) MDSX_SWAVE_X(2) MDSX_SWAVE_X(3) MDSX_SWAVE_X(4) MDSX_SWAVE_X(7)
+    MDSX_SWAVE_X(8)
+#undef MDSX_SWAVE_X
+    return mdsx::fail(MDSX_E_ARG, "mdsx: swave variant out of range");
   }
   MDSX_SWAVE(true, 6, 0)
   MDSX_SWAVE(true, 6, 4)

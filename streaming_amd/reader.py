@@ -36,7 +36,7 @@ import torch
 from streaming_amd import _native
 from streaming_amd.array import Array
 from streaming_amd.cache import DecodedShardCache, default_cache
-from streaming_amd.decoder import (DecodedBatch, Plan, RaggedColumn, _status_error, decode_batch,
+from streaming_amd.decoder import (DecodedBatch, Plan, RaggedColumn, _check, _status_error,
                                    output_bytes, stage_shards)
 from streaming_amd.encodings import (host_object_decode, is_mds_encoding_safe,
                                      ndarray_dyn_decode, parse_encoding)
@@ -385,36 +385,6 @@ class MDSReader(JointReader):
                 f'Relative sample index {idx} is not present in the {self.raw_data.basename} file.')
         return data
 
-    def _check_row(self, entry: _Decoded, idx: int) -> None:
-        """The decode of this shard reported an error: raise only if sample ``idx`` is one of the
-        bad ones (the reference raises only when a bad sample is read, mds/reader.py:145-148)."""
-        st = entry.status
-        if st.code not in (_native.MDSX_E_EMPTY, _native.MDSX_E_BOUNDS):
-            raise _status_error(st, self.plan)  # shard-level (header) error: every sample
-        # the device checks per sample (decode_kernel): the offsets pair inside the file after
-        # the offsets table, the u32 size heads and every column inside the sample
-        size = os.stat(self._filename()).st_size
-        with open(self._filename(), 'rb', 0) as fp:
-            fp.seek((1 + idx) * 4)
-            begin, end = (int(x) for x in np.frombuffer(fp.read(8), np.uint32))
-        if not (4 + 4 * (self.samples + 1) <= begin <= end <= size):
-            raise ValueError(f'MDS sample {idx} of {self.raw_data.basename} is out of bounds '
-                             f'([{begin}, {end}) in a file of {size} bytes).')
-        data = self.get_sample_data(idx)  # IndexError for an empty sample, as the reference
-        need, pos = 0, 0
-        for size_ in self.column_sizes:
-            if size_:
-                need += int(size_)
-            else:
-                if pos + 4 > len(data):
-                    need = len(data) + 1
-                    break
-                need += 4 + int(np.frombuffer(data[pos:pos + 4], np.uint32)[0])
-                pos += 4
-        if need > len(data):
-            raise ValueError(f'MDS sample {idx} of {self.raw_data.basename}: columns exceed the '
-                             f'sample ({need} > {len(data)} bytes).')
-
     def _materialize(self, host: _HostShard, idx: int) -> dict[str, Any]:
         getters = host.getters
         if getters is None:
@@ -491,7 +461,11 @@ class MDSReader(JointReader):
         os.stat(self._filename())  # FileNotFoundError once evicted, as the reference's open()
         entry = self.cache.lookup(self._key) or self._decode_entry()
         if entry.status.code != 0:
-            self._check_row(entry, idx)
+            # the whole-shard decode reported a sample that does not fit its range or columns (or
+            # a header error): every sample of this shard takes the reference's own per-sample
+            # path, get_sample_data + decode_sample (base/reader.py:310-320), whose slices clip
+            # where the whole-shard decode refuses (mdsx_decode_sample)
+            return self.decode_sample(self.get_sample_data(idx))
         host = entry.host
         if host is None:
             with self._lock:
@@ -504,14 +478,47 @@ class MDSReader(JointReader):
         return self._materialize(host, idx)
 
     def decode_sample(self, data: bytes) -> dict[str, Any]:
-        """Decode one sample's bytes on the device, as a one-sample shard."""
+        """Decode one sample's bytes on the device (mds/reader.py:103-126), each column handed the
+        slice the reference hands it: a size head larger than the bytes left, or a sample shorter
+        than its fixed columns, gives a shorter slice, which the column's decoder returns (bytes),
+        decodes (str: UnicodeDecodeError on a cut sequence) or rejects as numpy does (int,
+        scalars, static ndarrays); a size head cut short raises ValueError (mdsx_decode_sample)."""
+        _native.check_fork()
+        _native.require_gpu()
         plan = self.plan
-        header = 4 + 8
-        shard = (np.uint32(1).tobytes() + np.array([header, header + len(data)], np.uint32).tobytes() +
-                 data)
-        batch = stage_shards([shard], [1], plan, device=self.device)
-        decoded = decode_batch(plan, batch)
-        return self._materialize(_HostShard(plan, decoded), 0)
+        n = len(data)
+        dev = torch.device(self.device or 'cuda')
+        if dev.type == 'cuda' and dev.index is None:
+            dev = torch.device('cuda', torch.cuda.current_device())
+        host = torch.zeros(n + 128, dtype=torch.uint8)  # 64 readable bytes before and after
+        if n:
+            host[64:64 + n] = torch.from_numpy(np.frombuffer(data, np.uint8).copy())
+        buf = host.to(dev)
+        values = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+        ncols = len(plan.columns)
+        meta = torch.zeros(2 * ncols + 1, dtype=torch.int64, device=dev)
+        rc = _native.lib().mdsx_decode_sample(plan.handle, buf.data_ptr() + 64, n,
+                                              values.data_ptr(), meta.data_ptr(),
+                                              torch.cuda.current_stream(dev).cuda_stream)
+        if rc != 0:
+            _check(rc, 'mdsx_decode_sample')
+        m = meta.cpu().tolist()  # (syncs the stream)
+        vals = values.cpu().numpy()
+        vals.setflags(write=False)  # (views of it are read-only, as np.frombuffer's)
+        if m[-1]:  # `size, = np.frombuffer(data[idx:idx + 4], np.uint32)` on a short head
+            vi = sum(1 for c in plan.columns[:m[-1] - 1] if not c.is_fixed)  # its head's index
+            if 4 * vi >= n:
+                raise ValueError('not enough values to unpack (expected 1, got 0)')
+            raise ValueError('buffer size must be a multiple of element size')
+        sample = {}
+        for c, (col, enc, info) in enumerate(zip(plan.columns, self.column_encodings,
+                                                 self._infos)):
+            raw = vals[m[2 * c]:m[2 * c] + m[2 * c + 1]]
+            if col.is_fixed and len(raw) == col.row_bytes:
+                sample[col.name] = self._value(enc, info, raw, fixed=True)
+            else:  # ragged, or a fixed column clipped short: its decoder sees the short slice
+                sample[col.name] = self._value(enc, info, raw.tobytes(), fixed=False)
+        return sample
 
 
 def reader_from_json(dirname: str, split: Optional[str], obj: dict[str, Any],

@@ -38,6 +38,18 @@ def test_launcher_spawns_ranks_and_partitions_shards(gpus):
         for r in ranks:
             assert all(s % gpus == r['rank'] for s in r['shards'])  # owned_shards: g -> g % N
             assert len(r['shards']) == per_gpu  # weak scaling: fixed work per GPU
+    # the N-GPU line's per-rank report (gathered over the gloo group) and its aggregation
+    per = line['per_rank']
+    assert [p['rank'] for p in per] == list(range(gpus))
+    for p in per:
+        for k in ('ms_per_step', 'kernel_ms', 'frac', 'step_frac', 'copy_ceiling_GBps',
+                  'frac_of_same_run_copy'):
+            assert isinstance(p[k], float) and p[k] > 0, (k, p)
+    summ = line['per_rank_summary']
+    assert summ['ranks'] == gpus and summ['slowest_rank'] == gpus - 1
+    for k in ('ms_per_step', 'kernel_ms', 'frac', 'copy_ceiling_GBps', 'frac_of_same_run_copy'):
+        xs = [p[k] for p in per]
+        assert summ[k]['min'] == min(xs) and summ[k]['max'] == max(xs), k
 
 
 def test_world_mismatch_is_an_error():

@@ -3,11 +3,14 @@
 g % 8 (``owned_shards``; the build's replacement for the reference's per-rank sample split,
 ``streaming/base/partition/orig.py:140-181``), generated from per-shard seeds exactly as
 ``bench.py --gpus 8`` does -- resident at once and decoded in ONE batch, bit-exact against the
-encoded columns. Peak device memory: the shards (51 GB) + the decoded columns (51 GB) + one
+encoded columns, and eight spread shards sample by sample against the oracle. Peak device memory: the shards (51 GB) + the decoded columns (51 GB) + one
 shard's regenerated source at a time."""
 
+import numpy as np
 import pytest
 import torch
+
+from oracle import mds_oracle
 
 from streaming_amd.decoder import decode_batch
 from streaming_amd.distributed import owned_shards
@@ -51,6 +54,19 @@ def test_config_d_rank0_share_bit_exact():
         want = torch.randint(0, 256, (per, 4096), dtype=torch.uint8, device=dev, generator=gen)
         assert torch.equal(x[s * per:(s + 1) * per], want), g
         assert int(ids[s * per]) == g * per  # global sample ids of the 100M-sample layout
+    # eight shards spread over the share: every sample against the oracle reading the shard's
+    # bytes (the reference's per-sample get_sample_data + decode_sample, mds/reader.py:103-149)
+    names, encs, sizes = synth.plan.key
+    for s in sorted({round(k * (len(mine) - 1) / 7) for k in range(8)}):
+        info = {'column_names': list(names), 'column_encodings': list(encs),
+                'column_sizes': [sz or None for sz in sizes], 'samples': batch.samples[s],
+                'raw_data': {'basename': f'shard.{mine[s]:05d}.mds'}}
+        data = batch.buffer[batch.offsets[s]:batch.offsets[s] + batch.sizes[s]].cpu().numpy()
+        want = mds_oracle.decode_shard_columns(None, None, info, data=data.tobytes())
+        r0, n = batch.row0[s], batch.samples[s]
+        assert np.array_equal(ids[r0:r0 + n].cpu().numpy().view(np.uint8).reshape(n, 4),
+                              want['id'][1]), mine[s]
+        assert np.array_equal(x[r0:r0 + n].cpu().numpy(), want['x'][1]), mine[s]
     peak = torch.cuda.max_memory_allocated(dev)
     assert peak < 106e9, peak  # shards + outputs (~102.7 GB) + one regenerated shard
     del out, ids, x, synth, batch
