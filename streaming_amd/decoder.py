@@ -706,6 +706,19 @@ class BatchDecoder:
                 o.flags = out.flags.data_ptr() if out.flags is not None else None
                 o.capacity = int(out.values.numel())
 
+    def stream_tensors(self) -> list[torch.Tensor]:
+        """The device tensors a pass reads or writes: the batch and its tables, the workspace,
+        the totals and every output."""
+        ts = [self.batch.buffer, self.batch.descs, self.batch.tile_shard, self.workspace,
+              self.totals]
+        for col in self.plan.columns:
+            out = self.outputs[col.name]
+            if isinstance(out, RaggedColumn):
+                ts += [t for t in (out.values, out.offsets, out.flags) if t is not None]
+            else:
+                ts.append(self._fixed_raw[col.name])
+        return ts
+
     def _scan(self, stream: int) -> None:
         _check(
             self.plan._lib.mdsx_scan_shards(self.plan.handle, ctypes.byref(self._abi), self._outs,
@@ -865,9 +878,12 @@ class ScanAheadDecoder:
 
     def _new_slot(self, batch: DeviceBatch) -> BatchDecoder:
         caps = self._caps
-        if caps is None and self.plan.num_var:
+        if self.plan.num_var and (caps is None or batch is not self.batch):
+            # the given capacities fit the constructor's batch; another batch of the plan gets at
+            # least its upper bound, so no column can overflow (MDSX_E_CAPACITY) however it sizes
             bound = payload_bound(self.plan, batch)
-            caps = {c.name: bound for c in self.plan.columns if not c.is_fixed}
+            caps = {c.name: max(bound, int((caps or {}).get(c.name, 0)))
+                    for c in self.plan.columns if not c.is_fixed}
         dec = BatchDecoder(self.plan, batch, capacities=caps)
         dec._sized = True
         return dec
@@ -896,6 +912,10 @@ class ScanAheadDecoder:
             dec._scan(self._side.cuda_stream)
             if events is not None:
                 events[1].record(self._side)
+        # the tensors the side stream's scan reads and writes were allocated on the current stream:
+        # the caching allocator must not hand them out again before that scan is done
+        for t in dec.stream_tensors():
+            t.record_stream(self._side)
         done = torch.cuda.Event()
         done.record(self._side)
         self._pending.append((si, done, None))
@@ -973,6 +993,14 @@ class ScanAheadDecoder:
         self._side.synchronize()
         self._pending.clear()
         self._free = list(range(len(self._slots)))
+
+    def __del__(self) -> None:
+        side = getattr(self, '_side', None)
+        if side is not None and getattr(self, '_pending', None):
+            try:  # a scan still in flight writes this decoder's slots
+                side.synchronize()
+            except Exception:  # noqa: BLE001 -- interpreter shutdown: nothing left to protect
+                pass
 
 
 def decode_batch(plan: Plan, batch: DeviceBatch, check: bool = True,

@@ -107,3 +107,32 @@ def test_scan_ahead_capacity_error():
     sad.decode()
     with pytest.raises(RuntimeError, match='capacity exceeded'):
         sad.check()
+
+
+def test_scan_ahead_other_batch_gets_its_bound():
+    """Capacities given for the constructor's batch: a slot built for another batch of the plan
+    gets at least that batch's upper bound, so it decodes whole."""
+    synths = _batches((3072, 5120), (16, 256))
+    small = {'b': 1024, 's': 1024}
+    sad = ScanAheadDecoder(synths[0].plan, synths[0].batch, capacities=small)
+    sad.scan(synths[1].batch)
+    got = sad.decode()
+    sad.check()
+    _sources_equal(got, synths[1].sources)
+    sad.close()
+
+
+def test_scan_ahead_dropped_with_a_scan_in_flight():
+    """A decoder dropped while its side stream still scans: the slot tensors carry the side
+    stream (record_stream) and the decoder waits for it, so their memory is not reused early."""
+    synths = _batches((3072, 5120), (16, 256))
+    sad = ScanAheadDecoder(synths[0].plan, synths[0].batch)
+    sad.scan()
+    del sad  # no close()
+    fill = [torch.full((1 << 24,), 7, dtype=torch.uint8, device='cuda') for _ in range(8)]
+    torch.cuda.synchronize()
+    assert all(int(f[-1]) == 7 for f in fill)
+    dec = BatchDecoder(synths[0].plan, synths[0].batch)
+    out = dec.run()
+    dec.check()
+    _sources_equal(out, synths[0].sources)
