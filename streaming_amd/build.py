@@ -106,6 +106,27 @@ def _check_cross_lane_reads(obj: str, want: tuple = ('rows_decode_kernel',)) -> 
                                      for name, addrs in bad))
 
 
+# Kernels that must not spill at all: a VGPR reloaded from scratch under a partial exec mask holds
+# stale bits in its inactive lanes, which a later cross-lane read with every lane active returns.
+NO_SCRATCH = {'mdsx_swave.hip': ('swave_decode_kernel',)}
+
+
+def _check_no_scratch(obj: str, want: tuple) -> None:
+    rocm = os.environ.get('ROCM_PATH', '/opt/rocm')
+    text = subprocess.run([os.path.join(rocm, 'lib', 'llvm', 'bin', 'llvm-readelf'), '--notes',
+                           obj], capture_output=True, text=True, check=True).stdout
+    name, bad = None, []
+    for line in text.splitlines():
+        line = line.strip()
+        if line.startswith('.name:'):
+            name = line.split(':', 1)[1].strip()
+        elif line.startswith('.private_segment_fixed_size:') and name and \
+                any(w in name for w in want) and int(line.split(':', 1)[1]) != 0:
+            bad.append(name)
+    if bad:
+        raise RuntimeError(f'mdsx build: kernels that must not spill use scratch: {bad}')
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     """Compile every source to an object in parallel, then link libmdsx.so (in-tree)."""
     os.makedirs(os.path.dirname(OUTPUT), exist_ok=True)
@@ -129,6 +150,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
             f.result()
     for src, obj in devs.items():
         _check_cross_lane_reads(obj, ISA_CHECKED[src])
+        if src in NO_SCRATCH:
+            _check_no_scratch(obj, NO_SCRATCH[src])
     tmp = OUTPUT + '.tmp'
     cmd = [hipcc(), f'--offload-arch={ARCH}', '-shared', '-fPIC', '-o', tmp, *objs]
     if verbose:

@@ -85,10 +85,19 @@ struct DevArgs {
   uint32_t rows_pipe;    // row-parallel decode: tiles per workgroup through two stages (0: one)
   uint32_t rw_k;         // (measurement only, rowwave kX bit 2: offsets[0] taken as hdr_end + rw_k)
   uint32_t swave;        // ragged plans of long samples: one sample per wave (mdsx_swave.hip)
+  uint4* sw_rec;         // [ntiles x tile_rows] its per-sample records (scan_tiles_kernel<true>)
+  uint32_t sw_lds;       // ... bytes of its per-wave LDS copy of the columns past the first
   uint32_t gather_block0[MDSX_MAX_COLUMNS + 1];  // first gather workgroup of each ragged column
   DevCol cols[MDSX_MAX_COLUMNS];
 };
 
+
+// The one-sample-per-wave decode's record of a sample slot (tile x tile_rows + row of the tile),
+// written by its scan pass (scan_tiles_kernel<true>) so that a decode wave starts with ONE load
+// instead of the tile -> shard -> offsets chain: x | y << 32 = the sample's first byte in the batch
+// (bits 0-39) and its shard (bits 40-63); z = its bytes, or kSwIdle (no sample in the slot) /
+// kSwBad (its offsets failed the file checks: reported by the scan pass); w = its output row.
+constexpr uint32_t kSwIdle = 0xffffffffu, kSwBad = 0xfffffffeu;
 
 // Per-shard facts shared by the scan and decode kernels.
 struct TileView {

@@ -85,8 +85,11 @@ struct mdsx_plan {
                            // one-wave workgroup, in registers, instead (mdsx_swave.hip)
   int swave_kb = 6;        // ... KiB of a sample held in registers (4, 6 or 8; larger samples are
                            // copied straight from HBM)
-  int swave_occ = 0;       // ... waves per SIMD its registers are bounded for (0: the compiler's)
+  int swave_occ = 0;       // ... waves per SIMD its registers are bounded for (0: the compiler's;
+                           // bounds that make it spill are not built: build.py refuses scratch)
   int swave_tile = 64;
+  int swave_lds = 2048;    // ... bytes of its per-wave LDS copy of the columns past the first (a
+                           // sample whose later columns span more takes the huge-row kernel)
   int swave_x = 0;         // ... measurement variants (MDSX_TUNE swx, bits; mdsx_swave.hip)     // ... rows per tile (the scan pass's unit: 256 / this tiles per block)
   int gather_chunks = 2;  // 16-byte chunks per lane in the ragged gather (tile = 4 KiB x this)
   int gather_min = 256;   // ragged columns averaging fewer bytes per row use the gather kernel

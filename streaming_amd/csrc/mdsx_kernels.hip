@@ -50,6 +50,10 @@ namespace mdsx_kernels {
 // row order and a partial tile's missing rows count zero, so the scan is the output order; the
 // decode adds the scan block's prefix. Totals per scan block, not per tile, keep pass 1b an
 // eighth as long (32-row tiles).
+// kRec (the one-sample-per-wave decode): every sample slot's record (sw_rec), its range errors and
+// its shard's header checked here instead of in the decode (mds/reader.py:137-148,
+// mds/writer.py:133-144).
+template <bool kRec = false>
 __global__ __launch_bounds__(kBlock) void scan_tiles_kernel(const DevArgs a) {
   __shared__ int64_t s_wsum[kBlock / 64];
   const int t = threadIdx.x;
@@ -64,9 +68,25 @@ __global__ __launch_bounds__(kBlock) void scan_tiles_kernel(const DevArgs a) {
   const bool in_tile = tile_ok && v.table_ok && tt < int(v.nrows);
   uint32_t b = 0, e = 0;
   bool ok = false;
+  int rc = MDSX_OK;
   if (in_tile) {
-    const int rc = sample_range(v, i, &b, &e);
+    rc = sample_range(v, i, &b, &e);
     ok = rc == MDSX_OK && uint64_t(b) + 4ull * a.nvar <= e;
+  }
+  if constexpr (kRec) {
+    if (tile_ok) {
+      const uint64_t src = v.d.offset + b;
+      const uint32_t z = !in_tile ? kSwIdle : rc != MDSX_OK ? kSwBad : e - b;
+      a.sw_rec[uint64_t(tile) * uint32_t(TR) + uint32_t(tt)] =
+          make_uint4(uint32_t(src), uint32_t(src >> 32) | (v.shard_idx << 8), z,
+                     uint32_t(v.d.row0 + i));
+      if (in_tile && rc != MDSX_OK) report_decode(a, rc, int(v.shard_idx), int(i), -1);
+      // the shard header (mds/writer.py:133-144): u32 N, then N + 1 offsets
+      if (tt == 0 && tile == v.d.tile0 &&
+          (!v.table_ok || *reinterpret_cast<const uint32_t*>(v.shard) != v.d.samples ||
+           v.offs[0] < v.hdr_end || v.offs[v.d.samples] > v.d.bytes))
+        report_decode(a, MDSX_E_HEADER, int(v.shard_idx), -1, -1);
+    }
   }
   const bool few = a.nvar <= kHeadRegs;  // heads in registers (else re-read per column)
   Heads h;
@@ -745,7 +765,7 @@ __global__ __launch_bounds__(kBlock) void gather_ragged_kernel(const DevArgs a) 
 
 // ---------------------------------------------------------------------------------------------
 struct Layout {
-  uint64_t tile_total, tile_prefix, chunk_sum, tile_run, src_abs, row_map, map_len,
+  uint64_t tile_total, tile_prefix, chunk_sum, tile_run, src_abs, row_map, sw_rec, map_len,
       total;
 };
 
@@ -765,7 +785,12 @@ Layout workspace_layout(const mdsx_plan* plan, const mdsx_batch* b) {
   L.tile_run = L.chunk_sum + round256(nv * (b->ntiles / kScanChunk + 1) * 8);
   L.src_abs = L.tile_run + round256(nv ? uint64_t(b->ntiles) * sizeof(TileRun) : 0);
   L.row_map = L.src_abs + round256(nv * b->rows * 8);
-  L.total = L.row_map + round256(nv * L.map_len * 4);
+  L.sw_rec = L.row_map + round256(nv * L.map_len * 4);
+  L.total = L.sw_rec + round256(use_swave_decode(plan, b->bytes, b->rows)
+                                    ? uint64_t(b->ntiles) *
+                                          uint64_t(b->tile_rows ? b->tile_rows
+                                                                : uint32_t(plan->tile_rows)) * 16
+                                    : 0);
   return L;
 }
 
@@ -794,6 +819,7 @@ int build_args(const mdsx_plan* plan, const mdsx_batch* b, const mdsx_column_out
   a->tile_run = reinterpret_cast<TileRun*>(ws + L.tile_run);
   a->src_abs = reinterpret_cast<uint64_t*>(ws + L.src_abs);
   a->row_map = reinterpret_cast<uint32_t*>(ws + L.row_map);
+  a->sw_rec = reinterpret_cast<uint4*>(ws + L.sw_rec);
   a->lookback = reinterpret_cast<uint64_t*>(ws + L.tile_total);  // single pass: no tile totals
   a->ticket = reinterpret_cast<uint32_t*>(ws + kTicketOffset);
   a->map_len = L.map_len;
@@ -1387,8 +1413,12 @@ static int scan_pass(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
     const bool nt = plan->scan_nt >= 0 ? plan->scan_nt != 0 : a.run_slots == 0;
     rc = launch_stage_totals(a, nt, s);
     if (rc != MDSX_OK) return rc;
+  } else if (a.ntiles > 0 && a.swave) {
+    hipLaunchKernelGGL(scan_tiles_kernel<true>, dim3(a.nscan), dim3(kBlock), 0, s, a);
+    rc = hip_check(hipGetLastError(), "scan_tiles_kernel launch");
+    if (rc != MDSX_OK) return rc;
   } else if (a.ntiles > 0) {
-    hipLaunchKernelGGL(scan_tiles_kernel, dim3(a.nscan), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(scan_tiles_kernel<false>, dim3(a.nscan), dim3(kBlock), 0, s, a);
     rc = hip_check(hipGetLastError(), "scan_tiles_kernel launch");
     if (rc != MDSX_OK) return rc;
   }

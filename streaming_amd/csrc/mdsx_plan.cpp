@@ -247,9 +247,11 @@ void apply_tuning(mdsx_plan* p) {
       p->swave = v ? 1 : 0;
     } else if (key == "swkb" && (v == 4 || v == 6 || v == 8)) {
       p->swave_kb = int(v);
+    } else if (key == "swlds" && v >= 1 && v <= 8) {
+      p->swave_lds = int(v) * 1024;
     } else if (key == "swx" && v >= 0 && v <= 15) {
       p->swave_x = int(v);
-    } else if (key == "swocc" && (v == 0 || v == 4 || v == 5 || v == 6)) {
+    } else if (key == "swocc" && (v == 0 || v == 4 || v == 6)) {
       p->swave_occ = int(v);
     } else if (key == "swtile" && (v == 1 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32 ||
                                    v == 64 || v == 128 || v == 256)) {

@@ -71,12 +71,13 @@ __device__ __forceinline__ uint4 near_chunk(const uint4 (&L)[U], int G, int q, i
 }
 
 // One wide column of the sample: output bytes [d0, d0 + len) from stream byte S + h of the
-// loaded chunks (S = the stream byte of output chunk 0's byte 0, h = d0 & 15; S >= -15). near:
-// S in [-16, 32) -- chunks from the registers; else from the wave's LDS copy (buf: stream byte 0).
+// loaded chunks (S = the stream byte of output chunk 0's byte 0, h = d0 & 15; S >= -15). kNear:
+// S in [-16, 32) -- chunks from the registers; else from the wave's LDS copy (buf: where stream
+// byte 0 would be).
 // Returns (utf8) whether the value is not well-formed UTF-8 (wave-uniform).
-template <bool kNT, int U, int kX = 0>
+template <bool kNT, int U, bool kNear, int kX = 0>
 __device__ __forceinline__ bool sw_copy(const uint4 (&L)[U], const lds_u8* buf, uint64_t d0,
-                                        uint32_t len, int32_t S, bool near, bool utf8, int lane) {
+                                        uint32_t len, int32_t S, bool utf8, int lane) {
   const uint64_t dend = d0 + len;
   const uint64_t dbeg = d0 & ~uint64_t(15);
   const uint32_t nch = uint32_t((((dend + 15) & ~uint64_t(15)) - dbeg) >> 4);
@@ -90,7 +91,7 @@ __device__ __forceinline__ bool sw_copy(const uint4 (&L)[U], const lds_u8* buf, 
     if (64u * uint32_t(g) >= nch) break;  // wave-uniform
     const uint32_t k = 64u * uint32_t(g) + uint32_t(lane);
     uint4 out;
-    if (near) {
+    if constexpr (kNear) {
       const uint4 lo = near_chunk<U>(L, g, q, lane);
       out = lo;
       if (sh != 0) {
@@ -144,33 +145,32 @@ __global__ __launch_bounds__(64, kOcc > 0 ? kOcc : 1) void swave_decode_kernel(c
   uint32_t t_pair = 0, t_loads = 0;
   const lds_u8* const buf = (const lds_u8*)smem + kSwPad;
   const int lane = threadIdx.x;
-  // XCD-contiguous samples: the offsets line and the partial output chunks two neighbouring
+  // XCD-contiguous samples: the records' lines and the partial output chunks two neighbouring
   // samples share meet in one L2
   const uint32_t blk = (a.xcd_order & kXcdSeg) ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-  const uint32_t lg = uint32_t(__builtin_ctz(uint32_t(a.tile_rows)));
-  const uint32_t tile = blk >> lg, t = blk & uint32_t(a.tile_rows - 1);
+  const uint32_t tile = blk >> uint32_t(__builtin_ctz(uint32_t(a.tile_rows)));
   if (tile >= a.ntiles) return;  // wave-uniform; no barrier in this kernel
-  const TileView v = tile_view(a, tile);
-  const bool first = t == 0 && tile == v.d.tile0;
-  if (!v.table_ok) {
-    if (first && lane == 0) report_decode(a, MDSX_E_HEADER, int(v.shard_idx), -1, -1);
-    return;
-  }
-  if (t >= v.nrows) return;
-  const uint32_t i = v.r0 + t;
-  const uint64_t row = v.d.row0 + i;
+  // ---- requested first: the sample's record (its scan pass: the sample's first byte, size,
+  // shard and output row -- the offsets pair of mds/reader.py:137-142 checked there) and the
+  // ragged outputs' positions (lane c: column c; the scan pass left the scan-block-local offset in
+  // offsets[row])
+  const uint4 rec = a.sw_rec[blk];
+  // (readfirstlane returns an int: every field goes through uint32_t before it widens, or a byte
+  // offset past 2 GiB would sign-extend)
+  const uint32_t z = uint32_t(__builtin_amdgcn_readfirstlane(rec.z));
+  if (z == kSwIdle) return;
+  const uint32_t ry = uint32_t(__builtin_amdgcn_readfirstlane(rec.y));
+  const uint64_t row = uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(rec.w)));
+  const uint64_t src = uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(rec.x))) |
+                       (uint64_t(ry & 0xffu) << 32);
+  const uint32_t shard = ry >> 8;
   const int ncols = a.ncols, nvar = a.nvar;
   const uint32_t hv = 4u * uint32_t(nvar);
-  // ---- requested first: the offsets pair and the ragged outputs' positions (lane c: column c;
-  // the scan pass left the scan-block-local offset in offsets[row])
-  const uint32_t b = __builtin_amdgcn_readfirstlane(v.offs[i]);
-  const uint32_t e = __builtin_amdgcn_readfirstlane(v.offs[i + 1]);
   int vi = -1;
   uint32_t rb = 0;
   bool str = false;
   uint64_t data = 0, cap = 0;
   int64_t* offp = nullptr;
-  uint8_t* flp = nullptr;
   for (int c = 0; c < ncols; ++c) {  // uniform
     const DevCol& col = a.cols[c];
     const int cv = col.var_index;
@@ -178,30 +178,26 @@ __global__ __launch_bounds__(64, kOcc > 0 ? kOcc : 1) void swave_decode_kernel(c
     const bool cs = col.kind == MDSX_KIND_STR && col.flags != nullptr;
     const uint64_t cdata = reinterpret_cast<uint64_t>(col.data);
     int64_t* const coffs = col.offsets;
-    uint8_t* const cflags = col.flags;
     const uint64_t ccap = col.capacity;
-    if (lane == c) {
-      vi = cv, rb = crb, str = cs, data = cdata, offp = coffs,
-      flp = cflags, cap = ccap;
-    }
+    if (lane == c) vi = cv, rb = crb, str = cs, data = cdata, offp = coffs, cap = ccap;
   }
   int64_t off = 0;
   if (vi >= 0) off = a.tile_prefix[uint64_t(vi) * a.nscan + tile / a.scan_per] + offp[row];
-  // ---- the sample (mds/reader.py:137-148): its heads, then all of its bytes
-  int rc = !(v.hdr_end <= b && b <= e && e <= v.d.bytes) ? MDSX_E_BOUNDS
-           : b == e                                       ? MDSX_E_EMPTY
-           : e - b < hv                                   ? MDSX_E_BOUNDS
-                                                          : MDSX_OK;
-  const uint32_t size = rc == MDSX_OK ? e - b : 0u;
+  // the row inside its shard, for an error report (rare: one more load)
+  auto row_in_shard = [&]() { return int(row - a.shards[shard].row0); };
+  // ---- the sample (mds/reader.py:137-148): lane c's size head, then all of its bytes
+  int rc = z == kSwBad ? MDSX_E_BOUNDS : z < hv ? MDSX_E_BOUNDS : MDSX_OK;
+  const bool reported = z == kSwBad;  // (by the scan pass)
+  const uint32_t size = rc == MDSX_OK ? z : 0u;
   if constexpr ((kX & 8) != 0) t_pair = uint32_t(sw_clock() - t_start);
-  const uint64_t s0 = reinterpret_cast<uint64_t>(v.shard) + b;
+  const uint64_t s0 = reinterpret_cast<uint64_t>(a.batch) + src;
   const uint32_t sa = uint32_t(s0 & 15);
   const uint4* const sal = reinterpret_cast<const uint4*>(s0 - sa);
   const uint32_t nload = (sa + size + 15u) >> 4;
   const bool inreg = rc == MDSX_OK && nload <= 64u * U;  // wave-uniform
-  uint32_t hd = 0;
-  if (rc == MDSX_OK && lane < nvar)
-    hd = load_u32_any(reinterpret_cast<const uint8_t*>(s0) + 4u * uint32_t(lane));
+  uint32_t hl = 0;
+  if (rc == MDSX_OK && lane < ncols && vi >= 0)
+    hl = load_u32_any(reinterpret_cast<const uint8_t*>(s0) + 4u * uint32_t(vi));
   uint4 L[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -212,74 +208,91 @@ __global__ __launch_bounds__(64, kOcc > 0 ? kOcc : 1) void swave_decode_kernel(c
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     t_loads = uint32_t(sw_clock() - t_start);
   }
-  // ---- geometry (mds/reader.py:111-125): lane c's length, its place by a wave prefix sum
-  const uint32_t hl = uint32_t(__shfl(int(hd), vi > 0 ? vi : 0));
+  // ---- geometry (mds/reader.py:111-125): lane c's length, its place by a wave prefix sum (DPP;
+  // 32-bit sums of at most 64 columns of a sample under 64 MiB cannot wrap)
   const uint32_t len = lane < ncols ? (vi >= 0 ? hl : rb) : 0u;
   const bool over = lane < ncols && len > size;
   const uint32_t lc = over ? 0u : len;
-  const uint32_t incl = wave_incl_u32(lc, lane, ncols);
+  const uint32_t incl = size < (1u << 26) ? wave_incl_dpp(lc) : wave_incl_u32(lc, lane, ncols);
   const uint32_t total = uint32_t(__builtin_amdgcn_readlane(int(incl), ncols - 1));
   if (rc == MDSX_OK && (__any(over) || total > size - hv)) rc = MDSX_E_BOUNDS;
-  if (rc != MDSX_OK && lane == 0) report_decode(a, rc, int(v.shard_idx), int(i), -1);
+  if (rc != MDSX_OK && !reported && lane == 0)
+    report_decode(a, rc, int(shard), row_in_shard(), -1);
   const bool ok = rc == MDSX_OK;  // wave-uniform
   const uint32_t rel = hv + incl - lc;  // the column's first byte inside the sample
   bool skip = false;
   if (ok && vi >= 0 && uint64_t(off) + len > cap) {
-    report_decode(a, MDSX_E_CAPACITY, int(v.shard_idx), int(i), lane);
+    report_decode(a, MDSX_E_CAPACITY, int(shard), row_in_shard(), lane);
     skip = true;  // the sample writes nothing of the column
   }
+  // the row's ragged offsets, now (their registers are then free for the copies)
+  if (vi >= 0) *gp(offp + row) = off;
   const bool is_small = lane < ncols && vi < 0 && rb <= uint32_t(kSmallMax);
   const uint64_t D = vi >= 0 ? data + uint64_t(off) : data + row * rb;
   const bool small = ok && is_small;
   const bool wide = ok && lane < ncols && !is_small && !skip && len > 0;
   const uint64_t wide_mask = __ballot(wide);
   uint64_t badm = 0;  // bit c: column c's str value is not well-formed UTF-8
-  if (ok && inreg) {
-    // output chunk 0 of the column starts at stream byte S (relative to the aligned sample start)
-    const int32_t S = int32_t(sa + rel) - int32_t(D & 15);
-    const bool near = S >= -16 && S < 32;
-    const bool via_lds = (kX & 4) ? false : small || (wide && !near);
-    if (__ballot(via_lds)) {
-      // the chunks those columns' bytes lie in, copied to the wave's LDS
-      const uint32_t lo = via_lds ? (sa + rel) >> 4 : 0xffffffffu;
-      const uint32_t hi = via_lds ? (sa + rel + (small ? rb : len) + 15u) >> 4 : 0u;
-      uint32_t jlo = lo, jhi = hi;
-      for (int o = 32; o > 0; o >>= 1) {
-        jlo = min(jlo, uint32_t(__shfl_xor(int(jlo), o)));
-        jhi = max(jhi, uint32_t(__shfl_xor(int(jhi), o)));
-      }
-      jlo = __builtin_amdgcn_readfirstlane(jlo);
-      jhi = __builtin_amdgcn_readfirstlane(jhi);
+  // output chunk 0 of the column starts at stream byte S (relative to the aligned sample start)
+  const int32_t S = int32_t(sa + rel) - int32_t(D & 15);
+  // (str values are checked for UTF-8 from LDS: the check beside the whole sample in registers
+  // would cost the kernel a wave per SIMD)
+  const bool near = S >= -16 && S < 32 && !str;
+  const bool via_lds = (kX & 4) ? false : small || (wide && !near);
+  const uint64_t lds_mask = __ballot(via_lds);
+  // the chunks the LDS columns' bytes lie in (columns lie in the sample in column order: from the
+  // first such column's first chunk to the last one's end); a wider span than the wave's LDS
+  // copy takes the huge-row kernel
+  uint32_t jlo = 0, jhi = 0;
+  if (lds_mask) {
+    const uint32_t lo = (sa + rel) >> 4;
+    const uint32_t hi = (sa + rel + (is_small ? rb : len) + 15u) >> 4;
+    jlo = uint32_t(__builtin_amdgcn_readlane(int(lo), __builtin_ctzll(lds_mask)));
+    jhi = uint32_t(__builtin_amdgcn_readlane(int(hi), 63 - __builtin_clzll(lds_mask)));
+  }
+  const bool fits = inreg && 16u * (jhi - jlo) <= a.sw_lds;  // wave-uniform
+  if (ok && fits) {
+    const uint64_t str_mask = __ballot(str), near_mask = __ballot(near);
+    // the columns from the registers, then (the registers free) the ones from LDS
+    for (uint64_t m = wide_mask & near_mask; m; m &= m - 1) {
+      const int c = __builtin_ctzll(m);  // wave-uniform
+      sw_copy<kNT, U, true, kX>(L, buf, readlane64(D, c),
+                                uint32_t(__builtin_amdgcn_readlane(int(len), c)),
+                                __builtin_amdgcn_readlane(S, c), false, lane);
+    }
+    // the LDS copy: stream chunk k at LDS byte kSwPad + 16 (k - jlo)
+    const lds_u8* const base = buf - 16 * int32_t(jlo);
+    if (lds_mask) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (64u * uint32_t(u) >= jhi || 64u * uint32_t(u) + 64u <= jlo) continue;  // uniform
         const uint32_t k = 64u * uint32_t(u) + uint32_t(lane);
         if (k >= jlo && k < jhi)
-          *(MDSX_L u32x4*)(smem + kSwPad + 16u * k) = u32x4{L[u].x, L[u].y, L[u].z, L[u].w};
+          *(MDSX_L u32x4*)(smem + kSwPad + 16u * (k - jlo)) =
+              u32x4{L[u].x, L[u].y, L[u].z, L[u].w};
       }
-      if (small) small_store(reinterpret_cast<uint8_t*>(D), lds16(buf + (sa + rel)), rb);
+      if (small) small_store(reinterpret_cast<uint8_t*>(D), lds16(base + (sa + rel)), rb);
     }
-    const uint64_t str_mask = __ballot(str), near_mask = __ballot(near);
-    for (uint64_t m = (kX & 4) ? wide_mask & near_mask : wide_mask; m; m &= m - 1) {
-      const int c = __builtin_ctzll(m);  // wave-uniform, in column order
-      const bool bad = sw_copy<kNT, U, kX>(L, buf, readlane64(D, c),
-                                       uint32_t(__builtin_amdgcn_readlane(int(len), c)),
-                                       __builtin_amdgcn_readlane(S, c), (near_mask >> c) & 1ull,
-                                       (str_mask >> c) & 1ull, lane);
-      if (bad) badm |= 1ull << c;
+    for (uint64_t m = (kX & 4) ? 0ull : wide_mask & ~near_mask; m; m &= m - 1) {
+      const int c = __builtin_ctzll(m);  // wave-uniform
+      if (sw_copy<kNT, U, false, kX>(L, base, readlane64(D, c),
+                                     uint32_t(__builtin_amdgcn_readlane(int(len), c)),
+                                     __builtin_amdgcn_readlane(S, c), (str_mask >> c) & 1ull, lane))
+        badm |= 1ull << c;
     }
   } else if (ok && lane == 0) {
-    // a sample past the register window: listed for stage_huge_kernel (every column straight
+    // a sample past the register window (or its LDS copy): listed for stage_huge_kernel (every column straight
     // from HBM, after this launch; it reads the final offsets written below)
     uint32_t* count = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(a.status) +
                                                   kHugeCountOffset);
-    a.src_abs[atomicAdd(count, 1u)] = (uint64_t(tile) << 32) | t;
+    a.src_abs[atomicAdd(count, 1u)] = (uint64_t(tile) << 32) | (blk & uint32_t(a.tile_rows - 1));
   }
   const uint32_t t_copied = (kX & 8) ? uint32_t(sw_clock() - t_start) : 0u;
-  // ---- the row's ragged offsets and str flags
-  if (vi >= 0) {
-    *gp(offp + row) = off;
-    if (flp) *gp(flp + row) = uint8_t((badm >> lane) & 1ull);
+  // ---- the row's str flags (the pointers read again from the kernel arguments)
+  for (int c = 0; c < ncols; ++c) {  // uniform
+    uint8_t* const fl = a.cols[c].flags;
+    if (a.cols[c].var_index >= 0 && fl != nullptr && lane == 0)
+      *gp(fl + row) = uint8_t((badm >> c) & 1ull);
   }
   if constexpr ((kX & 8) != 0) {
     if (lane < 4) {
@@ -287,12 +300,6 @@ __global__ __launch_bounds__(64, kOcc > 0 ? kOcc : 1) void swave_decode_kernel(c
                                                                           : uint32_t(sw_clock() - t_start);
       *gp(reinterpret_cast<uint32_t*>(a.src_abs) + 4ull * row + lane) = st;
     }
-  }
-  // the shard header (mds/writer.py:133-144): u32 N, then N + 1 offsets
-  if (first && lane == 0) {
-    const uint32_t n = *reinterpret_cast<const uint32_t*>(v.shard);
-    if (n != v.d.samples || v.offs[0] < v.hdr_end || v.offs[v.d.samples] > v.d.bytes)
-      report_decode(a, MDSX_E_HEADER, int(v.shard_idx), -1, -1);
   }
 }
 
@@ -309,7 +316,9 @@ int launch_swave_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) 
   if (zc != MDSX_OK) return zc;
   const int U = plan->swave_kb, occ = plan->swave_occ;
   const bool nt = plan->run_nt != 0;
-  const size_t lds = size_t(U) * 1024 + 2 * kSwPad + size_t(plan->lds_pad_kb) * 1024;
+  DevArgs b = a;
+  b.sw_lds = uint32_t(plan->swave_lds);
+  const size_t lds = size_t(b.sw_lds) + 2 * kSwPad + size_t(plan->lds_pad_kb) * 1024;
 #define MDSX_SWAVE(NT, UU, OCC)                                                                  \
   if (nt == NT && U == UU && occ == OCC) {                                                       \
     const void* fn = reinterpret_cast<const void*>(swave_decode_kernel<NT, UU, OCC>);            \
@@ -319,7 +328,7 @@ int launch_swave_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) 
       return mdsx::fail(MDSX_E_HIP, "mdsx: swave_decode_kernel LDS attribute");                 \
     mdsx::set_last_kernel("swave_decode_kernel<" #NT ", " #UU ", " #OCC ">");                    \
     hipLaunchKernelGGL((swave_decode_kernel<NT, UU, OCC>), dim3(unsigned(waves)), dim3(64), lds, \
-                       s, a);                                                                    \
+                       s, b);                                                                    \
     const int rc = hip_check(hipGetLastError(), "swave_decode_kernel launch");                   \
     return rc != MDSX_OK ? rc : launch_huge_rows(a, NT, s);                                      \
   }
@@ -332,7 +341,7 @@ int launch_swave_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) 
   if (plan->swave_x == X) {                                                                      \
     mdsx::set_last_kernel("swave_decode_kernel<true, 6, 0, " #X ">");                            \
     hipLaunchKernelGGL((swave_decode_kernel<true, 6, 0, X>), dim3(unsigned(waves)), dim3(64),     \
-                       lds, s, a);                                                               \
+                       lds, s, b);                                                               \
     const int rc = hip_check(hipGetLastError(), "swave_decode_kernel launch");                   \
     return rc != MDSX_OK ? rc : launch_huge_rows(a, true, s);                                    \
   }
@@ -343,7 +352,6 @@ int launch_swave_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) 
   }
   MDSX_SWAVE(true, 6, 0)
   MDSX_SWAVE(true, 6, 4)
-  MDSX_SWAVE(true, 6, 5)
   MDSX_SWAVE(true, 6, 6)
   MDSX_SWAVE(true, 4, 0)
   MDSX_SWAVE(true, 4, 6)
@@ -352,7 +360,7 @@ int launch_swave_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) 
   MDSX_SWAVE(false, 6, 0)
 #undef MDSX_SWAVE
   return mdsx::fail(MDSX_E_ARG,
-                    "mdsx: swave: (nt, KiB, occupancy) of (1, 6, 0/4/5/6), (1, 4, 0/6), (1, 8, 0/4), "
+                    "mdsx: swave: (nt, KiB, occupancy) of (1, 6, 0/4/6), (1, 4, 0/6), (1, 8, 0/4), "
                     "(0, 6, 0)");
 }
 

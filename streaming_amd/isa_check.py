@@ -24,6 +24,12 @@ literals over the full mask (the empty conjunction is the full mask):
 A readlane is flagged unless exec is certainly full there. Exempt: a readlane whose lane comes
 from `s_ff1_i32_b64` in the same block (the compiler's loop over the active lanes of a wave
 reduction: that lane is active).
+
+Second rule (reload taint): a VGPR reloaded from scratch (`scratch_load_*`) where exec may be
+partial holds stale bits in the lanes that were inactive, until the next write of the register;
+any cross-lane read of it meanwhile -- readlane / readfirstlane, a DPP move, ds_(b)permute's data,
+permlane -- is flagged, whatever exec is at the read (a readfirstlane under a partial mask and the
+s_ff1 readlane read a lane active now: exempt).
 usage: python -m streaming_amd.isa_check <device object or objdump text> [kernel substring]"""
 import re
 import subprocess
@@ -183,19 +189,22 @@ def m_meet(a, b):
 
 
 class State:
-    """exec, SGPR halves ({sgpr: (mask, half)}), spill slots ({(vgpr, lane): (mask, half)}). A
-    loop's exit accumulator holds ('acc', exec before the loop)."""
+    """exec, SGPR halves ({sgpr: (mask, half)}), spill slots ({(vgpr, lane): (mask, half)}), and
+    the VGPRs reloaded from scratch where exec may have been partial (``taint``: their inactive
+    lanes hold stale bits until a full-exec write). A loop's exit accumulator holds ('acc', exec
+    before the loop)."""
 
-    def __init__(self, ex=FULL, sg=None, slots=None):
+    def __init__(self, ex=FULL, sg=None, slots=None, taint=frozenset()):
         self.ex, self.sg = ex, dict(sg or {})
         self.slots = dict(slots or {})
+        self.taint = frozenset(taint)
 
     def key(self):
         return (self.ex, tuple(sorted(self.sg.items(), key=str)),
-                tuple(sorted(self.slots.items(), key=str)))
+                tuple(sorted(self.slots.items(), key=str)), tuple(sorted(self.taint)))
 
     def copy(self):
-        return State(self.ex, self.sg, self.slots)
+        return State(self.ex, self.sg, self.slots, self.taint)
 
     def val(self, op_str):
         if op_str == 'exec':
@@ -245,10 +254,53 @@ def _meet_halves(x, y):
 def meet_states(a, b):
     if a is None:
         return b.copy()
-    out = State(m_meet(a.ex, b.ex))
+    out = State(m_meet(a.ex, b.ex), taint=a.taint | b.taint)
     out.sg = _meet_halves(a.sg, b.sg)
     out.slots = _meet_halves(a.slots, b.slots)
     return out
+
+
+def vregs(op_str):
+    """The VGPR numbers an operand names (v7, v[8:9]), or ()."""
+    m = re.match(r'v\[(\d+):(\d+)\]$', op_str)
+    if m:
+        return tuple(range(int(m.group(1)), int(m.group(2)) + 1))
+    m = re.match(r'v(\d+)$', op_str)
+    return (int(m.group(1)),) if m else ()
+
+
+_DPP = ('row_shr', 'row_shl', 'row_ror', 'wave_shl', 'wave_shr', 'wave_rol', 'wave_ror',
+        'row_bcast', 'quad_perm', 'row_mirror', 'row_half_mirror', 'row_share', 'row_xmask')
+
+
+def cross_lane_sources(op, args):
+    """The VGPRs an instruction reads from lanes other than the lane it writes (or from one
+    chosen lane): readlane / readfirstlane, DPP moves, ds_(b)permute's data, permlane."""
+    if op.startswith(('v_readlane', 'v_readfirstlane')) and len(args) >= 2:
+        return vregs(args[1])
+    if op.startswith(('ds_bpermute', 'ds_permute')) and len(args) >= 3:
+        return vregs(args[2])
+    if op.startswith('v_permlane'):
+        return tuple(r for a in args for r in vregs(a))
+    if op.startswith('v_') and any(a.startswith(_DPP) for a in args):
+        return tuple(r for a in args[1:] for r in vregs(a))
+    return ()
+
+
+def taint_step(st, op, args):
+    """The reload taint of one instruction: a scratch load under a possibly partial exec taints
+    the VGPRs it writes; any write with every lane active clears them."""
+    if not args:
+        return
+    dest = vregs(args[0])
+    if not dest or op.startswith(('v_cmp', 'v_readlane', 'v_readfirstlane', 'v_writelane')):
+        return
+    if op.startswith('scratch_load') or (op.startswith('buffer_load') and 'off' in args):
+        st.taint = (st.taint - set(dest)) if st.ex == FULL else (st.taint | set(dest))
+    elif op.startswith(('v_', 'global_load', 'flat_load', 'ds_read', 'ds_bpermute', 'ds_permute',
+                        'buffer_load')):
+        # a new value of the register (defined in the lanes active now, as the source defines it)
+        st.taint = st.taint - set(dest)
 
 
 _NO_DEST = ('s_cmp', 's_bitcmp', 's_cbranch', 's_branch', 's_store', 's_buffer_store', 's_waitcnt',
@@ -370,6 +422,7 @@ def check(text, want='rows_decode_kernel'):
             s, e = bl[k]
             for addr, op, args in ins[s:e]:
                 step(st, addr, op, args)
+                taint_step(st, op, args)
             last_op = ins[e - 1][1]
             for n, kind in succ[k]:
                 out = st
@@ -391,14 +444,22 @@ def check(text, want='rows_decode_kernel'):
                 if op == 'v_readlane_b32' and len(args) >= 3 and re.match(r's\d+$', args[2]):
                     if st.ex != FULL and st.ex != EMPTY and args[2] not in ff1:
                         hits.append(addr)
+                # a lane of a register reloaded under a partial mask (readfirstlane under a partial
+                # mask, and readlane of the s_ff1 lane, read a lane active now, which was active at
+                # the nested reload)
+                active_lane = (op.startswith('v_readfirstlane') and st.ex != FULL) or (
+                    op == 'v_readlane_b32' and len(args) >= 3 and args[2] in ff1)
+                if st.taint and set(cross_lane_sources(op, args)) & st.taint and not active_lane:
+                    hits.append(addr)
                 dest = args[0] if args else None
                 if op.startswith('s_ff1_i32'):
                     ff1.add(dest)
                 elif dest in ff1 and not op.startswith(_NO_DEST):
                     ff1.discard(dest)
                 step(st, addr, op, args)
+                taint_step(st, op, args)
         if hits:
-            bad.append((name, sorted(hits)))
+            bad.append((name, sorted(set(hits))))
     return bad
 
 

@@ -22,6 +22,7 @@ PER_FILE = 24  # random samples per written shard
 def _workload(config):
     import bench
     from streaming_amd.decoder import BatchDecoder
+    # (the plan and the batch's tiles are made under the caller's MDSX_TUNE)
     shard_ids = list(range(bench.SHARDS_PER_GPU[config]))
     synth, _ = bench.build_workload(config, shard_ids)
     dec = BatchDecoder(synth.plan, synth.batch)
@@ -73,7 +74,12 @@ def test_config_b_full_size_vs_oracle(tmp_path):
             (tmp_path / info['raw_data']['basename']).unlink()
 
 
-def test_config_c_full_size_vs_oracle(tmp_path):
+# config C through both decodes of its sample sizes: the default and the other one (the lean
+# streaming decode / one sample per wave), each over the 4.3 GB batch (byte offsets past 2 and 4
+# GiB)
+@pytest.mark.parametrize('tune', ['', 'swave=1', 'swave=0'])
+def test_config_c_full_size_vs_oracle(tmp_path, monkeypatch, tune):
+    monkeypatch.setenv('MDSX_TUNE', tune)
     synth, out = _workload('C')
     b = synth.batch
     assert b.nshards == 64 and b.total_rows == 963_880

@@ -182,3 +182,25 @@ def test_built_checked_kernels_pass():
         for w in want:
             assert w in text, (src, w)
             assert isa_check.check(text, w) == [], (src, w)
+
+
+def test_flags_cross_lane_read_of_a_partial_reload():
+    """A VGPR reloaded from scratch under a partial exec mask holds stale bits in its inactive
+    lanes: a later cross-lane read of it -- readlane, DPP, ds_bpermute -- is flagged even with
+    every lane active; a full-exec write (or a new value) clears it."""
+    def body(read):
+        return ['v_cmp_gt_u32_e32 vcc, s36, v0', 's_and_saveexec_b64 s[2:3], vcc',
+                'scratch_load_dwordx2 v[6:7], off, off offset:4', 's_or_b64 exec, exec, s[2:3]',
+                read, 's_endpgm']
+    assert flagged(body('v_readlane_b32 s1, v6, 5')) == [0x1010]
+    assert flagged(body('v_mov_b32_dpp v9, v7 row_shr:1 row_mask:0xf bank_mask:0xf')) == [0x1010]
+    assert flagged(body('ds_bpermute_b32 v9, v8, v6')) == [0x1010]
+    assert flagged(body('v_readlane_b32 s1, v8, 5')) == []  # another register
+    cleared = body('v_readlane_b32 s1, v6, 5')
+    cleared.insert(4, 'v_mov_b32_e32 v6, 0')  # a full-exec write
+    assert flagged(cleared) == []
+    full = ['v_cmp_gt_u32_e32 vcc, s36, v0', 's_and_saveexec_b64 s[2:3], vcc', 's_nop 0',
+            's_or_b64 exec, exec, s[2:3]',  # the reload after the join sees every lane
+            'scratch_load_dwordx2 v[6:7], off, off offset:4', 'v_readlane_b32 s1, v6, 5',
+            's_endpgm']
+    assert flagged(full) == []
