@@ -249,7 +249,7 @@ void apply_tuning(mdsx_plan* p) {
       p->swave_kb = int(v);
     } else if (key == "swlds" && v >= 1 && v <= 8) {
       p->swave_lds = int(v) * 1024;
-    } else if (key == "swx" && v >= 0 && v <= 15) {
+    } else if (key == "swx" && v >= 0 && v <= 127) {
       p->swave_x = int(v);
     } else if (key == "swocc" && (v == 0 || v == 4 || v == 6)) {
       p->swave_occ = int(v);

@@ -117,7 +117,7 @@ __device__ __forceinline__ bool sw_copy(const uint4 (&L)[U], const lds_u8* buf, 
       const uint4 vout = keep_range(out, D, d0, dend);  // this value's bytes only
       const uint32_t any8 = (vout.x | vout.y | vout.z | vout.w) & 0x80808080u;
       if (__any(any8 != 0) || hi_c0(prev_w)) {  // a byte >= 0x80 (or a sequence open before)
-        uint32_t pw = uint32_t(__shfl_up(int(vout.w), 1));
+        uint32_t pw = dpp_mov<kDppWaveShr1>(vout.w);  // lane k - 1's last dword
         if (lane == 0) pw = prev_w;
         if (k < nch) bad |= utf8_chunk_bad(vout, pw, k == nch - 1);
       }
@@ -134,8 +134,10 @@ __device__ __forceinline__ uint64_t sw_clock() {
 }
 
 // kOcc: registers bounded for that many waves per SIMD (0: the compiler's choice).
-// kX (measurement only, MDSX_TUNE swx; bits 1-4 leave outputs incomplete): 1 no UTF-8 check, 2 no
-// partial edge chunk stored, 4 only the register-path columns written (none through LDS), 8
+// kX (measurement only, MDSX_TUNE swx; bits 1-4, 16, 32 leave outputs incomplete): 1 no UTF-8
+// check, 2 no partial edge chunk stored, 4 only the register-path columns written (none through
+// LDS), 16 no small fixed column stored, 32 no LDS-path column copied (the LDS copy made), 64 the
+// LDS-path columns stored with the default cache policy, 8
 // shader-clock stamps per sample into src_abs (u32 x 4 per row, cycles from the wave's start: its
 // offsets pair in, its loads landed -- an added vmcnt(0) wait --, its stores issued, its end).
 template <bool kNT, int U, int kOcc, int kX = 0>
@@ -171,6 +173,7 @@ __global__ __launch_bounds__(64, kOcc > 0 ? kOcc : 1) void swave_decode_kernel(c
   bool str = false;
   uint64_t data = 0, cap = 0;
   int64_t* offp = nullptr;
+  uint8_t* flp = nullptr;
   for (int c = 0; c < ncols; ++c) {  // uniform
     const DevCol& col = a.cols[c];
     const int cv = col.var_index;
@@ -178,8 +181,10 @@ __global__ __launch_bounds__(64, kOcc > 0 ? kOcc : 1) void swave_decode_kernel(c
     const bool cs = col.kind == MDSX_KIND_STR && col.flags != nullptr;
     const uint64_t cdata = reinterpret_cast<uint64_t>(col.data);
     int64_t* const coffs = col.offsets;
+    uint8_t* const cflags = col.flags;
     const uint64_t ccap = col.capacity;
-    if (lane == c) vi = cv, rb = crb, str = cs, data = cdata, offp = coffs, cap = ccap;
+    if (lane == c)
+      vi = cv, rb = crb, str = cs, data = cdata, offp = coffs, flp = cflags, cap = ccap;
   }
   int64_t off = 0;
   if (vi >= 0) off = a.tile_prefix[uint64_t(vi) * a.nscan + tile / a.scan_per] + offp[row];
@@ -271,11 +276,13 @@ __global__ __launch_bounds__(64, kOcc > 0 ? kOcc : 1) void swave_decode_kernel(c
           *(MDSX_L u32x4*)(smem + kSwPad + 16u * (k - jlo)) =
               u32x4{L[u].x, L[u].y, L[u].z, L[u].w};
       }
-      if (small) small_store(reinterpret_cast<uint8_t*>(D), lds16(base + (sa + rel)), rb);
+      if ((kX & 16) == 0 && small)
+        small_store(reinterpret_cast<uint8_t*>(D), lds16(base + (sa + rel)), rb);
     }
-    for (uint64_t m = (kX & 4) ? 0ull : wide_mask & ~near_mask; m; m &= m - 1) {
+    // (measurement, kX bit 64: these columns stored with the default cache policy)
+    for (uint64_t m = (kX & 36) ? 0ull : wide_mask & ~near_mask; m; m &= m - 1) {
       const int c = __builtin_ctzll(m);  // wave-uniform
-      if (sw_copy<kNT, U, false, kX>(L, base, readlane64(D, c),
+      if (sw_copy<kNT && (kX & 64) == 0, U, false, kX>(L, base, readlane64(D, c),
                                      uint32_t(__builtin_amdgcn_readlane(int(len), c)),
                                      __builtin_amdgcn_readlane(S, c), (str_mask >> c) & 1ull, lane))
         badm |= 1ull << c;
@@ -288,12 +295,8 @@ __global__ __launch_bounds__(64, kOcc > 0 ? kOcc : 1) void swave_decode_kernel(c
     a.src_abs[atomicAdd(count, 1u)] = (uint64_t(tile) << 32) | (blk & uint32_t(a.tile_rows - 1));
   }
   const uint32_t t_copied = (kX & 8) ? uint32_t(sw_clock() - t_start) : 0u;
-  // ---- the row's str flags (the pointers read again from the kernel arguments)
-  for (int c = 0; c < ncols; ++c) {  // uniform
-    uint8_t* const fl = a.cols[c].flags;
-    if (a.cols[c].var_index >= 0 && fl != nullptr && lane == 0)
-      *gp(fl + row) = uint8_t((badm >> c) & 1ull);
-  }
+  // ---- the row's str flags
+  if (vi >= 0 && flp) *gp(flp + row) = uint8_t((badm >> lane) & 1ull);
   if constexpr ((kX & 8) != 0) {
     if (lane < 4) {
       const uint32_t st = lane == 0 ? t_pair : lane == 1 ? t_loads : lane == 2 ? t_copied
@@ -346,7 +349,7 @@ int launch_swave_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) 
     return rc != MDSX_OK ? rc : launch_huge_rows(a, true, s);                                    \
   }
     MDSX_SWAVE_X(1) MDSX_SWAVE_X(2) MDSX_SWAVE_X(3) MDSX_SWAVE_X(4) MDSX_SWAVE_X(7)
-    MDSX_SWAVE_X(8)
+    MDSX_SWAVE_X(8) MDSX_SWAVE_X(16) MDSX_SWAVE_X(32) MDSX_SWAVE_X(48) MDSX_SWAVE_X(64)
 #undef MDSX_SWAVE_X
     return mdsx::fail(MDSX_E_ARG, "mdsx: swave variant out of range");
   }
