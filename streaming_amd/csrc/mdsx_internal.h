@@ -81,16 +81,18 @@ struct mdsx_plan {
                            // else 4)
   int rows_pipe = 0;       // row-parallel decode: tiles per workgroup, the next tile's DMA in
                            // flight while one is written (two stages; 0: one tile, one stage)
-  int swave = 0;           // ragged batches of the streaming decode's sample sizes: one sample per
-                           // one-wave workgroup, in registers, instead (mdsx_swave.hip)
+  int swave = -1;          // ragged batches of the streaming decode's sample sizes: one sample per
+                           // one-wave workgroup, in registers, instead (mdsx_swave.hip; -1: when
+                           // the samples average <= 4/5 of its register window, +3 % on config C,
+                           // profiles/r06/swave/; 1: always; 0: never, MDSX_TUNE swave)
   int swave_kb = 6;        // ... KiB of a sample held in registers (4, 6 or 8; larger samples are
                            // copied straight from HBM)
   int swave_occ = 0;       // ... waves per SIMD its registers are bounded for (0: the compiler's;
                            // bounds that make it spill are not built: build.py refuses scratch)
-  int swave_tile = 64;
+  int swave_tile = 64;     // ... rows per tile (the scan pass's unit: 256 / this tiles per block)
   int swave_lds = 2048;    // ... bytes of its per-wave LDS copy of the columns past the first (a
                            // sample whose later columns span more takes the huge-row kernel)
-  int swave_x = 0;         // ... measurement variants (MDSX_TUNE swx, bits; mdsx_swave.hip)     // ... rows per tile (the scan pass's unit: 256 / this tiles per block)
+  int swave_x = 0;         // ... measurement variants (MDSX_TUNE swx, bits; mdsx_swave.hip)
   int gather_chunks = 2;  // 16-byte chunks per lane in the ragged gather (tile = 4 KiB x this)
   int gather_min = 256;   // ragged columns averaging fewer bytes per row use the gather kernel
   int group_max = 1024;   // ... fewer than this (and >= gather_min): four rows per wave
@@ -109,7 +111,8 @@ inline bool use_run_decode(const mdsx_plan* p, uint64_t bytes, uint64_t rows) {
 
 // Whether such a batch decodes one sample per wave instead (mdsx_swave.hip).
 inline bool use_swave_decode(const mdsx_plan* p, uint64_t bytes, uint64_t rows) {
-  return p->swave != 0 && use_run_decode(p, bytes, rows);
+  if (p->swave == 0 || !use_run_decode(p, bytes, rows)) return false;
+  return p->swave > 0 || bytes / rows <= uint64_t(p->swave_kb) * 1024 * 4 / 5;
 }
 
 // Whether a ragged batch of shorter samples decodes through the row-parallel decode

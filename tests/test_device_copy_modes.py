@@ -32,28 +32,32 @@ pytestmark = pytest.mark.gpu
 
 MODES = {
     'default': '',
-    'run': 'run=8,rmin=0',  # the streaming decode (mdsx_run.hip) whatever the sample size
-    'run4': 'run=4,rmin=0,rkb=4',  # small ring, 1-2-row tiles
-    'run16': 'run=16,rmin=0,rkb=1024',  # 32-row tiles
+    # the streaming decode's modes below pin swave=0: by default batches whose samples fit the
+    # one-sample-per-wave register window decode there (mdsx_swave.hip, modes swave*)
+    'seg_default': 'swave=0',  # the round-5 default for long samples (seg_decode_kernel<7,..>)
+    'run': 'run=8,rmin=0,swave=0',  # the streaming decode (mdsx_run.hip) whatever the sample size
+    'run4': 'run=4,rmin=0,rkb=4,swave=0',  # small ring, 1-2-row tiles
+    'run16': 'run=16,rmin=0,rkb=1024,swave=0',  # 32-row tiles
     # the streaming decode's lean path (seg_decode_kernel) for runs whose samples fit its ring,
     # the general path for the others, in the same launch
-    'seg4': 'run=4,seg=1,rmin=0,rkb=4',
-    'seg8': 'run=8,seg=1,rmin=0',
-    'seg7': 'run=7,seg=1,rmin=0',  # a 7 KiB ring (not a power of two: modulo addressing)
-    'seg7_touch': 'run=7,seg=1,rmin=0,rnt=1,sv=32',  # ... the run's lines past the ring touched
-    'seg7_edge': 'run=7,seg=1,rmin=0,rnt=1,sv=128',  # ... shared boundary lines: default policy
-    'run7': 'run=7,rmin=0',  # ... the general path through it
-    'seg16': 'run=16,seg=1,rmin=0,rkb=1024',
-    'seg8_nt': 'run=8,seg=1,rmin=0,rnt=1',
-    'seg16_64k': 'run=16,seg=1,rmin=0,rkb=64',
-    'seg8_wg1': 'run=8,seg=1,rmin=0,swg=1',  # one wave (run) per workgroup
-    'seg8_wg4': 'run=8,seg=1,rmin=0,swg=4',  # four (the default is two)
-    'seg8_xcd0': 'run=8,seg=1,rmin=0,xcd=0',  # runs in launch order (default: XCD-contiguous ranges)
+    'seg4': 'run=4,seg=1,rmin=0,rkb=4,swave=0',
+    'seg8': 'run=8,seg=1,rmin=0,swave=0',
+    'seg7': 'run=7,seg=1,rmin=0,swave=0',  # a 7 KiB ring (not a power of two: modulo addressing)
+    # ... the run's lines past the ring touched; shared boundary lines with the default policy
+    'seg7_touch': 'run=7,seg=1,rmin=0,rnt=1,sv=32,swave=0',
+    'seg7_edge': 'run=7,seg=1,rmin=0,rnt=1,sv=128,swave=0',
+    'run7': 'run=7,rmin=0,swave=0',  # ... the general path through it
+    'seg16': 'run=16,seg=1,rmin=0,rkb=1024,swave=0',
+    'seg8_nt': 'run=8,seg=1,rmin=0,rnt=1,swave=0',
+    'seg16_64k': 'run=16,seg=1,rmin=0,rkb=64,swave=0',
+    'seg8_wg1': 'run=8,seg=1,rmin=0,swg=1,swave=0',  # one wave (run) per workgroup
+    'seg8_wg4': 'run=8,seg=1,rmin=0,swg=4,swave=0',  # four (the default is two)
+    'seg8_xcd0': 'run=8,seg=1,rmin=0,xcd=0,swave=0',  # runs in launch order (default: by XCD)
     # the lean path's measured variants (mdsx_run.hip kV): early prologue, per-step slot release,
     # per-step waits
-    'seg7_v1': 'run=7,seg=1,rmin=0,sv=1',
-    'seg7_v3': 'run=7,seg=1,rmin=0,sv=3',
-    'seg7_v7': 'run=7,seg=1,rmin=0,sv=7',
+    'seg7_v1': 'run=7,seg=1,rmin=0,sv=1,swave=0',
+    'seg7_v3': 'run=7,seg=1,rmin=0,sv=3,swave=0',
+    'seg7_v7': 'run=7,seg=1,rmin=0,sv=7,swave=0',
     # one sample per one-wave workgroup, the sample in registers (mdsx_swave.hip), for every
     # sample size: the default 6 KiB window (larger samples straight from HBM), 4 KiB, a 1-row
     # tile, launch order, temporal loads / stores, registers bounded for 4 / 6 waves per SIMD

@@ -77,7 +77,7 @@ def test_config_b_full_size_vs_oracle(tmp_path):
 # config C through both decodes of its sample sizes: the default and the other one (the lean
 # streaming decode / one sample per wave), each over the 4.3 GB batch (byte offsets past 2 and 4
 # GiB)
-@pytest.mark.parametrize('tune', ['', 'swave=1', 'swave=0'])
+@pytest.mark.parametrize('tune', ['', 'swave=0'])  # default: one sample per wave
 def test_config_c_full_size_vs_oracle(tmp_path, monkeypatch, tune):
     monkeypatch.setenv('MDSX_TUNE', tune)
     synth, out = _workload('C')

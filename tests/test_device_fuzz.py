@@ -23,15 +23,16 @@ pytestmark = pytest.mark.gpu
 START = int(os.environ.get('MDSX_FUZZ_START', '1000'))
 SEEDS = int(os.environ.get('MDSX_FUZZ_SEEDS', '6'))
 MODES = {
-    'default': '',
-    'run': 'run=4,rmin=0,rkb=8',  # the streaming decode whatever the sample size
-    'seg': 'run=4,seg=1,rmin=0,rkb=8',  # ... its lean path where a sample fits the 4 KiB ring
-    'seg16': 'run=16,seg=1,rmin=0,rkb=64',
-    'seg7': 'run=7,seg=1,rmin=0,rkb=12',  # a ring of 7 slots (modulo addressing)
-    'seg7_v7': 'run=7,seg=1,rmin=0,rkb=12,sv=7',  # ... its early prologue, per-step release / waits
-    'seg7_edge': 'run=7,seg=1,rmin=0,rkb=12,sv=128',  # ... boundary lines, default policy
-    'seg7_v3': 'run=7,seg=1,rmin=0,sv=3',  # ... early prologue and per-step release, 2-sample runs
-    'seg_wg4': 'run=8,seg=1,rmin=0,swg=4',  # four waves per workgroup (the default is two)
+    'default': '',  # long samples: one per wave (mdsx_swave.hip); streaming modes pin swave=0
+    'seg_default': 'swave=0',
+    'run': 'run=4,rmin=0,rkb=8,swave=0',  # the streaming decode whatever the sample size
+    'seg': 'run=4,seg=1,rmin=0,rkb=8,swave=0',  # ... its lean path where a sample fits the ring
+    'seg16': 'run=16,seg=1,rmin=0,rkb=64,swave=0',
+    'seg7': 'run=7,seg=1,rmin=0,rkb=12,swave=0',  # a ring of 7 slots (modulo addressing)
+    'seg7_v7': 'run=7,seg=1,rmin=0,rkb=12,sv=7,swave=0',  # early prologue, per-step release / waits
+    'seg7_edge': 'run=7,seg=1,rmin=0,rkb=12,sv=128,swave=0',  # ... boundary lines, default policy
+    'seg7_v3': 'run=7,seg=1,rmin=0,sv=3,swave=0',  # ... and per-step release, 2-sample runs
+    'seg_wg4': 'run=8,seg=1,rmin=0,swg=4,swave=0',  # four waves per workgroup (the default is two)
     'swave': 'swave=1,rmin=0',  # one sample per wave, in registers (larger ones from HBM)
     'swave4': 'swave=1,rmin=0,swkb=4,swtile=2',
     'rows_small': 'rows=2,rmin=1000000000',  # row-parallel, 2 KiB stage (windows, huge rows)

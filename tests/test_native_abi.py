@@ -122,8 +122,9 @@ def test_too_many_columns():
 
 
 def test_tile_rows_for_sizes_ragged_tiles_to_the_decode(monkeypatch):
-    """Ragged plans: batches of long samples (>= 3 KiB on average) go to the streaming decode,
-    whose tiles hold 16-32 KiB of samples (1..32 rows); shorter samples to the row-parallel
+    """Ragged plans: batches of long samples (>= 3 KiB on average) decode one sample per wave
+    (64-row scan tiles) while they average <= 4/5 of its 6 KiB register window, else go to the
+    streaming decode, whose tiles hold 16-32 KiB of samples (1..32 rows); shorter samples to the row-parallel
     decode, whose tiles fill at most 8/9 of a 20 KiB (samples < 512 B) or 40 KiB stage (1..256
     rows, the workgroup's LDS within 160 KiB); the register decode and all-fixed plans: the plan's
     tile size whatever the batch."""
@@ -134,19 +135,22 @@ def test_tile_rows_for_sizes_ragged_tiles_to_the_decode(monkeypatch):
     assert c.tile_rows_for(1 << 26, (1 << 26) // 250) == 64
     assert c.tile_rows_for(1 << 26, (1 << 26) // 1000) == 32
     assert c.tile_rows_for(1 << 26, (1 << 26) // 2000) == 16
-    assert c.tile_rows_for(1 << 26, 15_700) == 2  # ~4.3 KB samples: streaming, 2-row runs
+    assert c.tile_rows_for(1 << 26, 15_700) == 64  # ~4.3 KB samples: one per wave, 64-row scan
+    assert c.tile_rows_for(1 << 26, 12_000) == 2  # ~5.6 KB: past 4/5 of the window, streaming
     assert c.tile_rows_for(1 << 26, (1 << 26) // 2048) == 16
     assert c.tile_rows_for(1 << 26, 10) == 1  # 6.7 MB samples: one per tile
     wide = Plan([f'c{i:02d}' for i in range(64)], ['str'] * 64, [None] * 64)
     assert wide.tile_rows_for(1 << 26, 1 << 20) == 64  # 64 columns: the tables bound the tile
     monkeypatch.setenv('MDSX_TUNE', 'rows=18')
     assert Plan(['b'], ['bytes'], [None]).tile_rows_for(1 << 26, (1 << 26) // 100) == 128
-    monkeypatch.setenv('MDSX_TUNE', 'swave=1')  # one sample per wave: the scan pass's tiles
-    assert Plan(['b'], ['bytes'], [None]).tile_rows_for(1 << 26, 15_700) == 64
+    monkeypatch.setenv('MDSX_TUNE', 'swave=0')  # never one sample per wave: 2-row runs
+    assert Plan(['b'], ['bytes'], [None]).tile_rows_for(1 << 26, 15_700) == 2
+    monkeypatch.setenv('MDSX_TUNE', 'swave=1')  # always, whatever the sample size
+    assert Plan(['b'], ['bytes'], [None]).tile_rows_for(1 << 26, 12_000) == 64
     assert Plan(['b'], ['bytes'], [None]).tile_rows_for(1 << 26, (1 << 26) // 100) == 128
     monkeypatch.setenv('MDSX_TUNE', 'swave=1,swtile=256')
     assert Plan(['b'], ['bytes'], [None]).tile_rows_for(1 << 26, 15_700) == 256
-    monkeypatch.setenv('MDSX_TUNE', 'run=4,rkb=256')
+    monkeypatch.setenv('MDSX_TUNE', 'run=4,rkb=256,swave=0')
     assert Plan(['b'], ['bytes'], [None]).tile_rows_for(1 << 26, 15_700) == 32
     monkeypatch.setenv('MDSX_TUNE', 'run=0,rows=0')  # the register decode: the plan's tiles
     c = Plan(['b', 'n', 's'], ['bytes', 'int', 'str'], [None, 8, None])
