@@ -7,13 +7,15 @@
 // value (encodings.py:62-81: bytes / str; 84-94: int; 270-397: ndarray and scalars).
 //
 // Here a wave takes one sample -- the same unit -- with nothing staged ahead of it:
-//   * pass 1 is the register decode's scan (scan_tiles_kernel + the chunk scans): each row's
-//     ragged bytes, scanned into scan-block-local offsets (left in the offsets outputs) and
-//     scan-block bases (tile_prefix). So every wave knows where its sample's ragged values go
-//     before it has read a byte of the sample;
-//   * the wave requests, together: its offsets pair (mds/reader.py:137-142), the output positions
-//     of its ragged columns, then its size heads (lane v: head v) and the whole sample as aligned
-//     16-byte chunks held in registers (lane k: chunk k of every 1 KiB step; up to U KiB);
+//   * pass 1 is the register decode's scan (scan_tiles_kernel<true> + the chunk scans): each
+//     row's ragged bytes, scanned into scan-block-local offsets (left in the offsets outputs) and
+//     scan-block bases (tile_prefix); it also checks each row's offsets pair against the file
+//     (mds/reader.py:137-142) and leaves one 16-byte record per sample slot: the sample's first
+//     byte in the batch, its size (or idle / bad), its shard and output row. So every wave knows
+//     where its sample is and where its ragged values go before it has read a byte of the sample;
+//   * the wave requests, together: its record (one load), then the output positions of its ragged
+//     columns, its size heads (lane v: head v) and the whole sample as aligned 16-byte chunks held
+//     in registers (lane k: chunk k of every 1 KiB step; up to U KiB);
 //   * lane-parallel geometry: lane c takes column c's length (its head, or the fixed size), a
 //     wave prefix sum places it in the sample, one ballot checks the boundaries
 //     (mds/reader.py:111-125);
@@ -137,9 +139,9 @@ __device__ __forceinline__ uint64_t sw_clock() {
 // kX (measurement only, MDSX_TUNE swx; bits 1-4, 16, 32 leave outputs incomplete): 1 no UTF-8
 // check, 2 no partial edge chunk stored, 4 only the register-path columns written (none through
 // LDS), 16 no small fixed column stored, 32 no LDS-path column copied (the LDS copy made), 64 the
-// LDS-path columns stored with the default cache policy, 8
-// shader-clock stamps per sample into src_abs (u32 x 4 per row, cycles from the wave's start: its
-// offsets pair in, its loads landed -- an added vmcnt(0) wait --, its stores issued, its end).
+// LDS-path columns stored with the default cache policy, 8 shader-clock stamps per sample into
+// src_abs (u32 x 4 per row, cycles from the wave's start: its record in, its loads landed -- an
+// added vmcnt(0) wait --, its stores issued, its end).
 template <bool kNT, int U, int kOcc, int kX = 0>
 __global__ __launch_bounds__(64, kOcc > 0 ? kOcc : 1) void swave_decode_kernel(const DevArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -288,8 +290,8 @@ __global__ __launch_bounds__(64, kOcc > 0 ? kOcc : 1) void swave_decode_kernel(c
         badm |= 1ull << c;
     }
   } else if (ok && lane == 0) {
-    // a sample past the register window (or its LDS copy): listed for stage_huge_kernel (every column straight
-    // from HBM, after this launch; it reads the final offsets written below)
+    // a sample past the register window (or its LDS copy): listed for stage_huge_kernel (every
+    // column straight from HBM, after this launch; it reads the final offsets written above)
     uint32_t* count = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(a.status) +
                                                   kHugeCountOffset);
     a.src_abs[atomicAdd(count, 1u)] = (uint64_t(tile) << 32) | (blk & uint32_t(a.tile_rows - 1));

@@ -385,6 +385,45 @@ class MDSReader(JointReader):
                 f'Relative sample index {idx} is not present in the {self.raw_data.basename} file.')
         return data
 
+    def _row_fits(self, idx: int) -> bool:
+        """Whether sample ``idx`` passes the whole-shard decode's per-sample checks (decode_kernel,
+        swave_decode_kernel): its offsets pair inside the file after the offsets table, its u32
+        size heads and every column inside the sample (bytes after the last column allowed)."""
+        size = os.stat(self._filename()).st_size
+        with open(self._filename(), 'rb', 0) as fp:
+            fp.seek((1 + idx) * 4)
+            begin, end = (int(x) for x in np.frombuffer(fp.read(8), np.uint32))
+            if not (4 + 4 * (self.samples + 1) <= begin <= end <= size):
+                return False
+            fp.seek(begin)
+            data = fp.read(end - begin)
+        need, pos = 0, 0
+        for size_ in self.column_sizes:
+            if size_:
+                need += int(size_)
+            else:
+                if pos + 4 > len(data):
+                    return False
+                need += 4 + int(np.frombuffer(data[pos:pos + 4], np.uint32)[0])
+                pos += 4
+        return 0 < need <= len(data)
+
+    def _check_row(self, entry: _Decoded, idx: int) -> None:
+        """The batch path (``order.DeviceSampleGather``) on a shard whose decode reported an
+        error: raise only if sample ``idx`` is one the decode refused (the reference raises only
+        when a bad sample is read, mds/reader.py:145-148) -- the reference's own exception for it
+        where the reference raises one (``get_item`` reproduces it), else ValueError: the batch
+        path does not hand out the clipped values the reference would. A
+        shard-level (header) error raises for every sample."""
+        st = entry.status
+        if st.code not in (_native.MDSX_E_EMPTY, _native.MDSX_E_BOUNDS):
+            raise _status_error(st, self.plan)
+        if self._row_fits(idx):
+            return
+        self.get_item(idx)  # raises what the reference raises for this sample, if anything
+        raise ValueError(f'MDS sample {idx} of {self.raw_data.basename} does not fit its layout '
+                         '(the reference would hand out clipped values; the batch path refuses).')
+
     def _materialize(self, host: _HostShard, idx: int) -> dict[str, Any]:
         getters = host.getters
         if getters is None:

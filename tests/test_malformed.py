@@ -95,3 +95,24 @@ def test_decode_sample_equals_reference_slices():
         for cut in range(len(data) + 1):
             assert _outcome(lambda _: r.decode_sample(data[:cut]), 0) == \
                 _outcome(lambda _: o.decode_sample(data[:cut]), 0), (i, cut)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case', CASES)
+def test_device_batches_raise_only_for_refused_samples(case):
+    """The batch path (iter_batches: a device gather of the decoded shard) on a malformed shard:
+    a sample the reference raises for raises the same exception type; a sample the reference
+    clips raises ValueError (the batch path hands out no clipped values) unless the decode took it
+    whole (junk after it); every other sample is served."""
+    from streaming_amd import LocalDataset
+    ds = LocalDataset(os.path.join(HERE, case), decoded_cache_bytes=1 << 20)
+    served = 0
+    for i, want in enumerate(OUTCOMES[case]):
+        got = _outcome(lambda j: next(iter(ds.iter_batches([j], 1))) and {}, i)
+        if 'exc' in want:
+            assert got == {'exc': want['exc']}, (case, i)
+        elif 'exc' in got:
+            assert case not in CLEAN and got == {'exc': 'ValueError'}, (case, i, got)
+        else:
+            served += 1
+    assert served >= (len(OUTCOMES[case]) if case in CLEAN else 1), case
