@@ -16,7 +16,6 @@ import torch
 
 import streaming_amd.decoder as D
 import streaming_amd.local
-import streaming_amd.reader
 import tests.test_device_copy_modes as copy_modes
 import tests.test_device_decode as device_decode
 from streaming_amd.decoder import BatchDecoder, Plan, RaggedColumn, decode_batch, stage_shards
@@ -49,7 +48,7 @@ def _single(plan, batch, check=True, single=True):
 def _single_pass(monkeypatch):
     if not torch.cuda.is_available():
         pytest.fail('GPU tests need an MI355X (torch.cuda.is_available() is False)')
-    for mod in (D, streaming_amd.local, streaming_amd.reader, device_decode, copy_modes):
+    for mod in (D, streaming_amd.local, device_decode, copy_modes):
         monkeypatch.setattr(mod, 'decode_batch', _single)
 
 
