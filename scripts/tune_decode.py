@@ -192,26 +192,6 @@ def main():
             phases[v]['median'] = [round(x) for x in raw.median(dim=0).values.tolist()]
             phases[v]['p90'] = [round(x) for x in raw.quantile(0.9, dim=0).tolist()]
             phases[v]['waves'] = rows
-        elif dbg and dbg[0] & 512 and 'runit=' in v:  # the row decode's unit form: per unit
-            dec.run()
-            torch.cuda.synchronize()
-            ntile = int(dec.batch.tile_shard.numel())
-            g = 4 if 'runit=4' in v else 1
-            units = (ntile + g - 1) // g
-            off = src_abs_offset(dec.plan.num_var, ntile, int(dec.batch.buffer.numel()))
-            raw = dec.workspace[off:off + 64 * units].cpu().view(torch.int64).view(units, 8)
-            raw = raw.double()
-            dur = raw[:, 3] - raw[:, 4]
-            cols = {'prologue': raw[:, 0], 'lookback_rounds': raw[:, 1],
-                    'lookback_cycles': raw[:, 2], 'unit_cycles': dur}
-            phases[v] = {k: {'mean': round(float(x.mean()), 1), 'median': round(float(x.median()), 1),
-                             'p90': round(float(x.quantile(0.9)), 1), 'max': round(float(x.max()), 1)}
-                         for k, x in cols.items()}
-            phases[v]['units'] = units
-            # by start order: the first 2000 units (the start-up chain) against the rest
-            order = raw[:, 4].argsort()
-            phases[v]['first2000_lookback_cycles'] = round(float(raw[order[:2000], 2].mean()), 1)
-            phases[v]['rest_lookback_cycles'] = round(float(raw[order[2000:], 2].mean()), 1)
         elif dbg and dbg[0] & 64 and 'run=' in v:  # the lean streaming decode's wave stamps
             dec.run()
             torch.cuda.synchronize()

@@ -87,9 +87,6 @@ struct DevArgs {
   uint32_t swave;        // ragged plans of long samples: one sample per wave (mdsx_swave.hip)
   uint4* sw_rec;         // [ntiles x tile_rows] its per-sample records (scan_tiles_kernel<true>)
   uint32_t sw_lds;       // ... bytes of its per-wave LDS copy of the columns past the first
-  uint32_t unit_ahead;   // row-parallel decode in one pass (mdsx_rows.hip kUnit): units ahead whose
-                         // ragged bytes a unit publishes (0: the scan pass ran before the decode)
-  uint32_t unit_ticket;  // ... units drawn from the ticket counter (else in workgroup order)
   uint32_t gather_block0[MDSX_MAX_COLUMNS + 1];  // first gather workgroup of each ragged column
   DevCol cols[MDSX_MAX_COLUMNS];
 };
@@ -288,10 +285,6 @@ __device__ __forceinline__ uint32_t draw_ticket(const DevArgs& a, uint32_t* s_ti
 int launch_stage_totals(const DevArgs& a, bool nt, hipStream_t s);
 int launch_run_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s);
 int launch_rows_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s);
-// The row-parallel decode's single-pass form (a.unit_ahead > 0, mdsx_rows.hip kUnit) takes the
-// batch: tiles of 64 rows, 1..kUnitMaxVars ragged columns, one stage, non-temporal.
-constexpr int kUnitMaxVars = 3;
-bool rows_unit_ok(const mdsx_plan* plan, const DevArgs& a);
 // The samples listed (tile << 32 | row in tile, a.src_abs; count at kHugeCountOffset) as larger
 // than an LDS stage: one workgroup each, straight from HBM (mdsx_stage.hip).
 int launch_huge_rows(const DevArgs& a, bool nt, hipStream_t s);

@@ -81,12 +81,6 @@ struct mdsx_plan {
                            // else 4)
   int rows_pipe = 0;       // row-parallel decode: tiles per workgroup, the next tile's DMA in
                            // flight while one is written (two stages; 0: one tile, one stage)
-  int rows_unit = 0;       // row-parallel decode, single pass: no scan pass -- units of tiles
-                           // (1: one tile per unit, in workgroup order; 2: the same from a ticket
-                           // counter; 4: four tiles per unit, ticket), each publishing the ragged
-                           // bytes of the unit rows_ahead units later and finding its own output
-                           // base by a look-back (mdsx_rows.hip kUnit; MDSX_TUNE runit)
-  int rows_ahead = 4096;   // ... (MDSX_TUNE rahead)
   int swave = -1;          // ragged batches of the streaming decode's sample sizes: one sample per
                            // one-wave workgroup, in registers, instead (mdsx_swave.hip; -1: when
                            // the samples average <= 4/5 of its register window, +3 % on config C,

@@ -1460,16 +1460,9 @@ static int launch_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s,
     return launch_swave_decode(plan, a, s);
   }
   if (plan->nvar > 0 && (a.run_slots > 0 || a.rows_bytes > 0)) {
-    // the row-parallel decode's single-pass form (plan->rows_unit: units of 256 samples, each
-    // publishing a later unit's ragged bytes and looking back for its own base, mdsx_rows.hip)
-    if (single && a.rows_bytes > 0 && plan->rows_unit && rows_unit_ok(plan, a)) {
-      DevArgs u = a;
-      u.unit_ahead = uint32_t(std::max(plan->rows_ahead, 1));
-      u.unit_ticket = plan->rows_unit != 1 ? 1u : 0u;
-      return launch_rows_decode(plan, u, s);
-    }
-    // else the scan pass, then the decode (the round-3 look-back of tiles in flight measured
-    // slower than the pass: profiles/r03/negative/rows_single_pass)
+    // the streaming and row-parallel decodes have no single-pass form: their scan pass, then
+    // the decode (a look-back across the ~1000 tiles in flight measured slower than the pass:
+    // profiles/r03/negative/rows_single_pass)
     if (single && (rc = scan_pass(plan, a, s)) != MDSX_OK) return rc;
     return a.run_slots > 0 ? launch_run_decode(plan, a, s) : launch_rows_decode(plan, a, s);
   }

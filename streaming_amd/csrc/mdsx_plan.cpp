@@ -218,10 +218,6 @@ void apply_tuning(mdsx_plan* p) {
       p->rows_occ = int(v);
     } else if (key == "rpipe" && v >= 0 && v <= 1024) {
       p->rows_pipe = int(v);
-    } else if (key == "runit" && (v == 0 || v == 1 || v == 2 || v == 4)) {
-      p->rows_unit = int(v);
-    } else if (key == "rahead" && v >= 1 && v <= (1 << 20)) {
-      p->rows_ahead = int(v);
     } else if (key == "rownt") {
       p->rows_nt = v ? 1 : 0;
     } else if (key == "swg" && (v == 1 || v == 2 || v == 4)) {

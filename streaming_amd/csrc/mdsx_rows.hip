@@ -119,339 +119,6 @@ __device__ __forceinline__ void rows_dma(const DevArgs& a, const TileRun& run, u
   }
 }
 
-// ---- the single pass (kUnit) ------------------------------------------------------------------
-// Without the scan pass a tile's output base must come from the tiles before it. The unit of that
-// scan is 256 consecutive samples (kRowsBlock / TR tiles in the batch's tile order), one unit per
-// workgroup, drawn from a ticket counter so that every unit a workgroup waits on is held by a
-// workgroup that is already running. A unit's ragged bytes per column are published early, by
-// the workgroup of the unit `unit_ahead` places before it: the offsets and size heads of those
-// samples (the scan pass's reads, stage_totals_kernel) are loaded beside that workgroup's first
-// DMA, inside the decode, where HBM has room (the decode of short samples runs at ~0.4 of the
-// copy rate). The first unit_ahead units publish their own. A unit then finds its base by a
-// decoupled look-back over the status words ([nvar][units], lookback_bases' encoding): the
-// aggregates before it are published long before, so one round of kLbQ x 64 words per column
-// usually reaches an inclusive prefix, and that round is in flight with the unit's first DMA.
-// (The round-3 single pass published each tile's bytes only after its own DMA and head parse and
-// looked back 32 tiles per round: 1.5x slower than scan + decode, profiles/r03/negative/
-// rows_single_pass.)
-constexpr int kUnitVars = kUnitMaxVars;  // ragged columns of the single-pass form
-
-// Loads at a wave-uniform address through the scalar cache: counted in lgkmcnt, so waiting for
-// them does not wait for this wave's vector loads, DMA and stores in flight (a vector load's
-// s_waitcnt vmcnt covers all of those). Read-only data of the launch (the batch and its tables).
-__device__ __forceinline__ uint64_t uniform_addr(const void* p) {  // (in SGPRs: readfirstlane)
-  const uint64_t x = reinterpret_cast<uint64_t>(p);
-  return uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(x))))) |
-         (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(x >> 32))))) << 32);
-}
-typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
-
-// A tile's facts for the single pass, one 48-byte record per tile written by unit_runs_kernel (in
-// the run-record space of the scan pass, which this form does not run), so that a workgroup
-// starts a tile with ONE load (two scalar loads in flight together) instead of the tile ->
-// shard -> descriptor -> offsets chain.
-struct UnitRun {
-  uint64_t shard_off;  // batch byte of the tile's shard
-  uint64_t row0;       // output row of the tile's first sample
-  uint32_t b0, e1;     // the tile's byte range in its shard (offsets of its first / after its last)
-  uint32_t r0, nrows;  // first sample in the shard, samples (0: none, or the table past the file)
-  uint32_t shard, hdr_end;  // batch shard index; the end of the shard's offsets table
-  uint32_t bytes;      // the shard's bytes (clamped to 2^32 - 1: every offset is a u32)
-  uint32_t fit;        // hdr_end <= b0 <= e1 <= bytes (each sample is checked by the decode)
-};
-static_assert(sizeof(UnitRun) == sizeof(TileRun), "UnitRun takes TileRun's space");
-
-__device__ __forceinline__ UnitRun sld_run(const UnitRun* p) {
-  u32x8 x;
-  u32x4 y;
-  const uint64_t ad = uniform_addr(p);
-  asm volatile("s_load_dwordx8 %0, %2, 0x0\n\ts_load_dwordx4 %1, %2, 0x20\n\ts_waitcnt lgkmcnt(0)"
-               : "=&s"(x), "=&s"(y) : "s"(ad) : "memory");
-  UnitRun r;
-  r.shard_off = uint64_t(x[0]) | (uint64_t(x[1]) << 32);
-  r.row0 = uint64_t(x[2]) | (uint64_t(x[3]) << 32);
-  r.b0 = x[4], r.e1 = x[5], r.r0 = x[6], r.nrows = x[7];
-  r.shard = y[0], r.hdr_end = y[1], r.bytes = y[2], r.fit = y[3];
-  return r;
-}
-
-// The single pass's pre-pass: every tile's UnitRun (two offsets per tile, no size heads -- the
-// scan pass reads a line per sample), and the shard header check at each shard's first tile
-// (stage_totals_kernel's).
-__global__ __launch_bounds__(kBlock) void unit_runs_kernel(const DevArgs a) {
-  const uint32_t tile = blockIdx.x * uint32_t(kBlock) + threadIdx.x;
-  if (tile >= a.ntiles) return;
-  const TileView v = tile_view(a, tile);
-  UnitRun r;
-  r.shard_off = v.d.offset;
-  r.row0 = v.d.row0 + v.r0;
-  r.r0 = v.r0;
-  r.nrows = v.table_ok ? v.nrows : 0u;
-  r.shard = v.shard_idx;
-  r.hdr_end = uint32_t(min(v.hdr_end, uint64_t(0xffffffffu)));
-  r.bytes = uint32_t(min(v.d.bytes, uint64_t(0xffffffffu)));
-  r.b0 = r.e1 = 0;
-  r.fit = 0;
-  if (r.nrows) {
-    r.b0 = v.offs[v.r0];
-    r.e1 = v.offs[v.r0 + r.nrows];
-    r.fit = v.hdr_end <= r.b0 && r.b0 <= r.e1 && r.e1 <= v.d.bytes ? 1u : 0u;
-  }
-  reinterpret_cast<UnitRun*>(a.tile_run)[tile] = r;
-  // header written by encode_joint_shard (mds/writer.py:133-144)
-  if (tile == v.d.tile0 &&
-      (!v.table_ok || *reinterpret_cast<const uint32_t*>(v.shard) != v.d.samples ||
-       v.offs[0] < v.hdr_end || v.offs[v.d.samples] > v.d.bytes))
-    report_decode(a, MDSX_E_HEADER, int(v.shard_idx), -1, -1);
-}
-
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-  return x;
-}
-
-// The samples whose ragged bytes this workgroup publishes: sample t of unit pu[k] (k < np), its
-// offsets pair loaded first (the loads go out before the unit's first tile head waits).
-struct UnitAhead {
-  uint32_t pu[2];
-  int np;
-  uint32_t b[2], e[2];
-  const uint8_t* shard[2];
-  uint64_t hdr_end[2], bytes[2];
-  bool in[2];
-};
-
-// (tiles of 64 rows: wave w takes tile w of the unit, lane l its sample l)
-__device__ __forceinline__ void unit_ahead_offsets(const DevArgs& a, UnitAhead& P, uint32_t unit,
-                                                   uint32_t nunits, uint32_t G, int wave,
-                                                   int lane) {
-  const uint32_t D = a.unit_ahead;
-  P.np = 0;
-  if (unit < D) P.pu[P.np++] = unit;  // (block-uniform)
-  if (uint64_t(unit) + D < nunits) P.pu[P.np++] = unit + D;
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    P.in[k] = false;
-    P.b[k] = P.e[k] = 0;
-    if (k >= P.np) continue;
-    const uint32_t tile = P.pu[k] * G + uint32_t(wave);  // (wave-uniform from here)
-    if (uint32_t(wave) >= G || tile >= a.ntiles) continue;
-    const UnitRun r = sld_run(reinterpret_cast<const UnitRun*>(a.tile_run) + tile);
-    P.shard[k] = a.batch + r.shard_off;
-    P.hdr_end[k] = r.hdr_end;
-    P.bytes[k] = r.bytes;
-    if (uint32_t(lane) >= r.nrows) continue;
-    P.in[k] = true;
-    const uint32_t* offs = reinterpret_cast<const uint32_t*>(P.shard[k] + 4);
-    P.b[k] = offs[r.r0 + uint32_t(lane)];
-    P.e[k] = offs[r.r0 + uint32_t(lane) + 1];
-  }
-}
-
-// The rest of the unit's prologue, every thread: the size heads of the published samples, their
-// ragged bytes by the scan pass's row rule (a sample failing its range or head checks counts
-// zero), the per-unit sums; then wave 1 publishes them, looks back for this unit's base and
-// publishes its inclusive prefix. Leaves the base of every ragged column in s_base[c]. Ends in a
-// workgroup barrier.
-//
-// The look-back (wave 1, every lane active): the wave splits into one segment of W = 64 / 2^k
-// lanes per ragged column (W = 32 for two columns); lane kk of a segment reads the status words
-// of units j - kk - W q (q < kLbQ), so a round covers W kLbQ units per column with the same
-// registers whatever the column count. Per segment: the nearest inclusive prefix in the window
-// with every word up to it published ends the column (its value plus the aggregates before it);
-// a window of aggregates only is summed and the window moves back; an unpublished word in the
-// span waits (s_sleep) and the window is read again. Every decision is a select on the lanes of a
-// segment, so the loop has no divergent branch; its exit is a ballot.
-// issue_own(): the unit's first DMA and its samples' offsets, issued once the published samples'
-// offsets have landed and before their heads are loaded; finish_own(): the checks on those
-// offsets, after the heads loads are issued (a wait for a vector load issued after the inline-asm
-// DMA waits for the DMA too: the compiler does not count it), so the heads, the look-back round
-// and the DMA are in flight together.
-template <bool kNT, int kLbQ, class IssueOwn, class FinishOwn>
-__device__ __forceinline__ void unit_publish_lookback(const DevArgs& a, const UnitAhead& P,
-                                                      uint32_t unit, uint32_t nunits, int t,
-                                                      int lane, int wave,
-                                                      MDSX_L uint64_t* s_part /*[4][2][kUnitVars]*/,
-                                                      const MDSX_L DevCol* cols,
-                                                      MDSX_L uint64_t* s_base, uint32_t shard,
-                                                      IssueOwn&& issue_own, FinishOwn&& finish_own) {
-  const int nv = a.nvar;
-  uint64_t* words = a.lookback;
-  const int W = nv <= 1 ? 64 : nv <= 2 ? 32 : 16;  // (nv <= kUnitVars = 4)
-  const int kk = lane & (W - 1), seg0 = lane & ~(W - 1), vi = lane / W;
-  const uint64_t wmask = W == 64 ? ~0ull : (1ull << W) - 1;
-  const bool own_here = P.np > 0 && P.pu[0] == unit;  // this workgroup computes its own bytes
-  // per lane (uniform within a segment): the window's top unit, done, the bases so far, own bytes
-  int64_t j = int64_t(unit) - 1;
-  bool done = vi >= nv;
-  bool need_own = vi < nv && !own_here;
-  uint64_t base = 0, own = 0, ow = 0;
-  uint64_t w[kLbQ];
-  gu64* st = (gu64*)(words + uint64_t(vi < nv ? vi : 0) * nunits);
-  auto lb_issue = [&]() {
-#pragma unroll
-    for (int q = 0; q < kLbQ; ++q) {
-      const int64_t k = j - kk - int64_t(W) * q;
-      w[q] = (!done && k >= 0)
-                 ? __hip_atomic_load(st + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                 : kLbInclusive;  // (before unit 0, or a finished column: an inclusive zero)
-    }
-    ow = need_own ? __hip_atomic_load(st + unit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-  };
-  // the published samples' heads and ragged bytes, one unit at a time (a second one only for the
-  // first unit_ahead units, which publish their own bytes too); the first unit's heads loads,
-  // the look-back round and the DMA go out together (every lane's offsets land before them)
-  // (nv <= 3: a sample's heads lie in one dword-aligned 16-byte load, unconditional, so the
-  // compiler counts it exactly)
-  struct UnitHeads {
-    u32x4 w;
-    uint32_t sh;
-    __device__ __forceinline__ uint32_t get(int k) const {
-      uint32_t r = 0;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) r = k == j ? alignbyte(w[j + 1], w[j], sh) : r;
-      return r;
-    }
-  };
-  auto publish_sums = [&](int k, const UnitHeads& h, bool hv) {
-    uint32_t x[kUnitVars];
-#pragma unroll
-    for (int c = 0; c < kUnitVars; ++c) x[c] = 0;
-    if (hv) {
-      const uint32_t b = P.b[k], e = P.e[k];
-      uint64_t need = 4ull * uint32_t(nv);
-      for (int c = 0; c < a.ncols; ++c)  // (the column table in LDS: no vector-memory wait)
-        need += cols[c].var_index >= 0 ? h.get(cols[c].var_index) : cols[c].row_bytes;
-      if (uint64_t(b) + need <= e) {
-#pragma unroll
-        for (int c = 0; c < kUnitVars; ++c) x[c] = c < nv ? h.get(c) : 0u;
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < kUnitVars; ++c) {
-      if (c >= nv) break;
-      const uint64_t sum = wave_sum64(x[c]);
-      if (lane == 0) s_part[(wave * 2 + k) * kUnitVars + c] = sum;
-    }
-  };
-  auto heads_of = [&](int k, UnitHeads& h) -> bool {
-    const uint32_t b = P.b[k], e = P.e[k];
-    const bool hv = P.in[k] && P.hdr_end[k] <= b && b < e && e <= P.bytes[k] &&
-                    4ull * uint32_t(nv) <= e - b;
-    // (the load is unconditional: a lane without a sample reads its shard's first bytes)
-    const uint64_t ad = reinterpret_cast<uint64_t>(P.shard[k]) + (hv ? b : 0u);
-    h.sh = uint32_t(ad & 3);
-    const MDSX_G u32x4* q = gp_at<const u32x4>(ad & ~uint64_t(3));
-    h.w = kNT ? __builtin_nontemporal_load(q) : *q;
-    return hv;
-  };
-  {
-    // (P's offsets land at the first use below; nothing else is in flight then)
-    const bool ok0 = P.np > 0 && P.in[0] && P.hdr_end[0] <= P.b[0] && P.b[0] < P.e[0] &&
-                     P.e[0] <= P.bytes[0];
-    if (wave == 1) lb_issue();  // round 1
-    issue_own();
-    UnitHeads h;
-    const bool hv = ok0 && heads_of(0, h);
-    finish_own();
-    if (P.np > 0) publish_sums(0, h, hv);
-  }
-  if (P.np > 1) {  // (block-uniform)
-    UnitHeads h;
-    const bool hv = heads_of(1, h);
-    publish_sums(1, h, hv);
-  }
-  lds_barrier();
-  if (wave == 1) {  // (a scalar branch: every lane active)
-    // publish: status and value in one 8-byte word (agent-scope atomic store), so no fence
-    // orders them; the lane that stores a unit's aggregate here is the one that stores this
-    // unit's inclusive prefix over its own word below (lane kk 0 of the column's segment)
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      if (k >= P.np) break;
-      uint64_t sum = 0;
-      for (int wv = 0; wv < kRowsBlock / 64; ++wv)
-        sum += s_part[(wv * 2 + k) * kUnitVars + (vi < nv ? vi : 0)];
-      const uint32_t pu = P.pu[k];
-      if (pu == unit) own = sum;
-      if (kk == 0 && vi < nv)
-        __hip_atomic_store(st + pu, (pu == 0 ? kLbInclusive : kLbAggregate) | sum,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    uint32_t polls = 0;
-    const uint64_t lb0 = (a.stage_debug & 512) ? shader_clock() : 0;  // (measurement: stamps)
-    for (;;) {
-      // this unit's own aggregate, published by the workgroup unit_ahead units before it
-      const bool own_wait = need_own && (ow >> 62) == 0;
-      if (need_own && !own_wait) own = ow & kLbValue, need_own = false;
-      // per segment: the nearest inclusive prefix, and whether every word up to it is published
-      uint64_t span_sum = 0;
-      bool incl_found = false, wait = false, past = false;  // past: an earlier q held it
-#pragma unroll
-      for (int q = 0; q < kLbQ; ++q) {
-        const uint64_t inc = (__ballot((w[q] >> 62) == 2) >> seg0) & wmask;
-        const uint64_t non = (__ballot((w[q] >> 62) == 0) >> seg0) & wmask;
-        // lanes of this q inside the span: all before the inclusive, up to its lowest lane
-        const uint64_t m = past ? 0ull : inc ? ((inc & (0 - inc)) << 1) - 1 : wmask;
-        wait = wait || (non & m) != 0;
-        span_sum += ((m >> kk) & 1) ? (w[q] & kLbValue) : 0;
-        incl_found = incl_found || (!past && inc != 0);
-        past = past || inc != 0;
-      }
-      // the segment's sum (every lane active: the shuffles stay inside the segment)
-      for (int o = W >> 1; o > 0; o >>= 1) span_sum += __shfl_xor(span_sum, o);
-      const bool step = !done && !wait && !own_wait;
-      base += step ? span_sum : 0;
-      j -= (step && !incl_found) ? int64_t(W) * kLbQ : 0;
-      done = done || (step && incl_found);
-      const bool waiting = __ballot(!done && (wait || own_wait)) != 0;
-      if (__ballot(!done || need_own) == 0) break;
-      // an earlier unit's workgroup is still loading its heads (units run in dispatch order, so
-      // it runs); the bound only keeps a broken invariant from hanging the launch
-      if (++polls >= (1u << 22)) {
-        if (lane == 0) report_decode(a, MDSX_E_HIP, int(shard), -1, -1);
-        break;
-      }
-      if (waiting) __builtin_amdgcn_s_sleep(1);
-      lb_issue();
-    }
-    if ((a.stage_debug & 512) && lane == 0) {  // measurement: rounds, cycles of the look-back
-      a.src_abs[8ull * unit + 1] = polls + 1;
-      a.src_abs[8ull * unit + 2] = shader_clock() - lb0;
-    }
-    // lane kk 0 of each segment: this unit's inclusive prefix, and the column totals if it is the
-    // batch's last unit; the bases into s_base, column by column (a scalar loop)
-    if (kk == 0 && vi < nv) {
-      __hip_atomic_store(st + unit, kLbInclusive | (base + own), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      if (unit + 1 == nunits) {
-        for (int c = 0; c < a.ncols; ++c)
-          if (cols[c].var_index == vi) cols[c].offsets[a.rows] = int64_t(base + own);
-        if (a.totals) a.totals[vi] = int64_t(base + own);
-      }
-    }
-    for (int v = 0; v < nv; ++v) {
-      const uint64_t bv = readlane64(base, v * W);
-      for (int c = lane; c < a.ncols; c += 64)
-        if (cols[c].var_index == v) s_base[c] = bv;
-    }
-  }
-  lds_barrier();
-}
-
-// The DMA of a tile's bytes [lo, lo + 16 nq) of frame into a stage by one wave (1 KiB per
-// instruction).
-template <bool kNT>
-__device__ __forceinline__ void rows_dma1(const uint8_t* frame, uint32_t lo, uint32_t nq,
-                                          uint32_t stage_lds, int lane) {
-  const uint4* src = reinterpret_cast<const uint4*>(frame + lo);
-  for (uint32_t kb = 0; kb * 64 < nq; ++kb) {
-    const uint32_t k = kb * 64 + uint32_t(lane);
-    if (k < nq) glds16<kNT>(src + k, stage_lds + kb * 1024u);
-  }
-}
-
 // One value of the window: output byte inside the window's output of its column, bytes (0: a
 // sample that failed a check), stage position of its first byte (read with one ds_read_b128).
 struct RowsRec {
@@ -476,21 +143,13 @@ struct RowsTab {
 // workgroups fit a CU where their LDS does).
 // kFlat: the write loop over all columns' chunks at once (else one loop per column; measurement
 // control, MDSX_TUNE sdbg bit 256).
-// kUnit: the single pass (above): the workgroup decodes the kRowsBlock / TR tiles of one unit of
-// 256 samples in turn, with no scan pass before it (tiles of at most 64 rows, at most kUnitVars
-// ragged columns); each tile's range, checks and DMA from its offsets (its head, wave 0).
 template <bool kNT, bool kPipe, bool kProf = false, bool kFence = false, int kOcc = 4,
-          bool kFlat = true, int kUnitG = 0>
+          bool kFlat = true>
 __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const DevArgs a) {
-  constexpr bool kUnit = kUnitG > 0;
-  constexpr uint32_t G = kUnit ? uint32_t(kUnitG) : 1u;  // kUnit: tiles per unit
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   __shared__ int64_t s_wsum[kRowsBlock / 64];
   __shared__ uint32_t s_gb, s_lo, s_hi;
-  __shared__ uint32_t s_fit, s_flo;  // kUnit: the tile fits the stage (DMA issued), its stage byte 0
-  __shared__ uint64_t s_part[kUnit ? (kRowsBlock / 64) * 2 * kUnitVars : 1];  // kUnit: wave sums
-  const int t = threadIdx.x, lane = t & 63;
-  const int wave = kUnit ? __builtin_amdgcn_readfirstlane(t >> 6) : t >> 6;  // (kUnit: an SGPR)
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const uint32_t blk = (a.xcd_order & kXcdRows) ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
   const int TR = a.tile_rows;
   const int ncols = a.ncols, nvar = a.nvar;
@@ -535,83 +194,9 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
     }
   }
 
-  // kUnit: the unit (ticket), its tiles, and the offsets of the samples it publishes
-  uint32_t unit = 0, nunits = 0;
-  UnitAhead P;
   uint32_t count = kPipe ? last - first : 1u;  // (1: the loop folds away)
-  // kUnit: a tile's head -- its range from the offsets of its first and last samples (scalar
-  // loads; unit_range), then (unit_issue) its DMA by wave 0 when the range is valid and fits the
-  // stage, its samples' offsets (the file checks; a sample failing them leaves the DMA unused and
-  // the tile to the window path), and s_fit / s_flo for every wave
-  auto unit_range = [&](const UnitRun& r, uint32_t& fit, uint32_t& lo, uint32_t& nq) {
-    // (a shard starts on a 256-byte boundary of the batch)
-    fit = r.nrows && r.fit && (r.b0 & 127u) + (r.e1 - r.b0) <= cap ? 1u : 0u;
-    lo = r.b0 & ~127u;
-    nq = ((r.b0 & 127u) + (r.e1 - r.b0) + 15) >> 4;
-  };
-  auto unit_issue = [&](const UnitRun& r, uint32_t fit, uint32_t lo, uint32_t nq, uint32_t& b,
-                        uint32_t& e) {
-    const uint8_t* sh = a.batch + r.shard_off;
-    if (fit && wave == 0) rows_dma1<kNT>(sh, lo, nq, lds0, lane);
-    const uint32_t* offs = reinterpret_cast<const uint32_t*>(sh + 4);
-    if (t < int(r.nrows)) b = offs[r.r0 + uint32_t(t)], e = offs[r.r0 + uint32_t(t) + 1];
-  };
-  auto unit_finish = [&](const UnitRun& r, uint32_t fit, uint32_t lo, uint32_t b, uint32_t e,
-                         bool& in_range) {
-    // (sample_range's checks on the offsets unit_issue loaded; the header: unit_runs_kernel)
-    const int n = int(r.nrows);
-    int rc = MDSX_OK;
-    if (t < n) {
-      if (!(r.hdr_end <= b && b <= e && e <= r.bytes)) rc = MDSX_E_BOUNDS;
-      else if (b == e) rc = MDSX_E_EMPTY;
-    }
-    in_range = t < n && rc == MDSX_OK;
-    if (wave == 0) {  // (a scalar branch: every lane active; every sample of the tile is in wave 0)
-      const bool bad = __ballot(t < n && rc != MDSX_OK) != 0;
-      if (lane == 0) s_fit = fit && !bad ? 1u : 0u, s_flo = lo;
-    }
-    if (t < n && rc != MDSX_OK) report_decode(a, rc, int(r.shard), int(r.r0 + t), -1);
-  };
-  if constexpr (kUnit) {
-    // the unit's prologue: its ticket, the offsets of the samples whose bytes it publishes, its
-    // first tile's head (DMA in flight), the publication and the look-back (its bases)
-    // (the unit: drawn from the ticket counter, or the workgroup's index -- workgroups are
-    // dispatched in index order, so every earlier unit's workgroup is running or done)
-    __shared__ uint32_t s_ticket;
-    if (a.unit_ticket && t == 0) s_ticket = atomicAdd(a.ticket, 1u);
-    if (t < ncols) s_skip[t] = 0;
-    lds_barrier();
-    unit = a.unit_ticket ? __builtin_amdgcn_readfirstlane(s_ticket) : blockIdx.x;
-    nunits = (a.ntiles + G - 1) / G;
-    if (unit >= nunits) return;  // (the grid is nunits workgroups)
-    const uint64_t pro0 = (a.stage_debug & 512) ? shader_clock() : 0;  // (measurement: stamps)
-    count = G == 1 ? 1u : min(G, a.ntiles - unit * G);
-    unit_ahead_offsets(a, P, unit, nunits, G, wave, lane);
-    const uint32_t tile = unit * G;
-    const UnitRun r = sld_run(reinterpret_cast<const UnitRun*>(a.tile_run) + tile);
-    const int n = int(r.nrows);
-    uint32_t fit, lo, nq;
-    unit_range(r, fit, lo, nq);
-    // its samples' offsets and checks for the loop's first trip (the value records' space,
-    // written later in that trip)
-    uint32_t b = 0, e = 0;
-    auto issue_own = [&]() { unit_issue(r, fit, lo, nq, b, e); };
-    auto finish_own = [&]() {
-      bool in_range = false;
-      unit_finish(r, fit, lo, b, e, in_range);
-      MDSX_L uint32_t* stash = (MDSX_L uint32_t*)T.rec;
-      if (t < n) stash[t] = b, stash[TR + t] = e, stash[2 * TR + t] = in_range;  // (<= 12 TR B)
-    };
-    unit_publish_lookback<kNT, 8>(a, P, unit, nunits, t, lane, wave, (MDSX_L uint64_t*)s_part,
-                                  cols, s_base, r.shard, issue_own, finish_own);
-    // measurement only (MDSX_TUNE sdbg bit 512; the huge-row list's space, 8 words per unit):
-    // cycles of the prologue, look-back rounds, cycles in the look-back loop, the unit's end and
-    // start (shader clock)
-    if ((a.stage_debug & 512) && t == 0)
-      a.src_abs[8ull * unit] = shader_clock() - pro0, a.src_abs[8ull * unit + 4] = pro0;
-  }
   for (uint32_t it = 0; it < count; ++it) {  // block-uniform
-  const uint32_t tile = kUnit ? unit * G + it : first + it;
+  const uint32_t tile = first + it;
   const uint32_t sbuf = kPipe ? it & 1u : 0u;
   const lds_u8* stage = (const lds_u8*)(smem + kStageFront + sbuf * stage_stride);
   const uint32_t stage_lds = lds0 + sbuf * stage_stride;
@@ -625,40 +210,16 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
   constexpr bool prof = kProf;
   uint64_t ts = prof ? shader_clock() : 0;
 
-  // ---- the tile: its run record (scan pass), its head (kUnit) or its shard's view
-  const TileRun run = kUnit ? TileRun{} : a.tile_run[tile];
-  bool fast = kUnit ? false : fits(run);  // block-uniform
+  // ---- the tile: its run record (scan pass) or its shard's view
+  const TileRun run = a.tile_run[tile];
+  const bool fast = fits(run);  // block-uniform
   const uint8_t* frame;  // b / e below are byte positions relative to frame
   int n;
   uint64_t row0;
   uint32_t shard_idx, r0;
   uint32_t b = 0, e = 0;
   bool in_range = false;
-  uint32_t unit_lo = 0;  // kUnit, a tile that fits: stage byte 0 = frame byte unit_lo
-  if constexpr (kUnit) {
-    const UnitRun r = sld_run(reinterpret_cast<const UnitRun*>(a.tile_run) + tile);
-    n = int(r.nrows);
-    row0 = r.row0;
-    shard_idx = r.shard;
-    r0 = r.r0;
-    frame = a.batch + r.shard_off;
-    if (it == 0) {  // the head ran in the prologue (which ended in a barrier)
-      const MDSX_L uint32_t* stash = (const MDSX_L uint32_t*)T.rec;
-      if (t < n) b = stash[t], e = stash[TR + t], in_range = stash[2 * TR + t] != 0;
-    } else {
-      uint32_t fit, lo, nq;
-      unit_range(r, fit, lo, nq);
-      unit_issue(r, fit, lo, nq, b, e);
-      unit_finish(r, fit, lo, b, e, in_range);
-      rows_barrier<kFence>();
-    }
-    fast = s_fit != 0;
-    unit_lo = s_flo;
-    if (n == 0) {  // block-uniform (a table past the file: reported above)
-      rows_barrier<kFence>();  // (every wave has read s_fit before the next head stores it)
-      continue;
-    }
-  } else if (fast) {
+  if (fast) {
     // one window: the DMA of the run's bytes goes out with the offsets loads
     n = run.nrows;
     row0 = run.row0;
@@ -694,7 +255,7 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
     in_range = t < n && rc == MDSX_OK;
     if (t < n && rc != MDSX_OK) report_decode(a, rc, shard_idx, int(r0 + t), -1);
   }
-  if (!kUnit && t < ncols) {
+  if (t < ncols) {
     const MDSX_L DevCol& col = cols[t];
     const int vi = col.var_index;
     uint32_t skip = 0;
@@ -716,7 +277,7 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
     bool direct = false;
     if (fast) {
       gb = n;
-      lo_al = kUnit ? unit_lo : uint32_t((run.stream & ~uint64_t(127)) - run.shard_off);
+      lo_al = uint32_t((run.stream & ~uint64_t(127)) - run.shard_off);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
       rows_barrier<kFence>();  // the previous window's readers of the stage and the tables are done
@@ -846,11 +407,6 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
           s_wbase[c] = base;
           s_wlen[c] = tot;
           s_base[c] = base + tot;
-          if (kUnit) {  // (the scan pass checks a tile's bytes against the capacity in advance)
-            const bool over = base + tot > col.capacity;
-            if (over) report_decode(a, MDSX_E_CAPACITY, int(shard_idx), int(r0 + ga), c);
-            s_skip[c] = over ? 1u : 0u;
-          }
         }
       }
       c0 = pair ? c2 + 1 : c1 + 1;
@@ -1060,20 +616,13 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
     if constexpr (prof) prof_mark(a, tile, 6, ts);
     ga = gb;
   }
-  if constexpr (kPipe || kUnit) rows_barrier<kFence>();  // this tile's readers of the tables and its stage are done
+  if constexpr (kPipe) rows_barrier<kFence>();  // this tile's readers of the tables and its stage are done
   }  // tile
-  if constexpr (kUnit)
-    if ((a.stage_debug & 512) && t == 0) a.src_abs[8ull * unit + 3] = shader_clock();
 }
 
 }  // namespace
 
 uint32_t rows_tile_rows_limit() { return kRowsBlock; }
-
-bool rows_unit_ok(const mdsx_plan* plan, const DevArgs& a) {
-  return a.rows_bytes > 0 && a.tile_rows == 64 && a.nvar >= 1 && a.nvar <= kUnitMaxVars &&
-         a.rows_pipe == 0 && plan->rows_nt != 0;
-}
 
 int launch_rows_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
   if (a.tile_rows > kRowsBlock)
@@ -1088,39 +637,6 @@ int launch_rows_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
   if (lds > 160 * 1024)
     return mdsx::fail(MDSX_E_ARG, "mdsx: row-parallel decode stage and tables exceed 160 KiB of LDS");
   const bool nt = plan->rows_nt != 0;
-  if (a.unit_ahead) {  // the single pass: one workgroup per unit
-    if (!rows_unit_ok(plan, a))
-      return mdsx::fail(MDSX_E_ARG, "mdsx: single-pass row decode: tiles of 64 rows, <= 3 ragged "
-                                    "columns, one stage, non-temporal");
-    // plan->rows_unit: 1 one tile per unit, units in workgroup order; 2 the same from the ticket
-    // counter; 4 four tiles per unit, ticket (registers bounded for six waves per SIMD as the
-    // two-pass default)
-    const int g = plan->rows_unit == 4 ? 4 : 1;
-    const unsigned units = (a.ntiles + g - 1) / g;
-    hipLaunchKernelGGL(unit_runs_kernel, dim3((a.ntiles + kBlock - 1) / kBlock), dim3(kBlock), 0,
-                       s, a);
-    rc = hip_check(hipGetLastError(), "unit_runs_kernel launch");
-    if (rc != MDSX_OK) return rc;
-#define MDSX_UNIT_CASE(G)                                                                        \
-  if (g == G) {                                                                                \
-    const void* fn =                                                                           \
-        reinterpret_cast<const void*>(rows_decode_kernel<true, false, false, false, 6, true, G>); \
-    if (lds > 64 * 1024) {                                                                     \
-      rc = hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)), \
-                     "hipFuncSetAttribute");                                                   \
-      if (rc != MDSX_OK) return rc;                                                            \
-    }                                                                                          \
-    mdsx::set_last_kernel("rows_decode_kernel<true, false, false, false, 6, true, " #G ">");    \
-    hipLaunchKernelGGL((rows_decode_kernel<true, false, false, false, 6, true, G>), dim3(units), \
-                       dim3(kRowsBlock), lds, s, a);                                           \
-  }
-    MDSX_UNIT_CASE(1)
-    MDSX_UNIT_CASE(4)
-#undef MDSX_UNIT_CASE
-    rc = hip_check(hipGetLastError(), "rows_decode_kernel launch");
-    if (rc != MDSX_OK) return rc;
-    return launch_huge_rows(a, nt, s);
-  }
   const unsigned grid = pipe ? (a.ntiles + a.rows_pipe - 1) / a.rows_pipe : a.ntiles;
   // registers bounded for six waves per SIMD where six workgroups' stages fit a CU (measured:
   // +7 % on 32-256-byte samples, -1 % on 256-1024-byte ones)

@@ -86,12 +86,6 @@ MODES = {
     'wave_xcd0': 'run=0,rows=0,gmin=0,gmax=0,ring=0,xcdb=0',  # register tiles in launch order
     'ring': 'run=0,rows=0,gmin=0,gmax=0,ring=8',   # one row per wave through the LDS-DMA ring
     'ring4': 'run=0,rows=0,gmin=0,gmax=0,ring=4',
-    # the row-parallel decode's single pass (mdsx_rows.hip kUnit; the two-pass collection runs
-    # these as scan + decode, test_device_single_pass as the unit form): every unit publishing its
-    # own bytes, each publishing the next one's, and a 2 KiB stage (windows, huge rows)
-    'rows_unit': 'runit=1,rmin=1000000000',
-    'rows_unit_ahead1': 'runit=1,rahead=1,rmin=1000000000',
-    'rows_unit_small': 'runit=1,rows=2,rahead=2,rmin=1000000000',
 }
 
 

@@ -47,12 +47,6 @@ SINGLE_MODES = {
     'single_rows_pipe': 'rows=4,rpipe=5,rmin=1000000000',  # ... two stages per workgroup
     'single_register': 'run=0,rows=0',  # the register decode's single-pass form (look-back)
     'single_swave': 'swave=1,rmin=0',  # scan pass + one sample per wave
-    # the row-parallel decode's own single pass (units of 256 samples, look-back; mdsx_rows.hip
-    # kUnit): every unit publishing its own bytes, every unit publishing the next one's, windows
-    # and huge rows
-    'single_rows_unit': 'runit=1,rmin=1000000000',
-    'single_rows_unit_ahead1': 'runit=1,rahead=1,rmin=1000000000',
-    'single_rows_unit_small': 'runit=1,rows=2,rahead=1,rmin=1000000000',
 }
 
 

@@ -68,12 +68,10 @@ def _columns_equal(a, b):
 C_PLAN = (['b', 'n', 's'], ['bytes', 'int', 'str'], [None, 8, None])
 
 
-@pytest.mark.parametrize('tune', ['', 'run=0,rows=0', 'runit=1,rmin=1000000000',
-                                  'runit=1,rahead=3,rmin=1000000000'])
+@pytest.mark.parametrize('tune', ['', 'run=0,rows=0'])
 def test_single_equals_two_pass_on_many_tiles(monkeypatch, tune):
-    """160k rows of config C, both passes bit-identical: the default decodes, the register
-    decode's look-back over 5000 tiles per column, and the row-parallel decode's unit form (625
-    units looking back; publishing their own bytes, or those of the unit 3 places on)."""
+    """160k rows of config C, both passes bit-identical: the default decodes, and the register
+    decode's look-back over 5000 tiles per column."""
     monkeypatch.setenv('MDSX_TUNE', tune)
     shards, counts, src = var_c_shards(160_000, seed=41, blob_bytes=(0, 600))
     plan = Plan(*C_PLAN)
