@@ -162,7 +162,8 @@ def _gather_batch(dataset: Any, gather: Any, ids: list, retry: int) -> DecodedBa
 
 
 def device_iter(dataset: Any, batch_size: int, *, num_workers: int = 0, retry: int = 7,
-                gather: Optional[Any] = None) -> Iterator[DecodedBatch]:
+                gather: Optional[Any] = None,
+                exchange: Union[bool, Any, None] = None) -> Iterator[DecodedBatch]:
     """``StreamingDataset.__iter__`` (``dataset.py:1475-1513``) yielding DEVICE batches, in the
     order ``DataLoader(dataset, batch_size, num_workers=num_workers)`` yields them on this rank.
 
@@ -192,6 +193,13 @@ def device_iter(dataset: Any, batch_size: int, *, num_workers: int = 0, retry: i
     :func:`register_device_stream`). ``gather``: what turns ids into a batch (default: a
     ``DeviceSampleGather`` over ``dataset.shards``); an object with ``gather(ids)``,
     ``locate(ids)`` and ``shards``.
+
+    ``exchange``: ``True`` (the default process group) or a process group -- each shard is
+    decoded by one rank of the group and every batch's rows are exchanged between the ranks
+    (:class:`streaming_amd.exchange.OwnedShardGather`, RCCL ``all_to_all``), instead of every rank
+    decoding every shard its batches touch. The batches are the same. Every rank of the group
+    runs ``device_iter`` over the same epoch; a rank out of batches (or stopped early) keeps
+    serving the others' requests until every rank is out.
     """
     if batch_size <= 0:
         raise ValueError('batch_size must be positive')
@@ -206,6 +214,20 @@ def device_iter(dataset: Any, batch_size: int, *, num_workers: int = 0, retry: i
                             f'not a device reader (build the dataset with stream_name=\'mdsx\', '
                             f'streaming_amd.plugin.register_device_stream)')
         gather = DeviceSampleGather(ds.shards)
+    if exchange:
+        from streaming_amd.exchange import OwnedShardGather
+        gather = OwnedShardGather(gather, batch_size, group=None if exchange is True else exchange,
+                                  prepare=getattr(ds, 'prepare_shard', None))
+    drain = getattr(gather, 'drain', None)
+    try:
+        yield from _device_iter(ds, mod, gather, batch_size, workers, retry)
+    finally:
+        if drain is not None:  # (every rank of the exchange group takes part until all are out)
+            drain()
+
+
+def _device_iter(ds: Any, mod: Any, gather: Any, batch_size: int, workers: int,
+                 retry: int) -> Iterator[DecodedBatch]:
     # -- StreamingDataset.__iter__, dataset.py:1481-1510
     if hasattr(ds, '_iterator'):
         ds._iterator.exit()

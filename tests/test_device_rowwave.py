@@ -112,6 +112,27 @@ def test_layouts(monkeypatch, mode):
         assert torch.equal(base[name], dec[name]), name
 
 
+def _oracle_malformed(shard):
+    """The samples the reference reader cannot return whole, by the oracle's restatement of it
+    (mds/reader.py:103-149): IndexError where it raises one (an empty read), else the samples
+    whose fixed columns it would slice short (decode_sample's data[idx:idx + size]) -- where the
+    whole-batch decode raises ValueError instead of returning a truncated row."""
+    n = int(np.frombuffer(shard[:4], np.uint32)[0])
+    r = mds_oracle.OracleMDSReader(None, None, {'raw_data': {'basename': ''},
+                                               'column_names': NAMES, 'column_encodings': ENCS,
+                                               'column_sizes': SIZES, 'samples': n}, data=shard)
+    bad = {}
+    for i in range(n):
+        try:
+            parts = r.split_sample(r.get_sample_data(i))
+        except IndexError:
+            bad[i] = IndexError
+            continue
+        if any(len(p) != size for p, size in zip(parts, SIZES)):
+            bad[i] = ValueError
+    return bad
+
+
 def _raises_like(monkeypatch, mode, shards, exact=True):
     with pytest.raises(Exception) as want:
         _decode(monkeypatch, 'rw=0', shards)
@@ -119,6 +140,14 @@ def _raises_like(monkeypatch, mode, shards, exact=True):
         _decode(monkeypatch, MODES[mode], shards)
     if exact:  # (one failing row: the same report; several: whichever lands first)
         assert str(got.value) == str(want.value)
+    # anchored on the oracle: the failing sample is one the reference cannot return whole, and
+    # the exception type is the one the batch path maps its failure to
+    if exact:
+        bad = _oracle_malformed(shards[0])
+        rows = [int(w) for w in str(got.value).replace(',', ' ').replace(')', ' ').split()
+                if w.isdigit()]
+        assert any(row in bad and isinstance(got.value, bad[row]) for row in rows), \
+            (str(got.value), bad)
 
 
 @pytest.mark.parametrize('mode', sorted(MODES))
@@ -131,7 +160,10 @@ def test_malformed_rows_report_like_the_register_decode(monkeypatch, mode):
     # an empty sample (the reference's IndexError)
     empty = [s if i != 3 else b'' for i, s in enumerate(rows)]
     _raises_like(monkeypatch, mode, [_shard(empty)])
-    # the last offset past the file: the header check (and the last row's range)
+    # the last offset past the file: the header check (and the last row's range); the reference
+    # reads every sample whole here (its read stops at the file's end), the batch path refuses
+    # the shard (malformed shards)
     bad = bytearray(_shard(rows))
     bad[4 + 4 * 40:4 + 4 * 41] = np.uint32(len(bad) + 100).tobytes()
+    assert _oracle_malformed(bytes(bad)) == {}
     _raises_like(monkeypatch, mode, [bytes(bad)], exact=False)
