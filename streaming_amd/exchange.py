@@ -240,12 +240,21 @@ class OwnedShardGather:
 
     def _schema(self) -> DecodedBatch:
         """Empty columns of the dataset's schema, for a rank that sends nothing this step: from
-        an earlier step, else from one sample of a shard it owns (one it would decode anyway)."""
+        an earlier step, else the decode of a shard of no samples under the readers' plan (no
+        sample is read, so no malformed one can fail it); for a gather whose shards carry no
+        plan, one sample of a shard this rank owns."""
         if self._proto is None:
-            mine = [g for g in self.owned() if self.shards[g].samples] or [0]
-            first = int(self.starts[mine[0]]) if self.starts is not None else 0
-            self._proto = _empty_like(self.local.gather(np.array([first], np.int64)))
-            self.decoded_shards.add(mine[0])
+            plan = getattr(self.shards[0], 'plan', None) if self.shards else None
+            if plan is not None:
+                from streaming_amd.decoder import decode_batch, stage_shards
+                empty = np.array([0, 8], np.uint32).tobytes()  # count 0, offsets [8] (the end)
+                dev = torch.device('cuda', torch.cuda.current_device())
+                self._proto = decode_batch(plan, stage_shards([empty], [0], plan, device=dev))
+            else:
+                mine = [g for g in self.owned() if self.shards[g].samples] or [0]
+                first = int(self.starts[mine[0]]) if self.starts is not None else 0
+                self._proto = _empty_like(self.local.gather(np.array([first], np.int64)))
+                self.decoded_shards.add(mine[0])
         return self._proto
 
 
