@@ -81,6 +81,8 @@ struct mdsx_plan {
                            // else 4)
   int rows_pipe = 0;       // row-parallel decode: tiles per workgroup, the next tile's DMA in
                            // flight while one is written (two stages; 0: one tile, one stage)
+  int rows_var = 0;        // row-parallel decode, write-loop variant (bits, mdsx_rows.hip kV;
+                           // MDSX_TUNE rv: 0, 1, 3, 5, 9, 13, 15, 17)
   int swave = -1;          // ragged batches of the streaming decode's sample sizes: one sample per
                            // one-wave workgroup, in registers, instead (mdsx_swave.hip; -1: when
                            // the samples average <= 4/5 of its register window, +3 % on config C,
@@ -126,7 +128,7 @@ inline bool use_rows_decode(const mdsx_plan* p, uint64_t bytes, uint64_t rows) {
 inline uint64_t rows_lds_bytes_est(const mdsx_plan* p, uint64_t stage, uint64_t tr) {
   const uint64_t nstage = p->rows_pipe > 0 ? 2 : 1;
   return 192 * nstage + stage * nstage + tr * uint64_t(p->ncols) * 16 + uint64_t(p->ncols) * 32 +
-         uint64_t(p->nvar) * (stage / 16 + 4) + uint64_t(p->ncols) * 72 + 64;
+         uint64_t(p->nvar) * (stage / 16 + 4) + uint64_t(p->ncols) * 104 + 64;
 }
 
 // The stage a tile of tr samples of per_row bytes needs: (1 + 1/slack) of its average bytes plus
