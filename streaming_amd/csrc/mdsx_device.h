@@ -332,26 +332,6 @@ __device__ __forceinline__ uint32_t utf8_lookup_err(uint32_t x, uint32_t p1, uin
   return (b1h & b1l & b2h) ^ must23;
 }
 
-// The 16 chunk bytes X as one stream after the dword pw (utf8_chunk_err2 with sB = 16): nonzero
-// where a byte errs. For a chunk of two values A | B this is the check of their concatenation, in
-// A's context throughout. It errs wherever the two-value check does, with no false pass: where A
-// is not open at sB (utf8_open_at), the bytes of A before sB cannot make a byte of B err or pass
-// (no lead >= C0 / E0 / F0 one / two / three bytes back, and a continuation after them errs as it
-// does after nothing); where A is open, the caller's utf8_open_at reports it.
-__device__ __forceinline__ uint32_t utf8_chunk_err1(const uint4 X, uint32_t pw) {
-  const uint32_t xs[4] = {X.x, X.y, X.z, X.w};
-  uint32_t err = 0, prev = pw, Ep = hi_e0(pw), Fp = hi_f0(pw);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint32_t x = xs[j];
-    const uint32_t E = hi_e0(x), F = hi_f0(x);
-    const uint32_t m23 = alignbyte(E, Ep, 2) | alignbyte(F, Fp, 1);
-    err |= utf8_lookup_err(x, alignbyte(x, prev, 3), m23);
-    prev = x, Ep = E, Fp = F;
-  }
-  return err;
-}
-
 // Bytes [a, b) of v (0 <= a <= b <= 16), others zero.
 __device__ __forceinline__ uint4 keep_bytes(const uint4 v, uint32_t a, uint32_t b) {
   const uint4 m = byte_mask(a, b);

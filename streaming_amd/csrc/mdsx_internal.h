@@ -81,8 +81,6 @@ struct mdsx_plan {
                            // else 4)
   int rows_pipe = 0;       // row-parallel decode: tiles per workgroup, the next tile's DMA in
                            // flight while one is written (two stages; 0: one tile, one stage)
-  int rows_var = 0;        // row-parallel decode, write-loop variant (bits, mdsx_rows.hip kV;
-                           // MDSX_TUNE rv: 0, 1, 3, 5, 9, 13, 15, 17)
   int swave = -1;          // ragged batches of the streaming decode's sample sizes: one sample per
                            // one-wave workgroup, in registers, instead (mdsx_swave.hip; -1: when
                            // the samples average <= 4/5 of its register window, +3 % on config C,

@@ -214,12 +214,10 @@ void apply_tuning(mdsx_plan* p) {
       p->rows_kb = int(v);
     } else if (key == "rslack" && v >= 2 && v <= 64) {
       p->rows_slack = int(v);
-    } else if (key == "rocc" && (v == 4 || v == 5 || v == 6 || v == 8)) {
+    } else if (key == "rocc" && (v == 4 || v == 6 || v == 8)) {
       p->rows_occ = int(v);
     } else if (key == "rpipe" && v >= 0 && v <= 1024) {
       p->rows_pipe = int(v);
-    } else if (key == "rv" && (v == 0 || v == 1 || v == 3 || v == 5 || v == 9 || v == 13 || v == 15 || v == 17)) {
-      p->rows_var = int(v);
     } else if (key == "rownt") {
       p->rows_nt = v ? 1 : 0;
     } else if (key == "swg" && (v == 1 || v == 2 || v == 4)) {

@@ -75,8 +75,9 @@ __host__ __device__ __forceinline__ size_t rows_lds_tables(uint32_t cap, int TR,
   return size_t(nstage) * (kStageFront + size_t(cap) + kStageSlack) +
          size_t(TR) * size_t(ncols) * 16 + size_t(ncols) * 32 + size_t(nvar) * rows_map_len(cap);
 }
-// One column's write descriptor (the write loop's variant rv bit 1): everything the loop reads of
-// the column, in one 32-byte record (one LDS round trip instead of the column table's three).
+// One column's write descriptor: everything the write loop reads of the column, in one 32-byte
+// record written once per window (one LDS round trip per chunk instead of the column table's,
+// window base's and length's three: +0.8-1.3 % on short rows, profiles/r06/rows_var/).
 struct __attribute__((aligned(16))) RowsDesc {
   uint64_t wout;  // the window's first output byte (absolute)
   uint32_t wlen;  // the window's output bytes
@@ -156,15 +157,8 @@ struct RowsTab {
 // workgroups fit a CU where their LDS does).
 // kFlat: the write loop over all columns' chunks at once (else one loop per column; measurement
 // control, MDSX_TUNE sdbg bit 256).
-// kV (MDSX_TUNE rv, bits): 1 the write loop reads each chunk's column from its RowsDesc; 2 the str
-// chunks of one or two values checked as one UTF-8 stream (utf8_chunk_err1), the two-value check
-// only for a chunk that fails it; 4 a str chunk's dword before it read together with the chunk
-// (one LDS round trip, not two); 8 the chunk map's column offset selected from scalar registers
-// with the column (schemas of <= 9 columns), so the map read goes out beside the descriptor's;
-// 16 (with 1) two chunks per thread per trip (chunks kw and kw + 256), each step's LDS reads for
-// both issued before either is used (schemas of <= 9 columns).
 template <bool kNT, bool kPipe, bool kProf = false, bool kFence = false, int kOcc = 4,
-          bool kFlat = true, int kV = 0>
+          bool kFlat = true>
 __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const DevArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   __shared__ int64_t s_wsum[kRowsBlock / 64];
@@ -432,20 +426,19 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
       }
       c0 = pair ? c2 + 1 : c1 + 1;
     }
-    if constexpr ((kV & 1) != 0) {
-      // (wave 0 only: thread 0 of this wave wrote s_wbase / s_wlen above; LDS in program order)
-      if (t < 64) {
-        for (int c = t; c < ncols; c += 64) {
-          const MDSX_L DevCol& col = cols[c];
-          RowsDesc d;
-          d.wout = reinterpret_cast<uint64_t>(col.data) + s_wbase[c];
-          d.wlen = s_wlen[c];
-          d.rb = col.var_index >= 0 ? 0u : col.row_bytes;
-          d.vi = col.var_index >= 0 ? col.var_index : 0;
-          d.utf8 = col.kind == MDSX_KIND_STR && col.flags != nullptr && !(a.stage_debug & 1);
-          d.pad[0] = d.pad[1] = 0;
-          s_desc[c] = d;
-        }
+    // the columns' write descriptors (wave 0 only: its thread 0 wrote s_wbase / s_wlen above, and
+    // one wave's LDS accesses take effect in program order; the barrier below publishes them)
+    if (t < 64) {
+      for (int c = t; c < ncols; c += 64) {
+        const MDSX_L DevCol& col = cols[c];
+        RowsDesc d;
+        d.wout = reinterpret_cast<uint64_t>(col.data) + s_wbase[c];
+        d.wlen = s_wlen[c];
+        d.rb = col.var_index >= 0 ? 0u : col.row_bytes;
+        d.vi = col.var_index >= 0 ? col.var_index : 0;
+        d.utf8 = col.kind == MDSX_KIND_STR && col.flags != nullptr && !(a.stage_debug & 1);
+        d.pad[0] = d.pad[1] = 0;
+        s_desc[c] = d;
       }
     }
     if (direct && t == ga && ok) {  // copied by the huge-row kernel after this one
@@ -497,7 +490,6 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
       constexpr int kEnds = 8;
       uint32_t total = 0;
       uint32_t ends[kEnds];
-      uint32_t mofs[kEnds + 1];  // (kV bit 8) column j's chunk map offset
       if constexpr (kFlat) {
         uint32_t cn = 0;
         if (lane < ncols && !s_skip[lane]) {
@@ -509,149 +501,9 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
         for (int j = 0; j < kEnds; ++j)
           ends[j] = j + 1 < ncols ? uint32_t(__builtin_amdgcn_readlane(int(cincl), j)) : ~0u;
         if (ncols > kEnds + 1 && lane < ncols) s_ends[lane] = cincl;  // (this wave reads its own)
-        if constexpr ((kV & 8) != 0) {
-          const int lvi = lane < ncols ? int(cols[lane].var_index) : -1;
-          const uint32_t lmo = lvi >= 0 ? uint32_t(lvi) * map_len : 0u;
-#pragma unroll
-          for (int j = 0; j <= kEnds; ++j)
-            mofs[j] = j < ncols ? uint32_t(__builtin_amdgcn_readlane(int(lmo), j)) : 0u;
-        }
         total = (a.stage_debug & 2) ? 0u : uint32_t(__builtin_amdgcn_readlane(int(cincl), ncols - 1));
       }
-      bool paired = false;  // (kV bit 16) the chunks written two per trip below
-      if constexpr ((kV & 16) != 0 && kFlat) {
-        static_assert((kV & 1) != 0, "two chunks per trip read the columns' descriptors");
-        if (ncols <= kEnds + 1) {  // uniform
-          paired = true;
-          for (uint32_t kw = uint32_t(t); kw < total; kw += 2 * kRowsBlock) {
-            bool live[2];
-            int cc[2];
-            uint32_t kk[2];
-            RowsDesc dd[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              const uint32_t kg = kw + uint32_t(h) * kRowsBlock;
-              live[h] = kg < total;
-              int c = 0;
-              uint32_t c0 = 0;
-#pragma unroll
-              for (int j = 0; j < kEnds; ++j) {
-                if (j + 1 >= ncols) break;
-                if (kg >= ends[j]) c = j + 1, c0 = ends[j];
-              }
-              cc[h] = c;
-              kk[h] = kg - c0;
-              dd[h] = s_desc[c];
-            }
-            int32_t P0[2], pos[2], endv[2];
-            int r[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              P0[h] = int32_t(kk[h] * 16) - int32_t(dd[h].wout & 15);
-              pos[h] = max(P0[h], 0);
-              endv[h] = min(P0[h] + 16, int32_t(dd[h].wlen));
-              r[h] = !live[h] ? ga
-                     : dd[h].rb ? ga + int(uint32_t(pos[h]) / dd[h].rb)
-                                : int(T.map[size_t(dd[h].vi) * map_len + min(kk[h], map_len - 1u)]);
-            }
-            RowsRec qa[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) qa[h] = T.rec[cc[h] * TR + r[h]];
-            uint4 val[2];
-            int32_t dsA[2], deA[2], hiA[2], paoff[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              dsA[h] = int32_t(qa[h].dst);
-              deA[h] = dsA[h] + int32_t(qa[h].len);
-              paoff[h] = int32_t(qa[h].src) - dsA[h] + P0[h];
-              val[h] = lds_read16(stage + paoff[h]);
-              hiA[h] = min(endv[h], deA[h]);
-            }
-            // then each chunk to its end (a second value's record and bytes, the UTF-8 check, the
-            // store), one after the other
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              if (!live[h]) continue;
-              const int c = cc[h], base = c * TR, rh = r[h];
-              const int32_t p0 = P0[h], end = endv[h];
-              int32_t ps = pos[h];
-              const bool utf8 = dd[h].utf8 != 0;
-              MDSX_L uint32_t* bad = T.bad + c * 8;
-              uint4 v = val[h];
-              bool simple = deA[h] > ps;
-              uint32_t sB = 16;
-              int32_t deL = deA[h];
-              if (simple && hiA[h] < end) {
-                const RowsRec qb = T.rec[base + rh + 1];
-                const int32_t dsB = int32_t(qb.dst), deB = dsB + int32_t(qb.len);
-                simple = dsB == hiA[h] && deB >= end;
-                if (simple) {
-                  const uint4 w = lds_read16(stage + (int32_t(qb.src) - dsB + p0));
-                  sB = uint32_t(hiA[h] - p0);
-                  const uint4 m = byte_mask(0, sB);
-                  v = make_uint4((v.x & m.x) | (w.x & ~m.x), (v.y & m.y) | (w.y & ~m.y),
-                                 (v.z & m.z) | (w.z & ~m.z), (v.w & m.w) | (w.w & ~m.w));
-                  deL = deB;
-                }
-              }
-              if (simple) {
-                if (utf8) {  // (as the one-chunk loop below)
-                  const uint32_t b = sB;
-                  const uint4 X = (ps > p0 || end < p0 + 16)
-                                      ? keep_bytes(v, uint32_t(ps - p0), uint32_t(end - p0)) : v;
-                  uint32_t pw = 0;
-                  if (ps > dsA[h]) {
-                    pw = lds_u32(stage + paoff[h] + (ps - p0) - 4);
-                    const int32_t nv = ps - dsA[h];
-                    if (nv < 4) pw &= ~((1u << (8 * (4 - nv))) - 1u);
-                  }
-                  const bool plain = (((X.x | X.y | X.z | X.w) & 0x80808080u) | hi_c0(pw)) == 0;
-                  if (!__all(plain) || (a.stage_debug & 32)) {
-                    uint32_t e = utf8_chunk_err2(X, pw, b);
-                    if (b < 16 && utf8_open_at(X, pw, b)) e |= 1u;
-                    if (end == p0 + 16 && end == deL) {
-                      if (b < 16) e |= utf8_open_at(keep_bytes(X, b, 16), 0, 16) ? 2u : 0u;
-                      else e |= utf8_open_at(X, pw, 16) ? 1u : 0u;
-                    }
-                    if (e & 1u) atomicOr(&bad[rh >> 5], 1u << (rh & 31));
-                    if (e & 2u) atomicOr(&bad[(rh + 1) >> 5], 1u << ((rh + 1) & 31));
-                  }
-                }
-              } else {
-                v = make_uint4(0, 0, 0, 0);
-                for (int rr = rh; rr < gb && ps < end; ++rr) {
-                  const RowsRec q = T.rec[base + rr];
-                  const int32_t ds = int32_t(q.dst);
-                  const int32_t de = ds + int32_t(q.len);
-                  if (de <= ps) continue;
-                  if (ds >= end) break;
-                  const int32_t lo = max(ps, ds), hi = min(end, de);
-                  const lds_u8* p = stage + (int32_t(q.src) - ds + p0);
-                  const uint4 pv = keep_bytes(lds_read16(p), uint32_t(lo - p0), uint32_t(hi - p0));
-                  v = make_uint4(v.x | pv.x, v.y | pv.y, v.z | pv.z, v.w | pv.w);
-                  if (utf8) {
-                    uint32_t pw = 0;
-                    if (lo > ds) {
-                      pw = lds_u32(p + (lo - p0) - 4);
-                      const int32_t nv = lo - ds;
-                      if (nv < 4) pw &= ~((1u << (8 * (4 - nv))) - 1u);
-                    }
-                    if ((utf8_chunk_err2(pv, pw, 16) & 1u) ||
-                        (hi == de && hi == p0 + 16 && utf8_open_at(pv, pw, 16)))
-                      atomicOr(&bad[rr >> 5], 1u << (rr & 31));
-                  }
-                  ps = hi;
-                }
-              }
-              const uint64_t D = (dd[h].wout & ~uint64_t(15)) + 16ull * kk[h];
-              if ((a.stage_debug & 16) && v.x != 0x9e3779b9u) continue;
-              if (p0 >= 0 && p0 + 16 <= int32_t(dd[h].wlen)) st16<kNT>(D, v);
-              else store_bytes(D, v, uint32_t(max(p0, 0) - p0), uint32_t(end - p0));
-            }
-          }
-        }
-      }
-      for (int cl = 0; cl < (kFlat ? (paired ? 0 : 1) : ncols); ++cl) {
+      for (int cl = 0; cl < (kFlat ? 1 : ncols); ++cl) {
         if (!kFlat && s_skip[cl]) continue;  // block-uniform
         const uint32_t kend = kFlat ? total
                                     : (a.stage_debug & 2) ? 0u
@@ -662,16 +514,12 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
         // the chunk's column c and its index k inside the column
         int c = cl;
         uint32_t c0 = 0;
-        uint32_t mo = (kV & 8) ? mofs[0] : 0u;
         if constexpr (kFlat) {
           if (ncols <= kEnds + 1) {  // uniform: the ends in scalar registers
 #pragma unroll
             for (int j = 0; j < kEnds; ++j) {
               if (j + 1 >= ncols) break;  // (uniform: a narrow schema compares ncols - 1 ends)
-              if (kg >= ends[j]) {
-                c = j + 1, c0 = ends[j];
-                if constexpr ((kV & 8) != 0) mo = mofs[j + 1];
-              }
+              if (kg >= ends[j]) c = j + 1, c0 = ends[j];
             }
           } else {
             for (int j = 0; j + 1 < ncols; ++j) {
@@ -682,30 +530,12 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
         }
         const uint32_t k = kg - c0;
         const int base = c * TR;
-        // (kV bit 8: the map entry requested before the column's descriptor arrives; a fixed
-        // column reads column 0's map, unused)
-        const bool early_map = (kV & 8) != 0 && kFlat && ncols <= kEnds + 1;
-        const uint32_t m_early = early_map ? uint32_t(T.map[mo + min(k, map_len - 1u)]) : 0u;
         // (measurement only, MDSX_TUNE sdbg: 1 no UTF-8 check, 2 no copy, 16 no stores)
-        bool utf8;
-        uint64_t wout;
-        uint32_t wlen, rb;
-        const MDSX_L uint8_t* mp;
-        if constexpr ((kV & 1) != 0) {
-          const RowsDesc d = s_desc[c];
-          utf8 = d.utf8 != 0;
-          wout = d.wout;
-          wlen = d.wlen;
-          rb = d.rb;
-          mp = T.map + size_t(d.vi) * map_len;
-        } else {
-          const MDSX_L DevCol& col = cols[c];
-          utf8 = col.kind == MDSX_KIND_STR && col.flags != nullptr && !(a.stage_debug & 1);
-          wout = reinterpret_cast<uint64_t>(col.data) + s_wbase[c];
-          wlen = s_wlen[c];
-          rb = col.var_index >= 0 ? 0u : col.row_bytes;
-          mp = T.map + size_t(col.var_index >= 0 ? col.var_index : 0) * map_len;
-        }
+        const RowsDesc d = s_desc[c];
+        const bool utf8 = d.utf8 != 0;
+        const uint64_t wout = d.wout;
+        const uint32_t wlen = d.wlen, rb = d.rb;
+        const MDSX_L uint8_t* mp = T.map + size_t(d.vi) * map_len;
         const uint64_t D0 = wout & ~uint64_t(15);
         const int32_t hd = int32_t(wout - D0);
         MDSX_L uint32_t* bad = T.bad + c * 8;
@@ -713,15 +543,12 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
           const int32_t P0 = int32_t(k * 16) - hd;  // window output byte of the chunk's byte 0
           int32_t pos = max(P0, 0);
           const int32_t end = min(P0 + 16, int32_t(wlen));
-          const int r = rb ? ga + int(uint32_t(pos) / rb) : early_map ? int(m_early) : int(mp[k]);
+          const int r = rb ? ga + int(uint32_t(pos) / rb) : int(mp[k]);
           // the common chunk: one value (A) or two (A, then B from byte sB), straight-line
           const RowsRec qa = T.rec[base + r];
           const int32_t dsA = int32_t(qa.dst), deA = dsA + int32_t(qa.len);
           const lds_u8* pa = stage + (int32_t(qa.src) - dsA + P0);
           uint4 val = lds_read16(pa);
-          // (kV bit 4) the dword before the chunk's first byte of A, with the chunk (the read may
-          // start up to 19 bytes before the stage: kStageFront)
-          const uint32_t pw_early = ((kV & 4) != 0 && utf8) ? lds_u32(pa + (pos - P0) - 4) : 0u;
           const int32_t hiA = min(end, deA);
           bool simple = deA > pos;  // (a fixed column's failed sample: no bytes)
           uint32_t sB = 16;
@@ -749,7 +576,7 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
                                   : val;
               uint32_t pw = 0;
               if (pos > dsA) {
-                pw = (kV & 4) ? pw_early : lds_u32(pa + (pos - P0) - 4);
+                pw = lds_u32(pa + (pos - P0) - 4);
                 const int32_t nv = pos - dsA;  // A's bytes before the chunk
                 if (nv < 4) pw &= ~((1u << (8 * (4 - nv))) - 1u);
               }
@@ -758,25 +585,14 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
               // (measurement knob sdbg 32: always check)
               const bool plain = (((X.x | X.y | X.z | X.w) & 0x80808080u) | hi_c0(pw)) == 0;
               if (!__all(plain) || (a.stage_debug & 32)) {
-                // kV bit 2: the chunk as one stream, A's end and the chunk's last value's end
-                // checked for an open sequence; only a chunk failing that takes the two-value
-                // check, which says whose the error is (utf8_chunk_err1)
-                bool exact = true;
-                if constexpr ((kV & 2) != 0) {
-                  exact = utf8_chunk_err1(X, pw) != 0;
-                  if (sB < 16) exact |= utf8_open_at(X, pw, sB);
-                  if (end == P0 + 16 && end == deL) exact |= utf8_open_at(X, pw, 16);
+                uint32_t e = utf8_chunk_err2(X, pw, sB);
+                if (sB < 16 && utf8_open_at(X, pw, sB)) e |= 1u;
+                if (end == P0 + 16 && end == deL) {
+                  if (sB < 16) e |= utf8_open_at(keep_bytes(X, sB, 16), 0, 16) ? 2u : 0u;
+                  else e |= utf8_open_at(X, pw, 16) ? 1u : 0u;
                 }
-                if (exact) {
-                  uint32_t e = utf8_chunk_err2(X, pw, sB);
-                  if (sB < 16 && utf8_open_at(X, pw, sB)) e |= 1u;
-                  if (end == P0 + 16 && end == deL) {
-                    if (sB < 16) e |= utf8_open_at(keep_bytes(X, sB, 16), 0, 16) ? 2u : 0u;
-                    else e |= utf8_open_at(X, pw, 16) ? 1u : 0u;
-                  }
-                  if (e & 1u) atomicOr(&bad[r >> 5], 1u << (r & 31));
-                  if (e & 2u) atomicOr(&bad[(r + 1) >> 5], 1u << ((r + 1) & 31));
-                }
+                if (e & 1u) atomicOr(&bad[r >> 5], 1u << (r & 31));
+                if (e & 2u) atomicOr(&bad[(r + 1) >> 5], 1u << ((r + 1) & 31));
               }
             }
           } else {
@@ -903,45 +719,6 @@ int launch_rows_decode(const mdsx_plan* plan, const DevArgs& a, hipStream_t s) {
     mdsx::set_last_kernel("rows_decode_kernel<true, false, true>");
     hipLaunchKernelGGL((rows_decode_kernel<true, false, true>), dim3(a.ntiles), dim3(kRowsBlock),
                        lds, s, a);
-  } else if (occ == 6 && nt && !pipe && plan->rows_var != 0) {
-    // the write loop's variants (kV), registers bounded for six waves per SIMD
-#define MDSX_ROWS_VAR(V)                                                                          \
-  if (plan->rows_var == V) {                                                                      \
-    const void* fn =                                                                              \
-        reinterpret_cast<const void*>(rows_decode_kernel<true, false, false, false, 6, true, V>);  \
-    if (lds > 64 * 1024) {                                                                        \
-      rc = hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)), \
-                     "hipFuncSetAttribute");                                                      \
-      if (rc != MDSX_OK) return rc;                                                               \
-    }                                                                                             \
-    mdsx::set_last_kernel("rows_decode_kernel<true, false, false, false, 6, true, " #V ">");        \
-    hipLaunchKernelGGL((rows_decode_kernel<true, false, false, false, 6, true, V>), dim3(a.ntiles), \
-                       dim3(kRowsBlock), lds, s, a);                                              \
-  } else
-    MDSX_ROWS_VAR(1) MDSX_ROWS_VAR(3) MDSX_ROWS_VAR(5) MDSX_ROWS_VAR(9) MDSX_ROWS_VAR(13)
-    MDSX_ROWS_VAR(15) MDSX_ROWS_VAR(17)
-    return mdsx::fail(MDSX_E_ARG, "mdsx: rows variant (rv) of 1, 3, 5, 9, 13, 15 or 17");
-#undef MDSX_ROWS_VAR
-  } else if (occ == 5 && nt && !pipe && (plan->rows_var == 1 || plan->rows_var == 17)) {
-    // (measurement: registers bounded for five waves per SIMD)
-    const bool two = plan->rows_var == 17;
-    const void* fn =
-        two ? reinterpret_cast<const void*>(rows_decode_kernel<true, false, false, false, 5, true, 17>)
-            : reinterpret_cast<const void*>(rows_decode_kernel<true, false, false, false, 5, true, 1>);
-    if (lds > 64 * 1024) {
-      rc = hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)),
-                     "hipFuncSetAttribute");
-      if (rc != MDSX_OK) return rc;
-    }
-    if (two) {
-      mdsx::set_last_kernel("rows_decode_kernel<true, false, false, false, 5, true, 17>");
-      hipLaunchKernelGGL((rows_decode_kernel<true, false, false, false, 5, true, 17>),
-                         dim3(a.ntiles), dim3(kRowsBlock), lds, s, a);
-    } else {
-      mdsx::set_last_kernel("rows_decode_kernel<true, false, false, false, 5, true, 1>");
-      hipLaunchKernelGGL((rows_decode_kernel<true, false, false, false, 5, true, 1>),
-                         dim3(a.ntiles), dim3(kRowsBlock), lds, s, a);
-    }
   } else if ((occ == 6 || occ == 8) && nt && !pipe) {
     const void* fn = occ == 6
                          ? reinterpret_cast<const void*>(rows_decode_kernel<true, false, false, false, 6>)

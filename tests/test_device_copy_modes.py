@@ -78,12 +78,6 @@ MODES = {
     'rows_pipe_one': 'rows=8,rpipe=1,rmin=1000000000',  # one tile per workgroup, two stages
     'rows_occ6': 'rows=-1,rocc=6,rmin=1000000000',  # registers bounded for six waves per SIMD
     'rows_occ8': 'rows=12,rocc=8,rmin=1000000000',  # ... eight, smaller tiles
-    # the write loop's variants (mdsx_rows.hip kV): column descriptors, one-stream UTF-8 check
-    'rows_rv1': 'rows=-1,rv=1,rmin=1000000000',
-    'rows_rv17': 'rows=-1,rv=17,rmin=1000000000',
-    'rows_small_rv17': 'rows=2,rv=17,rmin=1000000000',
-    'rows_rv15': 'rows=-1,rv=15,rmin=1000000000',
-    'rows_small_rv15': 'rows=2,rv=15,rmin=1000000000',  # ... with windows and HBM-direct samples
     # it lists; a 6 KiB ring (4 KiB windows) with small tiles and a 2 KiB fallback stage
     'gather': 'run=0,rows=0,gmin=1000000000',
     'group': 'run=0,rows=0,gmin=0,gmax=1000000000',

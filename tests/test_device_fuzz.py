@@ -37,10 +37,6 @@ MODES = {
     'swave4': 'swave=1,rmin=0,swkb=4,swtile=2',
     'rows_small': 'rows=2,rmin=1000000000',  # row-parallel, 2 KiB stage (windows, huge rows)
     'rows_pipe': 'rows=4,rpipe=5,rmin=1000000000',  # ... two stages, next tile's DMA in flight
-    'rows_rv15': 'rows=-1,rv=15,rmin=1000000000',  # write-loop variants (descriptors, UTF-8)
-    'rows_small_rv15': 'rows=2,rv=15,rmin=1000000000',
-    'rows_rv17': 'rows=-1,rv=17,rmin=1000000000',
-    'rows_small_rv17': 'rows=2,rv=17,rmin=1000000000',
     'register': 'run=0,rows=0',  # the register decode (+ gather / groups per column)
     'rowwave': 'rw=1,lpad=12',  # all-fixed plans: one row per wave (others: as the default)
 }
