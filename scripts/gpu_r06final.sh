@@ -6,10 +6,15 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/${TAG:-r06final}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+# PART: all (default), tests (suite + smoke only) or bench (bench lines + profiles only)
+PART=${PART:-all}
+if [ "$PART" != bench ]; then
 timeout -k 10 900 python3 -u -m pytest tests -m gpu --maxfail=20 -q --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 || { tail -40 "$OUT/pytest_gpu.log"; exit 1; }
 tail -2 "$OUT/pytest_gpu.log"
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { tail -30 "$OUT/smoke.log"; exit 1; }
 cat "$OUT/smoke.log"
+fi
+[ "$PART" = tests ] && exit 0
 for i in 1 2; do
   timeout -k 10 600 python3 bench.py > "$OUT/bench$i.json" 2> "$OUT/bench$i.err" || { tail -30 "$OUT/bench$i.err"; exit 1; }
   python3 - "$OUT/bench$i.json" <<'PY'
