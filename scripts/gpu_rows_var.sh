@@ -1,7 +1,9 @@
 #!/bin/bash
-# Row-parallel decode's write-loop variants (MDSX_TUNE rv, mdsx_rows.hip kV): their GPU parity
-# tests, then an in-process A/B on short ragged rows (scripts/tune_decode.py) against the default.
-# Output under gpurun_out/$TAG/. TESTS: pytest targets ('' skips); VARIANTS: tune_decode variants.
+# Short ragged rows through the row-parallel decode: optional GPU parity tests, then an
+# in-process A/B (scripts/tune_decode.py) of MDSX_TUNE variants against the default. Round 6 ran
+# it on the write-loop variants (MDSX_TUNE rv, mdsx_rows.hip kV, at the commit that held them)
+# and on the UTF-8 ablations (profiles/r06/rows_var/). Output under gpurun_out/$TAG/.
+# TESTS: pytest targets ('' skips); VARIANTS: tune_decode variants.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 TAG=${TAG:-rows_var}
