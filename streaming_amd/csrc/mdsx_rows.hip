@@ -617,8 +617,13 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
                   const int32_t nv = lo - ds;
                   if (nv < 4) pw &= ~((1u << (8 * (4 - nv))) - 1u);
                 }
-                if ((utf8_chunk_err2(pv, pw, 16) & 1u) ||
-                    (hi == de && hi == P0 + 16 && utf8_open_at(pv, pw, 16)))
+                // an ASCII piece after no lead byte cannot err nor end a sequence open (the
+                // simple path's `plain`, per lane here; measurement knob sdbg 16384: always check)
+                const bool ascii =
+                    (((pv.x | pv.y | pv.z | pv.w) & 0x80808080u) | hi_c0(pw)) == 0 &&
+                    !(a.stage_debug & 16384);
+                if (!ascii && ((utf8_chunk_err2(pv, pw, 16) & 1u) ||
+                               (hi == de && hi == P0 + 16 && utf8_open_at(pv, pw, 16))))
                   atomicOr(&bad[rr >> 5], 1u << (rr & 31));
               }
               pos = hi;

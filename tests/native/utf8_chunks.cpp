@@ -163,7 +163,10 @@ static std::vector<bool> run_chunks(const std::vector<std::vector<uint8_t>>& V, 
         const int lo = std::max(pos, d0), hi = std::min(end, d1);
         const uint4 pv = keep_bytes(val, lo - P0, hi - P0);
         const uint32_t pw = lo > d0 ? dword_before(st, 32 + lo, 32 + d0) : 0u;
-        if ((utf8_chunk_err2(pv, pw, 16) & 1) || (hi == d1 && hi == P0 + 16 && utf8_open_at(pv, pw, 16)))
+        // (an ASCII piece after no lead byte is skipped, as the kernel does)
+        const bool ascii = (((pv.x | pv.y | pv.z | pv.w) & 0x80808080u) | hi_c0(pw)) == 0;
+        if (!ascii && ((utf8_chunk_err2(pv, pw, 16) & 1) ||
+                       (hi == d1 && hi == P0 + 16 && utf8_open_at(pv, pw, 16))))
           bad[rr] = true;
         pos = hi;
       }
