@@ -491,8 +491,10 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
       uint32_t total = 0;
       uint32_t ends[kEnds];
       if constexpr (kFlat) {
+        // (a column with no bytes in the window has no chunks: a misaligned empty window would
+        // otherwise count one, whose chunk-map entry no sample wrote)
         uint32_t cn = 0;
-        if (lane < ncols && !s_skip[lane]) {
+        if (lane < ncols && !s_skip[lane] && s_wlen[lane] != 0) {
           const uint64_t w = reinterpret_cast<uint64_t>(cols[lane].data) + s_wbase[lane];
           cn = uint32_t(((w & 15) + s_wlen[lane] + 15) >> 4);
         }
@@ -506,7 +508,7 @@ __global__ __launch_bounds__(kRowsBlock, kOcc) void rows_decode_kernel(const Dev
       for (int cl = 0; cl < (kFlat ? 1 : ncols); ++cl) {
         if (!kFlat && s_skip[cl]) continue;  // block-uniform
         const uint32_t kend = kFlat ? total
-                                    : (a.stage_debug & 2) ? 0u
+                                    : (a.stage_debug & 2) || s_wlen[cl] == 0 ? 0u
                                     : uint32_t(((((reinterpret_cast<uint64_t>(cols[cl].data) +
                                                    s_wbase[cl]) & 15) + s_wlen[cl] + 15) >> 4));
         for (uint32_t kw = uint32_t(t); kw < kend; kw += kRowsBlock) {

@@ -74,11 +74,12 @@ static void gen_raw(uint8_t* s, int n) {
   for (int i = 0; i < n; ++i) s[i] = (rng() & 3) ? kPool[rng() % sizeof(kPool)] : uint8_t(rng());
 }
 
-// Well-formed text (1- to 4-byte code points, cut at n bytes), one bad byte a third of the time.
-static void gen_text(uint8_t* s, int n) {
+// Well-formed text (1- to `widths`-byte code points, cut at n bytes), one bad byte a third of
+// the time.
+static void gen_text(uint8_t* s, int n, int widths = 4) {
   int i = 0;
   while (i < n) {
-    const int w = rng() % 4;
+    const int w = rng() % widths;
     uint32_t cp;
     if (w == 0) cp = 0x20 + rng() % 95;
     else if (w == 1) cp = 0x80 + rng() % 0x780;
@@ -127,7 +128,7 @@ static std::vector<bool> run_chunks(const std::vector<std::vector<uint8_t>>& V, 
     memcpy(&v, st.data() + 32 + at, 16);
     return v;
   };
-  for (int k = 0; k * 16 < hd + wlen; ++k) {
+  for (int k = 0; wlen > 0 && k * 16 < hd + wlen; ++k) {  // (no chunks when no bytes, as the kernel)
     const int P0 = 16 * k - hd, end = std::min(P0 + 16, wlen);
     int pos = std::max(P0, 0);
     int r = 0;  // the chunk map: the value holding byte pos
@@ -183,7 +184,11 @@ int main(int argc, char** argv) {
     for (size_t i = 0; i < V.size(); ++i) {
       const int n = (rng() % 5 == 0) ? rng() % 4 : 1 + rng() % 40;  // some empty and tiny values
       V[i].resize(n);
-      if (n) ((it + i) & 1) ? gen_raw(V[i].data(), n) : gen_text(V[i].data(), n);
+      if (n) {
+        const int kind = int((it + i) % 3);
+        kind == 0 ? gen_raw(V[i].data(), n) : kind == 1 ? gen_text(V[i].data(), n)
+                                                      : gen_text(V[i].data(), n, 2);
+      }
     }
     const int hd = rng() % 16;
     const std::vector<bool> bad = run_chunks(V, hd);

@@ -30,7 +30,7 @@ def _device_code() -> str:
     h = DEVICE_H.read_text()
     parts = [
         _section(h, '// 0xFF in byte i of the result', '// Bytes [a, b) (0 <= a <= b <= 16) of `val`'),
-        _section(h, '__device__ __forceinline__ uint32_t hi_c0', '__device__ __forceinline__ uint32_t zero_bytes'),
+        _section(h, '__device__ __forceinline__ uint32_t hi_c0', '// Error bits of dword x'),
         _section(h, '// ---- The same check by nibble tables', '// Bytes of a 16-byte chunk at address D'),
     ]
     return '\n'.join(parts)
